@@ -1,0 +1,347 @@
+#!/usr/bin/env python3
+"""Benchmark of the Bitmessage double-SHA-512 PoW hot path on MI355X (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c1|c3|c4|c5]
+
+Default workload (N=1): BASELINE config C2 -- a batch of 1,024 pending msg objects,
+payload sizes L ~ U[512, 16384] drawn with payloads from random.Random(20250216 + rank),
+default difficulty (ntpb = extra = 1000), TTL = 345600 s, solved to the exact
+_doSafePoW answer through the batch session of libbmpow_hip.so (the engine behind
+proofofwork.run_batch).  One "step" = solving the whole batch from nonce 1.  The object
+table is uploaded before the timed region (inputs resident in HBM); each step resets the
+per-object state on the device (bmpow_batch_reset) and runs scheduler steps to completion.
+
+Multi-GPU (torch.distributed.run, one process per GPU): each rank drives its own GPU
+(LOCAL_RANK) on its own 1,024-object batch (seed + rank): units are independent, so the
+batch is sharded with no data-path collective ("scaling": "weak").  gloo carries only the
+timing barrier and the max-over-ranks / sum-over-ranks reductions.
+
+value = useful double-SHA-512 trials per second over the whole job (sum over objects of the
+found nonce, i.e. the trials the sequential _doSafePoW would need -- the reference's own
+nonce/time convention -- divided by the max-over-ranks wall time), in GH/s.  Trials the
+kernels actually hashed (incl. the work past a hit that the early exit did not cancel) are
+reported beside it.
+"""
+import argparse
+import hashlib
+import json
+import os
+import random
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "double-SHA512 PoW trials/sec (GH/s, node) at 1/2/4/8 GPUs; objects PoW'd/sec"
+SEED = 20250216
+#: algorithmic int32 lane-ops per trial: 2 blocks x (80 x 34 + 64 x 22 + 16)
+OPS_PER_TRIAL = 8288
+#: integer VALU peak, T lane-ops/s: 256 CUs x 64 lane-ops/clk (the VOP3-class issue rate of
+#: v_alignbit_b32 / v_lshl_add_u64 / v_bfi_b32, measured 38.7 T by tools/ubench_valu.hip) x 2.4 GHz
+PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
+
+
+def object_target(L, ttl, ntpb=1000, extra=1000):
+    from pybitmessage_amd.targets import object_target as f
+    return int(f(L, ttl, ntpb, extra))
+
+
+def make_objects(config, rank, n_override=None):
+    """-> (objects [(target, ih)], workload description)."""
+    rng = random.Random(SEED + rank)
+    objs = []
+    if config == 'c2':
+        n = n_override or 1024
+        for _ in range(n):
+            L = rng.randrange(512, 16385)
+            payload = rng.randbytes(L)
+            objs.append((object_target(L, 345600), hashlib.sha512(payload).digest()))
+        desc = ('C2: %d pending msg objects, L~U[512,16384], ntpb=extra=1000, TTL=345600 s, '
+                'exact first nonce via the batch session' % n)
+    elif config == 'c4':
+        n = n_override or 64
+        for _ in range(n):
+            payload = rng.randbytes(1024)
+            objs.append((object_target(1024, 2419200, 20000, 1000), hashlib.sha512(payload).digest()))
+        desc = 'C4: %d objects L=1024 at 20x ntpb (20000), TTL=28 d' % n
+    elif config == 'c5':
+        n = n_override or 100000
+        for i in range(n):
+            if i % 2 == 0:
+                payload = rng.randbytes(46)
+                objs.append((object_target(46, 2419200), hashlib.sha512(payload).digest()))
+            else:
+                payload = rng.randbytes(200)
+                objs.append((object_target(200, 345600), hashlib.sha512(payload).digest()))
+        desc = 'C5: %d objects, 50%% acks (L=46, TTL=28 d) + 50%% pubkey-size (L=200, TTL=4 d)' % n
+    else:
+        raise ValueError(config)
+    return objs, desc
+
+
+# ----------------------------------------------------------------------------------------
+# distributed plumbing (timing only; no data-path collective)
+# ----------------------------------------------------------------------------------------
+class Dist(object):
+    def __init__(self):
+        self.world = int(os.environ.get('WORLD_SIZE', '1'))
+        self.rank = int(os.environ.get('RANK', '0'))
+        self.local_rank = int(os.environ.get('LOCAL_RANK', '0'))
+        self.dist = None
+        if self.world > 1:
+            import torch.distributed as dist
+            os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+            dist.init_process_group('gloo', rank=self.rank, world_size=self.world)
+            self.dist = dist
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def reduce(self, value, op):
+        if not self.dist:
+            return value
+        import torch
+        t = torch.tensor([float(value)], dtype=torch.float64)
+        self.dist.all_reduce(t, op={'max': self.dist.ReduceOp.MAX, 'sum': self.dist.ReduceOp.SUM}[op])
+        return float(t.item())
+
+    def close(self):
+        if self.dist:
+            self.dist.destroy_process_group()
+
+
+# ----------------------------------------------------------------------------------------
+# GPU legs
+# ----------------------------------------------------------------------------------------
+def solve_batch(lib, h, budget=0):
+    from pybitmessage_amd import _lib
+    _lib.check(lib, lib.bmpow_batch_reset(h, None), 'bmpow_batch_reset')
+    pending = 1
+    while pending > 0:
+        pending = _lib.check(lib, lib.bmpow_batch_step(h, budget), 'bmpow_batch_step')
+
+
+def run_batch_bench(args, dist):
+    import ctypes
+
+    import numpy as np
+
+    from pybitmessage_amd import _lib, proofofwork
+    objs, desc = make_objects(args.config, dist.rank, args.objects)
+    lib = _lib.get()
+    n = len(objs)
+    ihs = b''.join(ih for _, ih in objs)
+    tg = np.array([t for t, _ in objs], dtype=np.uint64)
+    p64 = ctypes.POINTER(ctypes.c_uint64)
+    h = lib.bmpow_batch_create(n, ihs, tg.ctypes.data_as(p64), None)
+    if not h:
+        raise RuntimeError('bmpow_batch_create: %s' % lib.bmpow_last_error().decode())
+    try:
+        for _ in range(args.warmup):
+            solve_batch(lib, h)
+        dist.barrier()
+        lib.bmpow_reset_stats()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            solve_batch(lib, h)
+        dist.barrier()
+        elapsed = time.perf_counter() - t0
+        st = _lib.BmpowStats()
+        lib.bmpow_get_stats(ctypes.byref(st))
+        nonce = np.zeros(n, dtype=np.uint64)
+        trial = np.zeros(n, dtype=np.uint64)
+        done = np.zeros(n, dtype=np.uint8)
+        lib.bmpow_batch_results(h, nonce.ctypes.data_as(p64), trial.ctypes.data_as(p64),
+                                done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), None)
+    finally:
+        lib.bmpow_batch_destroy(h)
+    # every answer re-checked on the host: trial(nonce) <= target with hashlib
+    assert (done == _lib.DONE_FOUND).all()
+    for i in range(n):
+        proofofwork._verify(int(tg[i]), objs[i][1], int(trial[i]), int(nonce[i]))
+    useful = float(nonce.astype(np.float64).sum()) * args.steps
+    return {'desc': desc, 'objects': n * args.steps, 'useful': useful, 'elapsed': elapsed, 'stats': st,
+            'nonces_sum': int(nonce.astype(object).sum())}
+
+
+def run_c3_bench(args, dist):
+    """C3: fixed initialHash, target 0 (no hit), 2^log2 nonces split contiguously over ranks."""
+    import ctypes
+
+    from pybitmessage_amd import _lib
+    lib = _lib.get()
+    ih = hashlib.sha512(b'bmpow-sweep').digest()
+    total = 1 << args.c3_log2
+    share = total // dist.world
+    start = 1 + dist.rank * share
+    n, t = ctypes.c_uint64(), ctypes.c_uint64()
+
+    def sweep():
+        rc = _lib.check(lib, lib.bmpow_search(ih, 0, start, share, ctypes.byref(n), ctypes.byref(t)), 'search')
+        assert rc == _lib.NOT_FOUND
+    for _ in range(args.warmup):
+        sweep()
+    dist.barrier()
+    lib.bmpow_reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        sweep()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = _lib.BmpowStats()
+    lib.bmpow_get_stats(ctypes.byref(st))
+    desc = 'C3: fixed initialHash, target=0, 2^%d nonces split over %d GPU(s)' % (args.c3_log2, dist.world)
+    return {'desc': desc, 'objects': 0, 'useful': float(share) * args.steps, 'elapsed': elapsed, 'stats': st,
+            'scaling': 'strong'}
+
+
+def run_c1_bench(args, dist):
+    import ctypes
+
+    from pybitmessage_amd import _lib, proofofwork
+    lib = _lib.get()
+    payload = random.Random(SEED).randbytes(1024)
+    ih = hashlib.sha512(payload).digest()
+    target = object_target(1024, 345600)
+    for _ in range(args.warmup):
+        proofofwork.run(target, ih)
+    lib.bmpow_reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        tv, nonce = proofofwork.run(target, ih)
+    elapsed = time.perf_counter() - t0
+    assert nonce == 10909138, nonce
+    st = _lib.BmpowStats()
+    lib.bmpow_get_stats(ctypes.byref(st))
+    return {'desc': 'C1: one 1 KB msg at defaults via proofofwork.run (golden nonce 10909138)',
+            'objects': args.steps, 'useful': float(nonce) * args.steps, 'elapsed': elapsed, 'stats': st}
+
+
+# ----------------------------------------------------------------------------------------
+# CPU baseline (rank 0, N=1): the reference's own BitmessagePOW built from its source
+# ----------------------------------------------------------------------------------------
+def cpu_baseline_worker(seconds, threads):
+    """Runs in a child process pinned to `threads` CPUs (BitmessagePOW sizes its pool from the
+    affinity mask, bitmsghash.cpp:96,109-121).  Solves C2 objects in order until `seconds`
+    elapse; rate = sum(nonce) / time, the reference's nonce/time convention."""
+    cpus = sorted(os.sched_getaffinity(0))[:threads]
+    os.sched_setaffinity(0, cpus)
+    from oracle import oracle
+    objs, _ = make_objects('c2', 0, 64)
+    if oracle.have_ref():
+        ref = oracle.RefBitmsghash()
+        kind = 'reference'
+        solve = lambda t, ih: ref.pow(t, ih)[1]  # noqa: E731
+    else:
+        co = oracle.COracle()
+        kind = 'port'
+        solve = lambda t, ih: co.search_mt(ih, t, 1, 1 << 40, threads=len(cpus))[0][1]  # noqa: E731
+    t0 = time.perf_counter()
+    total, k = 0, 0
+    for t, ih in objs:
+        total += solve(t, ih)
+        k += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    el = time.perf_counter() - t0
+    print(json.dumps({'kind': kind, 'cores': len(cpus), 'objects': k, 'nonce_sum': total, 'seconds': el}))
+
+
+def cpu_baseline(seconds, threads):
+    cmd = [sys.executable, os.path.abspath(__file__), '--cpu-baseline-worker', '--cpu-seconds', str(seconds),
+           '--cpu-threads', str(threads)]
+    env = dict(os.environ)
+    env['HIP_VISIBLE_DEVICES'] = ''  # the baseline never touches the GPU
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds * 10 + 120, env=env)
+    line = [l for l in out.stdout.splitlines() if l.startswith('{')]
+    if out.returncode != 0 or not line:
+        return {'error': (out.stderr or out.stdout)[-400:]}
+    r = json.loads(line[-1])
+    rate = r['nonce_sum'] / r['seconds']
+    lib = 'oracle/_ref/bitmsghash.so (reference BitmessagePOW, OpenSSL SHA512, pthreads)' \
+        if r['kind'] == 'reference' else 'oracle/liboracle.so bmo_search_mt'
+    return {'value': rate / 1e9, 'unit': 'GH/s', 'cores': r['cores'], 'kind': r['kind'],
+            'objects_per_s': r['objects'] / r['seconds'],
+            'sample': '%d C2 objects (first of the rank-0 batch) solved in %.1f s by %s on %d host threads; '
+                      'rate = sum(nonce)/time' % (r['objects'], r['seconds'], lib, r['cores'])}
+
+
+# ----------------------------------------------------------------------------------------
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--config', default='c2', choices=['c1', 'c2', 'c3', 'c4', 'c5'])
+    ap.add_argument('--objects', type=int, default=None, help='override the object count (c2/c4/c5)')
+    ap.add_argument('--c3-log2', type=int, default=36)
+    ap.add_argument('--step-trials', type=int, default=0, help='per-launch trial budget per GPU (0 = lib default)')
+    ap.add_argument('--cpu-seconds', type=float, default=12.0)
+    ap.add_argument('--cpu-threads', type=int, default=16)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-baseline-worker', action='store_true', help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.cpu_baseline_worker:
+        cpu_baseline_worker(args.cpu_seconds, args.cpu_threads)
+        return
+
+    dist = Dist()
+    os.environ['BMPOW_DEVICES'] = str(dist.local_rank)  # one process per GPU
+    from pybitmessage_amd import _lib
+    lib = _lib.get()
+    if args.step_trials:
+        lib.bmpow_set_step_trials(args.step_trials)
+
+    runner = {'c1': run_c1_bench, 'c2': run_batch_bench, 'c3': run_c3_bench, 'c4': run_batch_bench,
+              'c5': run_batch_bench}[args.config]
+    r = runner(args, dist)
+    st = r['stats']
+    el_max = dist.reduce(r['elapsed'], 'max')
+    useful = dist.reduce(r['useful'], 'sum')
+    objects = dist.reduce(r['objects'], 'sum')
+    performed = dist.reduce(st.trials, 'sum')
+    kernel_ms = st.kernel_ms
+    launches = st.launches
+    line = {
+        'metric': METRIC,
+        'value': round(useful / el_max / 1e9, 4),
+        'unit': 'GH/s',
+        'n_gpus': dist.world,
+        'steps': args.steps,
+        'warmup': args.warmup,
+        'ms_per_step': round(el_max * 1e3 / args.steps, 2),
+        'higher_is_better': True,
+        'scaling': r.get('scaling', 'weak'),
+        'vs_baseline': None,
+        'dtype': 'u64',
+        'data': 'synthetic',
+        'config': {'workload': r['desc'], 'objects_per_rank_per_step': r['objects'] // max(args.steps, 1),
+                   'parallelism': 'object-sharded dp%d (one process per GPU, no collective)' % dist.world,
+                   'block': 256, 'lib': lib.bmpow_version().decode()},
+        'objects_per_s': round(objects / el_max, 3),
+        'performed_ghs': round(performed / el_max / 1e9, 4),
+        'wasted_frac': round(1.0 - useful / performed, 5) if performed else None,
+    }
+    if kernel_ms > 0:
+        achieved = OPS_PER_TRIAL * st.trials / (kernel_ms * 1e-3) / 1e12
+        line['roofline'] = {
+            'bound': 'valu', 'kernel': 'bm_search_kernel',
+            'achieved': round(achieved, 3), 'peak': round(PEAK_TOPS, 3),
+            'unit': 'T int32 lane-ops/s (8,288 algorithmic ops per trial)',
+            'frac': round(achieved / PEAK_TOPS, 4), 'traffic': None,
+            'kernel_ghs': round(st.trials / (kernel_ms * 1e-3) / 1e9, 4),
+            'avg_launch_ms': round(kernel_ms / max(launches, 1), 3), 'launches': int(launches),
+            'kernel_busy_frac': round(kernel_ms * 1e-3 / r['elapsed'], 4),
+        }
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+        line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_threads)
+    if dist.rank == 0:
+        print(json.dumps(line), flush=True)
+    dist.close()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,155 @@
+/*
+ * bmpow.h -- C ABI of libbmpow_hip.so, the MI355X proof-of-work engine for PyBitmessage.
+ *
+ * Drop-in boundary for the reference's native PoW.  Plain pointers and
+ * sizes only; loaded from Python with ctypes.CDLL exactly like the reference loads
+ * bitmsghash.so (src/proofofwork.py:371-388).
+ *
+ * Semantics of every search entry point (the _doSafePoW contract,
+ * src/proofofwork.py:100-111):
+ *     trial(n, ih) = BE64(SHA512(SHA512(BE64(n) || ih))[0:8])
+ *     answer       = min { n >= start : trial(n, ih) <= target }
+ * Searches are BOUNDED (a trial budget per call) so the caller can poll its shutdown flag
+ * between calls -- the pattern of dev/powinterrupttest.py:22-37 -- and bmpow_abort() stops
+ * an in-flight call from another thread or a signal handler.
+ *
+ * Return codes: >= 0 success (meaning per function), < 0 error (BMPOW_E_*);
+ * bmpow_last_error() describes the last error of the calling thread.
+ *
+ * Thread safety: all entry points may be called from any thread; searches are serialised
+ * by an internal mutex (one search in flight per process), the GIL is not needed.
+ */
+#ifndef BMPOW_H
+#define BMPOW_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__GNUC__) || defined(__clang__)
+#define BMPOW_API __attribute__((visibility("default")))
+#else
+#define BMPOW_API
+#endif
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BMPOW_ABI_VERSION 1
+
+#define BMPOW_NOT_FOUND 0      /* budget exhausted, no hit: resume at start + trials */
+#define BMPOW_FOUND 1          /* *nonce_out / *trial_out hold the exact first hit */
+#define BMPOW_E_NODEV (-1)     /* no usable gfx950 device / HIP runtime failure at init */
+#define BMPOW_E_HIP (-2)       /* HIP runtime error during a call */
+#define BMPOW_E_ARG (-3)       /* invalid argument */
+#define BMPOW_E_ABORTED (-4)   /* bmpow_abort() was called; nothing returned is final */
+#define BMPOW_E_STATE (-5)     /* library not initialised / handle misuse */
+
+/* Object state in bmpow_batch_results()/bmpow_search_batch() `done` arrays. */
+#define BMPOW_PENDING 0
+#define BMPOW_DONE_FOUND 1
+#define BMPOW_DONE_EXHAUSTED 2 /* reached nonce 2^64-1 without a hit */
+
+/* ---- lifecycle (replaces proofofwork.init / bmpow global, src/proofofwork.py:336-394) ---- */
+
+/* Initialise the HIP runtime and select every visible gfx950 device (or those named by the
+ * BMPOW_DEVICES env var, e.g. "0,1").  Idempotent.  Returns the number of devices in use
+ * (> 0) or BMPOW_E_NODEV. */
+BMPOW_API int bmpow_init(void);
+
+/* Number of gfx950 devices visible to the process (>= 0), without selecting them. */
+BMPOW_API int bmpow_device_count(void);
+
+/* Use exactly these device ordinals for subsequent searches (n >= 1).  A device may be
+ * listed more than once: each entry is a separate nonce shard with its own stream.
+ * n == 0 selects every visible device.  Returns the number of shards or < 0. */
+BMPOW_API int bmpow_set_devices(const int *ids, int n);
+
+/* Copy the active shard -> device map into ids[0..cap); returns the shard count. */
+BMPOW_API int bmpow_get_devices(int *ids, int cap);
+
+/* Release all device memory and streams (bmpow_init may be called again). */
+BMPOW_API void bmpow_shutdown(void);
+
+BMPOW_API const char *bmpow_last_error(void);
+BMPOW_API const char *bmpow_version(void);
+
+/* ---- interrupt (replaces the dead OpenCL shutdown check, src/openclpow.py:10,99) ---- */
+
+/* Async-signal-safe.  In-flight and later searches return BMPOW_E_ABORTED at their next
+ * step boundary (<= one launch, ~tens of ms) until bmpow_clear_abort(). */
+BMPOW_API void bmpow_abort(void);
+BMPOW_API void bmpow_clear_abort(void);
+
+/* ---- the hot path ---- */
+
+/* trial(nonces[i], ih) for i < n, computed on the first shard's device.
+ * Parity probe for the trial function (reference src/proofofwork.py:106-107). */
+BMPOW_API int bmpow_trials(const uint8_t ih[64], const uint64_t *nonces, size_t n, uint64_t *trials_out);
+
+/* Bounded single-object search of [start, start + max_trials) (never past 2^64-1), nonce
+ * space sharded over the active devices.  Replaces BitmessagePOW
+ * (src/bitmsghash/bitmsghash.cpp:127-165) and do_opencl_pow (src/openclpow.py:77-111).
+ * Returns BMPOW_FOUND with the exact first hit, BMPOW_NOT_FOUND, or < 0. */
+BMPOW_API int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials,
+                 uint64_t *nonce_out, uint64_t *trial_out);
+
+/* Bounded batch search: n objects (ihs: n x 64 bytes, targets: n), each resuming at
+ * next_start[i] (in/out).  Spends about `budget` trials in total, then returns the number
+ * of objects still pending (>= 0) or < 0.  For objects with done[i] = BMPOW_DONE_FOUND,
+ * nonce_out[i]/trial_out[i] are final.  Objects already marked done on entry are skipped,
+ * so calling it in a loop until it returns 0 solves the whole batch (run_batch). */
+BMPOW_API int bmpow_search_batch(size_t n, const uint8_t *ihs, const uint64_t *targets, uint64_t *next_start,
+                       uint64_t budget, uint64_t *nonce_out, uint64_t *trial_out, uint8_t *done);
+
+/* ---- device-resident batch session (the object table stays in HBM across steps) ---- */
+typedef struct bmpow_batch bmpow_batch;
+
+/* Upload n objects; start may be NULL (every object starts at nonce 1). NULL on error. */
+BMPOW_API bmpow_batch *bmpow_batch_create(size_t n, const uint8_t *ihs, const uint64_t *targets,
+                                const uint64_t *start);
+
+/* One bounded step of ~budget trials over the pending objects (0 = library default).
+ * Returns the number of objects still pending (>= 0) or < 0. */
+BMPOW_API int bmpow_batch_step(bmpow_batch *b, uint64_t budget);
+
+/* Copy out per-object state; any pointer may be NULL. Returns the pending count. */
+BMPOW_API int bmpow_batch_results(const bmpow_batch *b, uint64_t *nonce_out, uint64_t *trial_out,
+                        uint8_t *done, uint64_t *next_start);
+
+/* Restart every object at nonce `start` (NULL = 1) without re-uploading the object table
+ * (used by bench.py to time repeated full solves with inputs already resident in HBM). */
+BMPOW_API int bmpow_batch_reset(bmpow_batch *b, const uint64_t *start);
+
+BMPOW_API void bmpow_batch_destroy(bmpow_batch *b);
+
+/* ---- instrumentation (bench.py's roofline leg) ---- */
+typedef struct bmpow_stats {
+    uint64_t launches;        /* search-kernel launches (summed over shards) */
+    uint64_t trials;          /* trials actually hashed by search kernels (device-counted) */
+    double kernel_ms;         /* sum over launches of search-kernel time, HIP events on the
+                                 launching stream */
+    double max_shard_kernel_ms; /* max over shards of their summed kernel time */
+    uint64_t steps;           /* host scheduler steps */
+} bmpow_stats;
+
+BMPOW_API int bmpow_get_stats(bmpow_stats *out);
+BMPOW_API void bmpow_reset_stats(void);
+
+/* Default per-shard trial budget of one step (one kernel launch); settable for tests. */
+BMPOW_API uint64_t bmpow_get_step_trials(void);
+BMPOW_API void bmpow_set_step_trials(uint64_t trials_per_shard);
+
+/* ---- compatibility shim ---- */
+
+/* Same signature as the reference's export (src/bitmsghash/bitmsghash.cpp:127), so an
+ * unmodified _doCPoW (src/proofofwork.py:157-170) can load this library.  Blocks until
+ * found; returns the EXACT first nonce >= 1 with trial <= target (the _doSafePoW answer,
+ * not the racy strict-< answer of the reference C code).  Returns 0 on error/abort. */
+BMPOW_API unsigned long long BitmessagePOW(unsigned char *starthash, unsigned long long target);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BMPOW_H */

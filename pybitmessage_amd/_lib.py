@@ -1,0 +1,134 @@
+"""ctypes binding of ``libbmpow_hip.so`` (C ABI in ``include/bmpow.h``).
+
+Loaded the way the reference loads its native PoW library
+(``src/proofofwork.py:371-388``: ``ctypes.CDLL(codePath/bitmsghash/bitmsghash.so)``), but with
+``argtypes``/``restype`` set for every entry point.  There is no CPU fallback: if the library
+or a gfx950 device is missing, :func:`get` raises :class:`BmpowUnavailable`.
+"""
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+DEFAULT_PATH = os.path.join(HERE, 'lib', 'libbmpow_hip.so')
+
+NOT_FOUND = 0
+FOUND = 1
+E_NODEV = -1
+E_HIP = -2
+E_ARG = -3
+E_ABORTED = -4
+E_STATE = -5
+
+PENDING = 0
+DONE_FOUND = 1
+DONE_EXHAUSTED = 2
+
+U64_MAX = (1 << 64) - 1
+
+
+class BmpowError(RuntimeError):
+    """A libbmpow_hip call failed (HIP error, bad argument, ...)."""
+
+    def __init__(self, code, msg):
+        RuntimeError.__init__(self, '%s (code %d)' % (msg, code))
+        self.code = code
+
+
+class BmpowUnavailable(BmpowError):
+    """The HIP library is not built or no gfx950 device is visible."""
+
+
+class BmpowStats(ctypes.Structure):
+    _fields_ = [('launches', ctypes.c_uint64), ('trials', ctypes.c_uint64),
+                ('kernel_ms', ctypes.c_double), ('max_shard_kernel_ms', ctypes.c_double),
+                ('steps', ctypes.c_uint64)]
+
+
+# (name, restype, argtypes) for every symbol include/bmpow.h declares
+_u64, _p64, _pu8 = ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint8)
+_vp = ctypes.c_void_p
+SIGNATURES = [
+    ('bmpow_init', ctypes.c_int, []),
+    ('bmpow_device_count', ctypes.c_int, []),
+    ('bmpow_set_devices', ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ('bmpow_get_devices', ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ('bmpow_shutdown', None, []),
+    ('bmpow_last_error', ctypes.c_char_p, []),
+    ('bmpow_version', ctypes.c_char_p, []),
+    ('bmpow_abort', None, []),
+    ('bmpow_clear_abort', None, []),
+    ('bmpow_trials', ctypes.c_int, [ctypes.c_char_p, _p64, ctypes.c_size_t, _p64]),
+    ('bmpow_search', ctypes.c_int, [ctypes.c_char_p, _u64, _u64, _u64, _p64, _p64]),
+    ('bmpow_search_batch', ctypes.c_int,
+     [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _u64, _p64, _p64, _pu8]),
+    ('bmpow_batch_create', _vp, [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64]),
+    ('bmpow_batch_step', ctypes.c_int, [_vp, _u64]),
+    ('bmpow_batch_results', ctypes.c_int, [_vp, _p64, _p64, _pu8, _p64]),
+    ('bmpow_batch_reset', ctypes.c_int, [_vp, _p64]),
+    ('bmpow_batch_destroy', None, [_vp]),
+    ('bmpow_get_stats', ctypes.c_int, [ctypes.POINTER(BmpowStats)]),
+    ('bmpow_reset_stats', None, []),
+    ('bmpow_get_step_trials', _u64, []),
+    ('bmpow_set_step_trials', None, [_u64]),
+    ('BitmessagePOW', ctypes.c_ulonglong, [ctypes.c_char_p, ctypes.c_ulonglong]),
+]
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib_path():
+    return os.environ.get('BMPOW_LIB', DEFAULT_PATH)
+
+
+def load(path=None):
+    """dlopen the library and bind every signature (no device access)."""
+    path = path or lib_path()
+    if not os.path.exists(path):
+        raise BmpowUnavailable(E_NODEV, 'libbmpow_hip.so not built at %s (run __graft_entry__.build() '
+                                        'or make -C pybitmessage_amd/csrc)' % path)
+    lib = ctypes.CDLL(path)
+    for name, res, args in SIGNATURES:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def get():
+    """The initialised library (devices selected).  Raises BmpowUnavailable."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            lib = load()
+            rc = lib.bmpow_init()
+            if rc <= 0:
+                raise BmpowUnavailable(rc, 'bmpow_init failed: %s' % lib.bmpow_last_error().decode())
+            _lib = lib
+        return _lib
+
+
+def reset():
+    """Forget the loaded handle's device selection (``resetPoW``)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            _lib.bmpow_shutdown()
+            _lib = None
+
+
+def check(lib, rc, what):
+    if rc < 0:
+        msg = lib.bmpow_last_error().decode(errors='replace')
+        if rc == E_NODEV:
+            raise BmpowUnavailable(rc, '%s: %s' % (what, msg))
+        raise BmpowError(rc, '%s: %s' % (what, msg))
+    return rc
+
+
+def u64_array(values):
+    arr = (ctypes.c_uint64 * len(values))()
+    for i, v in enumerate(values):
+        arr[i] = v
+    return arr

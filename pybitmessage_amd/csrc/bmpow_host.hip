@@ -1,0 +1,667 @@
+// bmpow_host.hip -- C ABI (include/bmpow.h) and host scheduler of libbmpow_hip.so.
+//
+// Replaces the reference's native PoW entry points:
+//   BitmessagePOW          src/bitmsghash/bitmsghash.cpp:127-165  (pthreads + OpenSSL)
+//   do_opencl_pow/initCL   src/openclpow.py:31-111                (pyopencl window loop)
+//
+// Scheduler ("step" = one kernel launch per shard, bounded so the caller can poll its
+// shutdown flag between steps, dev/powinterrupttest.py:22-37):
+//   1. take the pending objects in index order; give each k chunks (k*BM_CHUNK nonces,
+//      contiguous from its next_start) so that the step totals ~budget trials;
+//   2. flatten all windows into one chunk list and cut it into S contiguous slices, one per
+//      shard (device/stream): large objects are nonce-sharded, small ones object-sharded;
+//   3. per shard: upload the item list, launch bm_search_kernel (+ bm_resolve_kernel),
+//      read back per-item {min hit nonce, trial};
+//   4. host min-reduction over shards per object -- the only cross-device exchange (no
+//      RCCL: no data moves between GPUs).  An object with a hit in this step is final
+//      (its whole window below the hit has been hashed); otherwise next_start += window.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/bmpow.h"
+#include "bmpow_kernels.h"
+
+namespace {
+
+constexpr uint64_t kU64Max = ~0ULL;
+constexpr uint64_t kDefaultStepTrials = 1ULL << 28;  // per shard per step, ~40-60 ms on MI355X
+
+thread_local std::string g_err;
+std::mutex g_mu;
+std::atomic<int> g_abort{0};
+uint64_t g_step_trials = kDefaultStepTrials;
+
+int set_err(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPTRY(expr)                                                                            \
+  do {                                                                                          \
+    hipError_t e_ = (expr);                                                                     \
+    if (e_ != hipSuccess)                                                                       \
+      return set_err(BMPOW_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));           \
+  } while (0)
+
+struct Shard {
+  int dev = -1;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // per-step staging (capacity grows)
+  bm_item* d_items = nullptr;
+  bm_result* d_res = nullptr;
+  unsigned long long* d_trials = nullptr;
+  bm_item* h_items = nullptr;      // pinned
+  bm_result* h_res = nullptr;      // pinned
+  unsigned long long* h_trials = nullptr;  // pinned
+  size_t item_cap = 0;
+  // step bookkeeping
+  uint32_t nitems = 0, nchunks = 0;
+  std::vector<uint32_t> item_obj;
+  // stats
+  double kernel_ms = 0.0;
+};
+
+std::vector<Shard> g_shards;
+bool g_inited = false;
+bmpow_stats g_stats{};
+
+int ensure_items(Shard& s, size_t n) {
+  if (n <= s.item_cap) return 0;
+  size_t cap = std::max<size_t>(n, 2 * s.item_cap);
+  HIPTRY(hipSetDevice(s.dev));
+  if (s.d_items) {
+    HIPTRY(hipFree(s.d_items));
+    HIPTRY(hipFree(s.d_res));
+    HIPTRY(hipHostFree(s.h_items));
+    HIPTRY(hipHostFree(s.h_res));
+  }
+  HIPTRY(hipMalloc(&s.d_items, cap * sizeof(bm_item)));
+  HIPTRY(hipMalloc(&s.d_res, cap * sizeof(bm_result)));
+  HIPTRY(hipHostMalloc(&s.h_items, cap * sizeof(bm_item), hipHostMallocDefault));
+  HIPTRY(hipHostMalloc(&s.h_res, cap * sizeof(bm_result), hipHostMallocDefault));
+  s.item_cap = cap;
+  return 0;
+}
+
+void free_shard(Shard& s) {
+  if (s.dev < 0) return;
+  (void)hipSetDevice(s.dev);
+  if (s.d_items) (void)hipFree(s.d_items);
+  if (s.d_res) (void)hipFree(s.d_res);
+  if (s.d_trials) (void)hipFree(s.d_trials);
+  if (s.h_items) (void)hipHostFree(s.h_items);
+  if (s.h_res) (void)hipHostFree(s.h_res);
+  if (s.h_trials) (void)hipHostFree(s.h_trials);
+  if (s.ev0) (void)hipEventDestroy(s.ev0);
+  if (s.ev1) (void)hipEventDestroy(s.ev1);
+  if (s.stream) (void)hipStreamDestroy(s.stream);
+  s = Shard();
+}
+
+int make_shard(int dev, Shard& s) {
+  s.dev = dev;
+  HIPTRY(hipSetDevice(dev));
+  HIPTRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+  HIPTRY(hipEventCreate(&s.ev0));
+  HIPTRY(hipEventCreate(&s.ev1));
+  HIPTRY(hipMalloc(&s.d_trials, sizeof(unsigned long long)));
+  HIPTRY(hipHostMalloc(&s.h_trials, sizeof(unsigned long long), hipHostMallocDefault));
+  return ensure_items(s, 1024);
+}
+
+std::vector<int> visible_gfx950() {
+  std::vector<int> out;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return out;
+  for (int i = 0; i < n; ++i) {
+    hipDeviceProp_t p;
+    if (hipGetDeviceProperties(&p, i) != hipSuccess) continue;
+    if (std::strncmp(p.gcnArchName, "gfx950", 6) == 0) out.push_back(i);
+  }
+  return out;
+}
+
+int select_devices(const std::vector<int>& ids) {
+  for (auto& s : g_shards) free_shard(s);
+  g_shards.clear();
+  const auto vis = visible_gfx950();
+  for (int id : ids) {
+    if (std::find(vis.begin(), vis.end(), id) == vis.end())
+      return set_err(BMPOW_E_ARG, "device " + std::to_string(id) + " is not a visible gfx950 device");
+  }
+  g_shards.resize(ids.size());
+  for (size_t i = 0; i < ids.size(); ++i) {
+    int rc = make_shard(ids[i], g_shards[i]);
+    if (rc < 0) return rc;
+  }
+  return (int)g_shards.size();
+}
+
+int init_locked() {
+  if (g_inited) return (int)g_shards.size();
+  const auto vis = visible_gfx950();
+  if (vis.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
+  std::vector<int> ids = vis;
+  if (const char* env = std::getenv("BMPOW_DEVICES")) {
+    ids.clear();
+    std::string e(env);
+    size_t pos = 0;
+    while (pos <= e.size()) {
+      size_t c = e.find(',', pos);
+      std::string tok = e.substr(pos, c == std::string::npos ? std::string::npos : c - pos);
+      if (!tok.empty()) ids.push_back(std::atoi(tok.c_str()));
+      if (c == std::string::npos) break;
+      pos = c + 1;
+    }
+    if (ids.empty()) return set_err(BMPOW_E_ARG, "BMPOW_DEVICES names no device");
+  }
+  int rc = select_devices(ids);
+  if (rc < 0) return rc;
+  g_inited = true;
+  return rc;
+}
+
+void pack_obj(const uint8_t* ih, uint64_t target, bm_obj* o) {
+  std::memset(o, 0, sizeof(*o));
+  for (int i = 0; i < 8; ++i) {
+    uint64_t v = 0;
+    for (int j = 0; j < 8; ++j) v = (v << 8) | ih[8 * i + j];
+    o->w[i] = v;
+  }
+  o->target = target;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------
+// Batch state: the object table and per-object running minimum stay in HBM for the
+// lifetime of the batch (one copy per shard).
+// ---------------------------------------------------------------------------------------
+struct bmpow_batch {
+  size_t n = 0;
+  std::vector<bm_obj> objs;
+  std::vector<uint64_t> next, nonce, trial;
+  std::vector<uint8_t> done;
+  size_t first_pending = 0;
+  size_t pending = 0;
+  struct Dev {
+    bm_obj* d_obj = nullptr;
+    unsigned long long* d_best = nullptr;
+  };
+  std::vector<Dev> dev;  // one per shard (indexed like g_shards)
+};
+
+namespace {
+
+void batch_free_dev(bmpow_batch* b) {
+  for (size_t s = 0; s < b->dev.size() && s < g_shards.size(); ++s) {
+    (void)hipSetDevice(g_shards[s].dev);
+    if (b->dev[s].d_obj) (void)hipFree(b->dev[s].d_obj);
+    if (b->dev[s].d_best) (void)hipFree(b->dev[s].d_best);
+  }
+  b->dev.clear();
+}
+
+int batch_upload(bmpow_batch* b) {
+  b->dev.assign(g_shards.size(), bmpow_batch::Dev());
+  const size_t n = std::max<size_t>(b->n, 1);
+  for (size_t s = 0; s < g_shards.size(); ++s) {
+    Shard& sh = g_shards[s];
+    HIPTRY(hipSetDevice(sh.dev));
+    HIPTRY(hipMalloc(&b->dev[s].d_obj, n * sizeof(bm_obj)));
+    HIPTRY(hipMalloc(&b->dev[s].d_best, n * sizeof(unsigned long long)));
+    if (b->n) {
+      HIPTRY(hipMemcpyAsync(b->dev[s].d_obj, b->objs.data(), b->n * sizeof(bm_obj), hipMemcpyHostToDevice,
+                            sh.stream));
+      HIPTRY(hipMemsetAsync(b->dev[s].d_best, 0xFF, b->n * sizeof(unsigned long long), sh.stream));
+    }
+  }
+  for (auto& sh : g_shards) {
+    HIPTRY(hipSetDevice(sh.dev));
+    HIPTRY(hipStreamSynchronize(sh.stream));
+  }
+  return 0;
+}
+
+int batch_init(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
+  b->n = n;
+  b->objs.resize(n);
+  b->next.resize(n);
+  b->nonce.assign(n, 0);
+  b->trial.assign(n, 0);
+  b->done.assign(n, BMPOW_PENDING);
+  for (size_t i = 0; i < n; ++i) {
+    pack_obj(ihs + 64 * i, targets[i], &b->objs[i]);
+    b->next[i] = start ? start[i] : 1;
+  }
+  b->first_pending = 0;
+  b->pending = n;
+  return batch_upload(b);
+}
+
+// One bounded step.  Returns pending count (>= 0) or < 0.
+int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
+  if (trials_out) *trials_out = 0;
+  if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
+  if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
+  while (b->first_pending < b->n && b->done[b->first_pending] != BMPOW_PENDING) ++b->first_pending;
+  if (b->pending == 0) return 0;
+  const size_t S = g_shards.size();
+  if (budget == 0) budget = g_step_trials * S;
+  budget = std::min<uint64_t>(budget, (uint64_t)S << 36);  // grid.x stays far below 2^31
+  uint64_t total_chunks = std::max<uint64_t>(budget / BM_CHUNK, S);
+
+  // 1. windows: pending objects in index order, k chunks each
+  struct Win { uint32_t obj; uint64_t start, count, chunks, chunk0; };
+  std::vector<Win> wins;
+  const uint64_t k = std::max<uint64_t>(1, total_chunks / b->pending);
+  uint64_t chunk_acc = 0;
+  for (size_t i = b->first_pending; i < b->n && chunk_acc < total_chunks; ++i) {
+    if (b->done[i] != BMPOW_PENDING) continue;
+    const uint64_t st = b->next[i];
+    uint64_t want = k * BM_CHUNK;
+    const uint64_t room = kU64Max - st;  // nonces remaining after st
+    if (room < want - 1) want = room + 1;   // st + want - 1 <= 2^64-1
+    const uint64_t ch = (want + BM_CHUNK - 1) / BM_CHUNK;
+    wins.push_back({(uint32_t)i, st, want, ch, chunk_acc});
+    chunk_acc += ch;
+  }
+  const uint64_t C = chunk_acc;
+
+  // 2. slice the chunk list over shards
+  std::vector<uint64_t> cut(S + 1);
+  for (size_t s = 0; s <= S; ++s) cut[s] = C * s / S;
+  for (size_t s = 0; s < S; ++s) {
+    Shard& sh = g_shards[s];
+    sh.nitems = 0;
+    sh.nchunks = (uint32_t)(cut[s + 1] - cut[s]);
+    sh.item_obj.clear();
+  }
+  // items per shard
+  {
+    size_t s = 0;
+    for (const Win& w : wins) {
+      uint64_t c = w.chunk0;
+      const uint64_t cend = w.chunk0 + w.chunks;
+      while (c < cend) {
+        while (s < S && cut[s + 1] <= c) ++s;
+        const uint64_t seg_end = std::min(cend, cut[s + 1]);
+        Shard& sh = g_shards[s];
+        int rc = ensure_items(sh, sh.nitems + 1);
+        if (rc < 0) return rc;
+        bm_item& it = sh.h_items[sh.nitems];
+        const uint64_t off = (c - w.chunk0) * BM_CHUNK;
+        it.start = w.start + off;
+        it.count = std::min<uint64_t>(w.count - off, (seg_end - c) * BM_CHUNK);
+        it.obj = w.obj;
+        it.chunk_base = (uint32_t)(c - cut[s]);
+        it.pad = 0;
+        sh.item_obj.push_back(w.obj);
+        sh.nitems++;
+        c = seg_end;
+      }
+    }
+  }
+
+  // 3. launch on every shard, then collect
+  for (size_t s = 0; s < S; ++s) {
+    Shard& sh = g_shards[s];
+    if (sh.nitems == 0) continue;
+    HIPTRY(hipSetDevice(sh.dev));
+    HIPTRY(hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream));
+    HIPTRY(hipMemsetAsync(sh.d_trials, 0, sizeof(unsigned long long), sh.stream));
+    HIPTRY(hipEventRecord(sh.ev0, sh.stream));
+    HIPTRY(bm_launch_search(sh.stream, sh.nchunks, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best,
+                            sh.d_trials));
+    HIPTRY(hipEventRecord(sh.ev1, sh.stream));
+    HIPTRY(bm_launch_resolve(sh.stream, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best, sh.d_res));
+    HIPTRY(hipMemcpyAsync(sh.h_res, sh.d_res, sh.nitems * sizeof(bm_result), hipMemcpyDeviceToHost, sh.stream));
+    HIPTRY(hipMemcpyAsync(sh.h_trials, sh.d_trials, sizeof(unsigned long long), hipMemcpyDeviceToHost, sh.stream));
+  }
+  uint64_t step_trials = 0;
+  double step_max_ms = 0;
+  for (size_t s = 0; s < S; ++s) {
+    Shard& sh = g_shards[s];
+    if (sh.nitems == 0) continue;
+    HIPTRY(hipSetDevice(sh.dev));
+    HIPTRY(hipStreamSynchronize(sh.stream));
+    float ms = 0;
+    HIPTRY(hipEventElapsedTime(&ms, sh.ev0, sh.ev1));
+    sh.kernel_ms += ms;
+    g_stats.kernel_ms += ms;
+    g_stats.launches++;
+    step_max_ms = std::max<double>(step_max_ms, ms);
+    step_trials += *sh.h_trials;
+  }
+  g_stats.trials += step_trials;
+  g_stats.steps++;
+  double mx = 0;
+  for (auto& sh : g_shards) mx = std::max(mx, sh.kernel_ms);
+  g_stats.max_shard_kernel_ms = mx;
+  if (trials_out) *trials_out = step_trials;
+
+  // 4. host min-reduction over shards per object
+  std::vector<uint64_t> bestn(wins.size(), kU64Max), bestt(wins.size(), 0);
+  // wins are in ascending object order: map obj -> win index by binary search
+  auto win_of = [&](uint32_t obj) {
+    size_t lo = 0, hi = wins.size();
+    while (hi - lo > 1) {
+      size_t mid = (lo + hi) / 2;
+      if (wins[mid].obj <= obj) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  for (size_t s = 0; s < S; ++s) {
+    Shard& sh = g_shards[s];
+    for (uint32_t k2 = 0; k2 < sh.nitems; ++k2) {
+      const bm_result& r = sh.h_res[k2];
+      if (r.nonce == kU64Max) continue;
+      const size_t wi = win_of(sh.item_obj[k2]);
+      if (r.nonce < bestn[wi]) {
+        bestn[wi] = r.nonce;
+        bestt[wi] = r.trial;
+      }
+    }
+  }
+  for (size_t wi = 0; wi < wins.size(); ++wi) {
+    const Win& w = wins[wi];
+    if (bestn[wi] != kU64Max) {
+      b->done[w.obj] = BMPOW_DONE_FOUND;
+      b->nonce[w.obj] = bestn[wi];
+      b->trial[w.obj] = bestt[wi];
+      b->next[w.obj] = bestn[wi] + 1;
+      b->pending--;
+    } else if (w.count - 1 == kU64Max - w.start) {
+      b->done[w.obj] = BMPOW_DONE_EXHAUSTED;
+      b->next[w.obj] = kU64Max;
+      b->pending--;
+    } else {
+      b->next[w.obj] = w.start + w.count;
+    }
+  }
+  return (int)std::min<size_t>(b->pending, 0x7fffffff);
+}
+
+// Library-owned scratch batch reused by the stateless entry points.
+bmpow_batch* g_scratch = nullptr;
+
+int scratch_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
+  if (g_scratch) {
+    batch_free_dev(g_scratch);
+    delete g_scratch;
+    g_scratch = nullptr;
+  }
+  g_scratch = new bmpow_batch();
+  return batch_init(g_scratch, n, ihs, targets, start);
+}
+
+}  // namespace
+
+// =======================================================================================
+// C ABI
+// =======================================================================================
+extern "C" {
+
+int bmpow_init(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return init_locked();
+}
+
+int bmpow_device_count(void) { return (int)visible_gfx950().size(); }
+
+int bmpow_set_devices(const int* ids, int n) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (n < 0 || (n > 0 && !ids)) return set_err(BMPOW_E_ARG, "bad device list");
+  if (g_scratch) {
+    batch_free_dev(g_scratch);
+    delete g_scratch;
+    g_scratch = nullptr;
+  }
+  std::vector<int> v;
+  if (n == 0) v = visible_gfx950();
+  else v.assign(ids, ids + n);
+  if (v.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
+  int rc = select_devices(v);
+  g_inited = rc > 0;
+  return rc;
+}
+
+int bmpow_get_devices(int* ids, int cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (int i = 0; i < (int)g_shards.size() && i < cap; ++i) ids[i] = g_shards[i].dev;
+  return (int)g_shards.size();
+}
+
+void bmpow_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_scratch) {
+    batch_free_dev(g_scratch);
+    delete g_scratch;
+    g_scratch = nullptr;
+  }
+  for (auto& s : g_shards) free_shard(s);
+  g_shards.clear();
+  g_inited = false;
+}
+
+const char* bmpow_last_error(void) { return g_err.c_str(); }
+
+const char* bmpow_version(void) {
+  static char buf[128];
+  std::snprintf(buf, sizeof buf, "bmpow %d gfx950 block=%d iters=%d", BMPOW_ABI_VERSION, BM_BLOCK, BM_ITERS);
+  return buf;
+}
+
+void bmpow_abort(void) { g_abort.store(1); }
+void bmpow_clear_abort(void) { g_abort.store(0); }
+
+int bmpow_trials(const uint8_t ih[64], const uint64_t* nonces, size_t n, uint64_t* trials_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (!ih || (n && (!nonces || !trials_out))) return set_err(BMPOW_E_ARG, "null pointer");
+  if (n == 0) return 0;
+  Shard& sh = g_shards[0];
+  HIPTRY(hipSetDevice(sh.dev));
+  bm_obj o;
+  pack_obj(ih, 0, &o);
+  bm_obj* d_o = nullptr;
+  uint64_t *d_n = nullptr, *d_t = nullptr;
+  HIPTRY(hipMalloc(&d_o, sizeof(bm_obj)));
+  HIPTRY(hipMalloc(&d_n, n * sizeof(uint64_t)));
+  HIPTRY(hipMalloc(&d_t, n * sizeof(uint64_t)));
+  hipError_t e = hipMemcpyAsync(d_o, &o, sizeof o, hipMemcpyHostToDevice, sh.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_n, nonces, n * sizeof(uint64_t), hipMemcpyHostToDevice, sh.stream);
+  if (e == hipSuccess) e = bm_launch_trials(sh.stream, d_o, d_n, n, d_t);
+  if (e == hipSuccess) e = hipMemcpyAsync(trials_out, d_t, n * sizeof(uint64_t), hipMemcpyDeviceToHost, sh.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
+  (void)hipFree(d_o);
+  (void)hipFree(d_n);
+  (void)hipFree(d_t);
+  if (e != hipSuccess) return set_err(BMPOW_E_HIP, std::string("bmpow_trials: ") + hipGetErrorString(e));
+  return 0;
+}
+
+int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials,
+                 uint64_t* nonce_out, uint64_t* trial_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (!ih || !nonce_out || !trial_out) return set_err(BMPOW_E_ARG, "null pointer");
+  if (max_trials == 0) return BMPOW_NOT_FOUND;
+  rc = scratch_batch(1, ih, &target, &start);
+  if (rc < 0) return rc;
+  bmpow_batch* b = g_scratch;
+  uint64_t left = max_trials;
+  const uint64_t step = g_step_trials * g_shards.size();
+  while (left > 0) {
+    // This step's window for the single object is `want` nonces rounded up to whole chunks;
+    // a hit in the round-up tail lies beyond the caller's budget and is reported as
+    // NOT_FOUND (the caller resumes at start + max_trials and finds it again: exactness
+    // only needs every nonce below a reported hit to have been hashed).
+    const uint64_t want = std::min(left, step);
+    const uint64_t chunks = (want + BM_CHUNK - 1) / BM_CHUNK;
+    const uint64_t st = b->next[0];
+    rc = batch_step_locked(b, chunks * BM_CHUNK, nullptr);
+    if (rc < 0) return rc;
+    if (b->done[0] == BMPOW_DONE_FOUND) {
+      if (b->nonce[0] - st >= want) return BMPOW_NOT_FOUND;
+      *nonce_out = b->nonce[0];
+      *trial_out = b->trial[0];
+      return BMPOW_FOUND;
+    }
+    if (b->done[0] == BMPOW_DONE_EXHAUSTED) return BMPOW_NOT_FOUND;
+    left -= std::min(left, b->next[0] - st);
+  }
+  return BMPOW_NOT_FOUND;
+}
+
+int bmpow_search_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* next_start,
+                       uint64_t budget, uint64_t* nonce_out, uint64_t* trial_out, uint8_t* done) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (n == 0) return 0;
+  if (!ihs || !targets || !next_start || !nonce_out || !trial_out || !done)
+    return set_err(BMPOW_E_ARG, "null pointer");
+  rc = scratch_batch(n, ihs, targets, next_start);
+  if (rc < 0) return rc;
+  bmpow_batch* b = g_scratch;
+  for (size_t i = 0; i < n; ++i) {
+    if (done[i] != BMPOW_PENDING) {
+      b->done[i] = done[i];
+      b->pending--;
+    }
+  }
+  uint64_t spent = 0;
+  if (budget == 0) budget = g_step_trials * g_shards.size();
+  int pending = (int)b->pending;
+  while (pending > 0 && spent < budget) {
+    uint64_t t = 0;
+    pending = batch_step_locked(b, std::min(budget - spent, g_step_trials * g_shards.size()), &t);
+    if (pending < 0) return pending;
+    spent += std::max<uint64_t>(t, BM_CHUNK);
+  }
+  for (size_t i = 0; i < n; ++i) {
+    if (done[i] != BMPOW_PENDING) continue;
+    done[i] = b->done[i];
+    next_start[i] = b->next[i];
+    if (b->done[i] == BMPOW_DONE_FOUND) {
+      nonce_out[i] = b->nonce[i];
+      trial_out[i] = b->trial[i];
+    }
+  }
+  return pending;
+}
+
+bmpow_batch* bmpow_batch_create(size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (init_locked() < 0) return nullptr;
+  if (n && (!ihs || !targets)) {
+    set_err(BMPOW_E_ARG, "null pointer");
+    return nullptr;
+  }
+  if (n > 0xffffffffULL) {
+    set_err(BMPOW_E_ARG, "too many objects");
+    return nullptr;
+  }
+  bmpow_batch* b = new bmpow_batch();
+  if (batch_init(b, n, ihs, targets, start) < 0) {
+    batch_free_dev(b);
+    delete b;
+    return nullptr;
+  }
+  return b;
+}
+
+int bmpow_batch_step(bmpow_batch* b, uint64_t budget) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!b) return set_err(BMPOW_E_STATE, "null batch");
+  return batch_step_locked(b, budget, nullptr);
+}
+
+int bmpow_batch_results(const bmpow_batch* b, uint64_t* nonce_out, uint64_t* trial_out, uint8_t* done,
+                        uint64_t* next_start) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!b) return set_err(BMPOW_E_STATE, "null batch");
+  for (size_t i = 0; i < b->n; ++i) {
+    if (nonce_out) nonce_out[i] = b->nonce[i];
+    if (trial_out) trial_out[i] = b->trial[i];
+    if (done) done[i] = b->done[i];
+    if (next_start) next_start[i] = b->next[i];
+  }
+  return (int)std::min<size_t>(b->pending, 0x7fffffff);
+}
+
+int bmpow_batch_reset(bmpow_batch* b, const uint64_t* start) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!b) return set_err(BMPOW_E_STATE, "null batch");
+  if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
+  for (size_t i = 0; i < b->n; ++i) {
+    b->next[i] = start ? start[i] : 1;
+    b->nonce[i] = b->trial[i] = 0;
+    b->done[i] = BMPOW_PENDING;
+  }
+  b->first_pending = 0;
+  b->pending = b->n;
+  for (size_t s = 0; s < g_shards.size(); ++s) {
+    Shard& sh = g_shards[s];
+    HIPTRY(hipSetDevice(sh.dev));
+    if (b->n) HIPTRY(hipMemsetAsync(b->dev[s].d_best, 0xFF, b->n * sizeof(unsigned long long), sh.stream));
+  }
+  for (auto& sh : g_shards) {
+    HIPTRY(hipSetDevice(sh.dev));
+    HIPTRY(hipStreamSynchronize(sh.stream));
+  }
+  return (int)std::min<size_t>(b->pending, 0x7fffffff);
+}
+
+void bmpow_batch_destroy(bmpow_batch* b) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!b) return;
+  batch_free_dev(b);
+  delete b;
+}
+
+int bmpow_get_stats(bmpow_stats* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!out) return BMPOW_E_ARG;
+  *out = g_stats;
+  return 0;
+}
+
+void bmpow_reset_stats(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_stats = bmpow_stats{};
+  for (auto& s : g_shards) s.kernel_ms = 0;
+}
+
+uint64_t bmpow_get_step_trials(void) { return g_step_trials; }
+
+void bmpow_set_step_trials(uint64_t t) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_step_trials = std::max<uint64_t>(t, BM_CHUNK);
+}
+
+unsigned long long BitmessagePOW(unsigned char* starthash, unsigned long long target) {
+  uint64_t start = 1, nonce = 0, tv = 0;
+  for (;;) {
+    const uint64_t budget = 1ULL << 34;
+    int rc = bmpow_search(starthash, target, start, budget, &nonce, &tv);
+    if (rc == BMPOW_FOUND) return nonce;
+    if (rc < 0) return 0;
+    if (start > kU64Max - budget) return 0;
+    start += budget;
+  }
+}
+
+}  // extern "C"

@@ -1,0 +1,39 @@
+// bmpow_kernels.h -- device data layout shared by the kernels and the host scheduler.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// One workgroup = BM_BLOCK lanes x BM_ITERS nonces = one CHUNK of a work item.
+#ifndef BM_ITERS
+#define BM_ITERS 32
+#endif
+#define BM_BLOCK 256
+#define BM_CHUNK ((uint64_t)BM_BLOCK * BM_ITERS)
+
+// Per-object record, device resident for the life of a batch (128 B, one per object).
+struct bm_obj {
+  uint64_t w[8];     // initialHash as 8 big-endian words = W1..W8 of SHA-512 block 1
+  uint64_t target;   // accept trial <= target
+  uint64_t pad[7];
+};
+
+// Work item = one object's contiguous nonce window inside one launch (32 B).
+struct bm_item {
+  uint64_t start;       // first nonce of the window
+  uint64_t count;       // trials in the window (> 0; start + count - 1 <= 2^64 - 1)
+  uint32_t obj;         // object index (into bm_obj[] and best[])
+  uint32_t chunk_base;  // first chunk (workgroup) index of this item in the launch
+  uint64_t pad;
+};
+
+struct bm_result {
+  uint64_t nonce;  // UINT64_MAX = no hit in this item's object yet
+  uint64_t trial;
+};
+
+hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, const bm_obj* objs, const bm_item* items,
+                            uint32_t nitems, unsigned long long* best, unsigned long long* trials_done);
+hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
+                             const unsigned long long* best, bm_result* res);
+hipError_t bm_launch_trials(hipStream_t st, const bm_obj* obj, const uint64_t* nonces, uint64_t n,
+                            uint64_t* out);

@@ -1,0 +1,103 @@
+// sha512_dev.h -- gfx950 device primitives for the Bitmessage trial function.
+//
+// trial(n, ih) = BE64(SHA512(SHA512(BE64(n) || ih))[0:8])     (reference:
+// src/proofofwork.py:106-107, docs/pow.rst:42-49).  In SHA-512 words no byte swap is
+// needed anywhere: block 1 is W0 = n, W1..8 = ih as big-endian u64, W9 = 0x80.., W15 = 576;
+// block 2 is W0..7 = H(block 1), W8 = 0x80.., W15 = 512; trial = IV0 + a80(block 2).
+//
+// All arithmetic is 32-bit VALU on register pairs:
+//   ROTR64  -> 2 x v_alignbit_b32          (explicit builtin; hipcc's default lowering of
+//                                           (x>>n)|(x<<64-n) emits 64-bit shifts + ORs)
+//   XOR3 / Ch / Maj -> 2 x v_bitop3_b32   (gfx950 3-input LUT op, selected by the compiler)
+//   ADD64   -> v_lshl_add_u64 (gfx950)    (selected by the compiler for uint64_t +)
+#pragma once
+#include <stdint.h>
+
+#define BM_DEV __device__ __forceinline__
+
+namespace bm {
+
+// FIPS 180-4 4.2.3 / 5.3.5 constants (compile-time: every round index is a constant).
+constexpr uint64_t K(int t) {
+  constexpr uint64_t k[80] = {
+      0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+      0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+      0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+      0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+      0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+      0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+      0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+      0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+      0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+      0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+      0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+      0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+      0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+      0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+      0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+      0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+      0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+      0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+      0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+      0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+  return k[t];
+}
+
+constexpr uint64_t IV(int i) {
+  constexpr uint64_t iv[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                              0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                              0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+  return iv[i];
+}
+
+// ---- 64-bit rotates / shifts on 32-bit halves via v_alignbit_b32 ----
+BM_DEV uint32_t lo32(uint64_t x) { return (uint32_t)x; }
+BM_DEV uint32_t hi32(uint64_t x) { return (uint32_t)(x >> 32); }
+BM_DEV uint64_t mk64(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+template <int N>
+BM_DEV uint64_t rotr(uint64_t x) {
+  static_assert(N > 0 && N < 64, "rotate");
+  const uint32_t l = lo32(x), h = hi32(x);
+  if constexpr (N < 32) {
+    return mk64(__builtin_amdgcn_alignbit(h, l, N), __builtin_amdgcn_alignbit(l, h, N));
+  } else if constexpr (N == 32) {
+    return mk64(h, l);
+  } else {
+    return mk64(__builtin_amdgcn_alignbit(l, h, N - 32), __builtin_amdgcn_alignbit(h, l, N - 32));
+  }
+}
+
+template <int N>
+BM_DEV uint64_t shr(uint64_t x) {
+  static_assert(N > 0 && N < 32, "shift");
+  const uint32_t l = lo32(x), h = hi32(x);
+  return mk64(__builtin_amdgcn_alignbit(h, l, N), h >> N);
+}
+
+// FIPS 180-4 4.1.3 functions.
+BM_DEV uint64_t Sig0(uint64_t a) { return rotr<28>(a) ^ rotr<34>(a) ^ rotr<39>(a); }
+BM_DEV uint64_t Sig1(uint64_t e) { return rotr<14>(e) ^ rotr<18>(e) ^ rotr<41>(e); }
+BM_DEV uint64_t sig0(uint64_t w) { return rotr<1>(w) ^ rotr<8>(w) ^ shr<7>(w); }
+BM_DEV uint64_t sig1(uint64_t w) { return rotr<19>(w) ^ rotr<61>(w) ^ shr<6>(w); }
+BM_DEV uint64_t Ch(uint64_t e, uint64_t f, uint64_t g) { return g ^ (e & (f ^ g)); }
+BM_DEV uint64_t Maj(uint64_t a, uint64_t b, uint64_t c) { return (a & b) | (c & (a | b)); }
+
+// constexpr twins (host + device) for compile-time folding of IV-only expressions.
+constexpr uint64_t crotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+constexpr uint64_t cSig0(uint64_t a) { return crotr(a, 28) ^ crotr(a, 34) ^ crotr(a, 39); }
+constexpr uint64_t cSig1(uint64_t e) { return crotr(e, 14) ^ crotr(e, 18) ^ crotr(e, 41); }
+constexpr uint64_t csig0(uint64_t w) { return crotr(w, 1) ^ crotr(w, 8) ^ (w >> 7); }
+constexpr uint64_t csig1(uint64_t w) { return crotr(w, 19) ^ crotr(w, 61) ^ (w >> 6); }
+constexpr uint64_t cCh(uint64_t e, uint64_t f, uint64_t g) { return (e & f) ^ (~e & g); }
+constexpr uint64_t cMaj(uint64_t a, uint64_t b, uint64_t c) { return (a & b) ^ (a & c) ^ (b & c); }
+
+// Round 0 from the IV with W0 the only unknown (both blocks start from the IV):
+//   T1 = T1C + W0,  a1 = W0 + A1C,  e1 = W0 + E1C
+constexpr uint64_t T1C = IV(7) + cSig1(IV(4)) + cCh(IV(4), IV(5), IV(6)) + K(0);
+constexpr uint64_t A1C = T1C + cSig0(IV(0)) + cMaj(IV(0), IV(1), IV(2));
+constexpr uint64_t E1C = IV(3) + T1C;
+
+constexpr uint64_t PAD = 0x8000000000000000ULL;
+
+}  // namespace bm

@@ -1,0 +1,236 @@
+"""MI355X proof of work -- drop-in for the reference's ``src/proofofwork.py``.
+
+Same public names and return shapes as the reference:
+
+* ``run(target, initialHash) -> [trialValue, nonce]``      (reference ``:288-325``)
+* ``init()``, ``resetPoW()``, ``getPowType()``, ``estimate()`` (``:336-394, 328-330, 229-236, 197-226``)
+
+plus the batched entry point BASELINE.json's north star asks for:
+
+* ``run_batch([(target, initialHash), ...]) -> [[trialValue, nonce], ...]`` in input order,
+  each element equal to ``run`` on that element;
+* ``iter_batch(...)`` yields ``(index, trialValue, nonce)`` as objects finish (lets a
+  caller release msgs whose embedded ack just finished, ``class_singleWorker.py:1220``).
+
+Every answer is the ``_doSafePoW`` answer (``:100-111``): the first ``nonce >= 1`` with
+``trialValue <= target``.  The search runs on gfx950 through ``libbmpow_hip.so`` in bounded
+steps; between steps ``state.shutdown`` is polled and a set flag raises
+``StopIteration("Interrupted")`` (the reference contract, ``:104-109``; the polling
+pattern of ``dev/powinterrupttest.py:22-37``).  There is NO CPU fallback: a missing library
+or device raises :class:`BmpowUnavailable` (the reference silently degraded to Python).
+"""
+import ctypes
+import hashlib
+import logging
+from struct import pack, unpack
+
+from . import _lib
+from . import state
+from ._lib import BmpowError, BmpowUnavailable  # noqa: F401  (re-exported)
+
+logger = logging.getLogger('default')
+
+U64_MAX = _lib.U64_MAX
+#: trials per bounded ``bmpow_search`` call from ``run``: a few steps of the scheduler
+#: (~0.1-0.3 s on one MI355X), i.e. the shutdown-poll interval of the Python loop.
+CALL_TRIALS = 1 << 30
+#: re-check every returned nonce with hashlib, as ``_doGPUPoW`` does (``:176-190``)
+VERIFY = True
+
+
+def _ih_bytes(initialHash):
+    """The reference passes ``create_string_buffer(initialHash, 64)`` (``:161``): shorter
+    input is zero-padded to 64 bytes.  The GPU kernel's block layout is fixed to a 64-byte
+    initialHash (``sha512(payload).digest()`` at every call site)."""
+    if isinstance(initialHash, str):
+        initialHash = initialHash.encode('latin-1')
+    ih = bytes(initialHash)
+    if len(ih) > 64:
+        raise ValueError('initialHash must be at most 64 bytes (got %d)' % len(ih))
+    return ih + b'\x00' * (64 - len(ih))
+
+
+def _clamp_target(target):
+    """``trialValue <= target`` on Python ints: any target >= 2^64-1 accepts every trial;
+    a negative target accepts none (the reference then loops until shutdown)."""
+    target = int(target)
+    if target >= U64_MAX:
+        return U64_MAX, True
+    if target < 0:
+        return 0, False
+    return target, True
+
+
+def _trial_host(nonce, ih):
+    return unpack('>Q', hashlib.sha512(hashlib.sha512(pack('>Q', nonce) + ih).digest()).digest()[0:8])[0]
+
+
+def _verify(target, ih, trial, nonce):
+    if VERIFY and _trial_host(nonce, ih) != trial:
+        raise BmpowError(_lib.E_HIP, 'GPU returned a wrong trial value for nonce %d' % nonce)
+    if trial > target:
+        raise BmpowError(_lib.E_HIP, 'GPU returned nonce %d above target' % nonce)
+
+
+def _interrupted():
+    return getattr(state, 'shutdown', 0) != 0
+
+
+def _doHIPPoW(target, initialHash):
+    """Single object on the GPU; replaces ``_doGPUPoW``/``_doCPoW`` (``:157-194``)."""
+    lib = _lib.get()
+    ih = _ih_bytes(initialHash)
+    t, satisfiable = _clamp_target(target)
+    start = 1
+    n, tv = ctypes.c_uint64(), ctypes.c_uint64()
+    logger.debug('HIP PoW start')
+    while True:
+        if _interrupted():
+            raise StopIteration('Interrupted')
+        if not satisfiable:
+            # no trial can be <= a negative target: spin like the reference, interruptibly
+            import time
+            time.sleep(0.05)
+            continue
+        rc = _lib.check(lib, lib.bmpow_search(ih, t, start, CALL_TRIALS, ctypes.byref(n), ctypes.byref(tv)),
+                        'bmpow_search')
+        if rc == _lib.FOUND:
+            break
+        if start > U64_MAX - CALL_TRIALS:
+            raise BmpowError(_lib.E_ARG, 'nonce space exhausted without a hit')
+        start += CALL_TRIALS
+    trialValue, nonce = tv.value, n.value
+    _verify(t, ih, trialValue, nonce)
+    if _interrupted():
+        raise StopIteration('Interrupted')
+    logger.debug('HIP PoW done')
+    return [trialValue, nonce]
+
+
+def run(target, initialHash):
+    """Run the proof of work (reference ``:288-325``).  Returns ``[trialValue, nonce]``."""
+    if _interrupted():
+        # the reference's bare ``raise`` outside an except block (``:291-292``)
+        raise RuntimeError('No active exception to reraise')
+    return _doHIPPoW(int(target), initialHash)
+
+
+class PowInterrupted(Exception):
+    """Raised by :func:`iter_batch` when ``state.shutdown`` is set (a generator cannot raise
+    StopIteration, PEP 479); :func:`run_batch` turns it into ``StopIteration("Interrupted")``."""
+
+
+def iter_batch(objects, step_trials=0):
+    """Solve many ``(target, initialHash)`` objects at once on the GPU, yielding
+    ``(index, trialValue, nonce)`` as each finishes (ascending index within a step).
+
+    The object table stays in HBM (``bmpow_batch_create``); each ``bmpow_batch_step`` is one
+    bounded launch per device over the pending objects, so large objects are nonce-sharded
+    and small ones packed many per launch.  Raises :class:`PowInterrupted` on shutdown."""
+    import numpy as np
+    lib = _lib.get()
+    objs = list(objects)
+    n = len(objs)
+    if n == 0:
+        return
+    ihs = bytearray()
+    targets = np.empty(n, dtype=np.uint64)
+    for i, (target, ih) in enumerate(objs):
+        ihs += _ih_bytes(ih)
+        t, ok = _clamp_target(target)
+        if not ok:
+            raise ValueError('object %d has a negative target: no nonce can satisfy it' % i)
+        targets[i] = t
+    ihs = bytes(ihs)
+    p64 = ctypes.POINTER(ctypes.c_uint64)
+    h = lib.bmpow_batch_create(n, ihs, targets.ctypes.data_as(p64), None)
+    if not h:
+        raise BmpowError(_lib.E_HIP, 'bmpow_batch_create: %s' % lib.bmpow_last_error().decode())
+    try:
+        nonce = np.zeros(n, dtype=np.uint64)
+        trial = np.zeros(n, dtype=np.uint64)
+        done = np.zeros(n, dtype=np.uint8)
+        reported = np.zeros(n, dtype=bool)
+        pending = n
+        while pending > 0:
+            if _interrupted():
+                raise PowInterrupted('Interrupted')
+            pending = _lib.check(lib, lib.bmpow_batch_step(h, step_trials), 'bmpow_batch_step')
+            lib.bmpow_batch_results(h, nonce.ctypes.data_as(p64), trial.ctypes.data_as(p64),
+                                    done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), None)
+            fresh = np.flatnonzero((done != _lib.PENDING) & ~reported)
+            reported[fresh] = True
+            for i in fresh.tolist():
+                if done[i] != _lib.DONE_FOUND:
+                    raise BmpowError(_lib.E_ARG, 'object %d: nonce space exhausted' % i)
+                tv, nn = int(trial[i]), int(nonce[i])
+                _verify(int(targets[i]), ihs[64 * i:64 * i + 64], tv, nn)
+                yield i, tv, nn
+    finally:
+        lib.bmpow_batch_destroy(h)
+
+
+def run_batch(objects, step_trials=0):
+    """``[(target, initialHash), ...] -> [[trialValue, nonce], ...]`` in input order."""
+    objs = list(objects)
+    out = [None] * len(objs)
+    if _interrupted() and objs:
+        raise RuntimeError('No active exception to reraise')
+    try:
+        for i, tv, nonce in iter_batch(objs, step_trials):
+            out[i] = [tv, nonce]
+    except PowInterrupted:
+        raise StopIteration('Interrupted')
+    return out
+
+
+def init():
+    """Load ``libbmpow_hip.so`` and select the gfx950 devices (reference ``:336-394``).
+    Returns the number of device shards; logs and returns 0 when unavailable."""
+    try:
+        return _device_count()
+    except BmpowUnavailable as e:
+        logger.error('HIP PoW unavailable: %s', e)
+        return 0
+
+
+def _device_count():
+    lib = _lib.get()
+    ids = (ctypes.c_int * 64)()
+    return lib.bmpow_get_devices(ids, 64)
+
+
+def resetPoW():
+    """Re-select devices (reference ``:328-330`` re-ran ``openclpow.initCL``)."""
+    _lib.reset()
+    return init()
+
+
+def getPowType():
+    """``"HIP"`` when the gfx950 engine is usable (reference ``:229-236`` returned
+    ``"OpenCL"``/``"C"``/``"python"``); ``"none"`` otherwise (there is no CPU fallback)."""
+    try:
+        _lib.get()
+        return 'HIP'
+    except BmpowUnavailable:
+        return 'none'
+
+
+def estimate(difficulty, format=False):  # pylint: disable=redefined-builtin
+    """Kept with the reference's exact semantics (``:197-226``, ``difficulty / 10`` and
+    ``None`` when ``format`` is set) for API compatibility."""
+    ret = difficulty / 10
+    if ret < 1:
+        ret = 1
+    if format:
+        ret = None
+    return ret
+
+
+def abort():
+    """Make an in-flight device search return at its next step boundary (thread/signal safe)."""
+    _lib.get().bmpow_abort()
+
+
+def clear_abort():
+    _lib.get().bmpow_clear_abort()

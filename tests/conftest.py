@@ -1,0 +1,42 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, 'tests', 'golden')
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line('markers', 'gpu: needs an MI355X (gfx950) GPU and libbmpow_hip.so')
+    config.addinivalue_line('markers', 'slow: long-running (minutes)')
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope='session')
+def golden():
+    return load_golden
+
+
+@pytest.fixture(scope='session')
+def coracle():
+    """The C restatement (oracle/liboracle.so), built on demand with make."""
+    from oracle import oracle
+    if not oracle.have_c_oracle():
+        import subprocess
+        subprocess.check_call(['make', '-C', os.path.join(ROOT, 'oracle'), 'liboracle.so'])
+    return oracle.COracle()
+
+
+@pytest.fixture(scope='session')
+def gpulib():
+    """libbmpow_hip.so initialised on the GPU (gpu tests only)."""
+    from pybitmessage_amd import _lib
+    return _lib.get()

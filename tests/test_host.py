@@ -1,0 +1,187 @@
+"""Host-side logic that needs no GPU: ABI export table, Python mirror of the reference
+interface, target formulas, verifier, interrupt loop (against a scripted test double of the
+C ABI -- the double lives here in tests/, the product has no fallback)."""
+import ctypes
+import hashlib
+import os
+import random
+import re
+import threading
+
+import pytest
+
+from tests.conftest import ROOT
+
+from pybitmessage_amd import _lib, proofofwork, state, targets
+
+HEADER = os.path.join(ROOT, 'include', 'bmpow.h')
+
+
+def declared_symbols():
+    text = open(HEADER).read()
+    return sorted(set(re.findall(r'BMPOW_API\s+[\w\s\*]+?\b(\w+)\s*\(', text)))
+
+
+@pytest.fixture(scope='module')
+def rawlib():
+    path = _lib.lib_path()
+    if not os.path.exists(path):
+        import subprocess
+        subprocess.check_call(['make', '-C', os.path.join(ROOT, 'pybitmessage_amd', 'csrc')])
+    return ctypes.CDLL(path)
+
+
+def test_header_declares_the_boundary():
+    syms = declared_symbols()
+    for s in ['bmpow_init', 'bmpow_search', 'bmpow_search_batch', 'bmpow_trials', 'bmpow_abort',
+              'bmpow_batch_create', 'bmpow_batch_step', 'bmpow_batch_results', 'bmpow_batch_destroy',
+              'bmpow_set_devices', 'bmpow_last_error', 'BitmessagePOW']:
+        assert s in syms
+    assert len(syms) == 22
+
+
+def test_library_exports_every_declared_symbol(rawlib):
+    for s in declared_symbols():
+        assert hasattr(rawlib, s), s
+
+
+def test_python_binding_covers_header():
+    bound = sorted(n for n, _, _ in _lib.SIGNATURES)
+    assert bound == declared_symbols()
+
+
+def test_load_binds_all_signatures(rawlib):
+    lib = _lib.load()
+    assert lib.bmpow_version().startswith(b'bmpow 1 gfx950')
+    assert lib.bmpow_get_step_trials() > 0
+
+
+@pytest.mark.skipif(os.path.exists('/dev/kfd'), reason='a GPU is present')
+def test_no_device_fails_loudly():
+    lib = _lib.load()
+    assert lib.bmpow_device_count() == 0
+    assert lib.bmpow_init() == _lib.E_NODEV
+    assert b'gfx950' in lib.bmpow_last_error()
+    n, t = ctypes.c_uint64(), ctypes.c_uint64()
+    assert lib.bmpow_search(bytes(64), 1, 1, 10, ctypes.byref(n), ctypes.byref(t)) == _lib.E_NODEV
+    with pytest.raises(_lib.BmpowUnavailable):
+        proofofwork.run(2 ** 60, bytes(64))
+    assert proofofwork.getPowType() == 'none'
+    assert proofofwork.init() == 0
+
+
+def test_ih_padding_mirrors_create_string_buffer():
+    assert proofofwork._ih_bytes(b'') == bytes(64)
+    assert proofofwork._ih_bytes(b'ab') == b'ab' + bytes(62)
+    assert proofofwork._ih_bytes('ab') == b'ab' + bytes(62)
+    with pytest.raises(ValueError):
+        proofofwork._ih_bytes(bytes(65))
+
+
+def test_target_clamp():
+    assert proofofwork._clamp_target(2 ** 64) == (2 ** 64 - 1, True)
+    assert proofofwork._clamp_target(2.0 ** 70) == (2 ** 64 - 1, True)
+    assert proofofwork._clamp_target(12345.9) == (12345, True)
+    assert proofofwork._clamp_target(-1) == (0, False)
+
+
+def test_estimate_matches_reference():
+    assert proofofwork.estimate(5) == 1
+    assert proofofwork.estimate(100) == 10
+    assert proofofwork.estimate(100, format=True) is None
+
+
+def test_targets_match_golden(golden):
+    for t in golden('config_targets.json')['targets']:
+        if t['kind'] == 'singleWorker':
+            f = targets.object_target(t['L'], t['ttl'], t['ntpb'], t['extra'])
+        else:
+            f = targets.api_target(t['L'], t['ntpb'], t['extra'])
+        assert f.hex() == t['target_float']
+        assert targets.int_target(f) == t['target']
+
+
+def test_verifier_matches_reference(golden):
+    for k in golden('verifier_kats.json')['kats']:
+        obj = bytes.fromhex(k['object'])
+        assert targets.isProofOfWorkSufficient(obj, k['ntpb'], k['extra'], k['recvTime']) == k['sufficient']
+        nxt = targets.attach_nonce(int.from_bytes(obj[:8], 'big') + 1, obj[8:])
+        assert targets.isProofOfWorkSufficient(nxt, k['ntpb'], k['extra'], k['recvTime']) == \
+            k['object_next_nonce_sufficient']
+        assert targets.isProofOfWorkSufficient(obj, k['ntpb'], k['extra'], k['recvTime'] - 10 ** 6) == \
+            k['recvTime_minus_1e6_sufficient']
+
+
+# ---------------- interrupt / loop logic against a scripted C-ABI double ----------------
+class ScriptedLib(object):
+    """Test double of the C ABI: bmpow_search answers from the C oracle over the bounded
+    window it is asked for (so loop/resume logic is exercised exactly)."""
+
+    def __init__(self, coracle, stop_after=None):
+        self.co = coracle
+        self.calls = []
+        self.stop_after = stop_after
+
+    def bmpow_search(self, ih, target, start, max_trials, pn, pt):
+        self.calls.append((start, max_trials))
+        if self.stop_after is not None and len(self.calls) >= self.stop_after:
+            state.shutdown = 1
+        res = self.co.search(ih, target, start, max_trials)
+        if res is None:
+            return _lib.NOT_FOUND
+        pt._obj.value, pn._obj.value = res
+        return _lib.FOUND
+
+    def bmpow_last_error(self):
+        return b''
+
+
+@pytest.fixture
+def scripted(monkeypatch, coracle):
+    def make(**kw):
+        lib = ScriptedLib(coracle, **kw)
+        monkeypatch.setattr(_lib, 'get', lambda: lib)
+        return lib
+    yield make
+    state.shutdown = 0
+
+
+def test_run_resumes_across_bounded_calls(scripted, monkeypatch):
+    lib = scripted()
+    monkeypatch.setattr(proofofwork, 'CALL_TRIALS', 100)
+    ih = hashlib.sha512(b'hello').digest()
+    assert proofofwork.run(2 ** 64 // 1000, ih) == [2417842470843601, 1315]
+    assert lib.calls[0] == (1, 100) and lib.calls[-1] == (1301, 100) and len(lib.calls) == 14
+
+
+def test_run_raises_interrupted_between_calls(scripted, monkeypatch):
+    lib = scripted(stop_after=3)
+    monkeypatch.setattr(proofofwork, 'CALL_TRIALS', 10)
+    with pytest.raises(StopIteration, match='Interrupted'):
+        proofofwork.run(0, bytes(64))
+    assert len(lib.calls) == 3
+
+
+def test_run_refuses_during_shutdown(scripted):
+    scripted()
+    state.shutdown = 1
+    with pytest.raises(RuntimeError):
+        proofofwork.run(10, bytes(64))
+
+
+def test_negative_target_spins_until_shutdown(scripted):
+    lib = scripted()
+    timer = threading.Timer(0.2, lambda: setattr(state, 'shutdown', 1))
+    timer.start()
+    with pytest.raises(StopIteration):
+        proofofwork.run(-5, bytes(64))
+    assert lib.calls == []
+
+
+def test_verify_rejects_wrong_gpu_answer():
+    ih = hashlib.sha512(b'hello').digest()
+    proofofwork._verify(2 ** 64 // 1000, ih, 2417842470843601, 1315)
+    with pytest.raises(_lib.BmpowError):
+        proofofwork._verify(2 ** 64 // 1000, ih, 2417842470843602, 1315)
+    with pytest.raises(_lib.BmpowError):
+        proofofwork._verify(10, ih, 2417842470843601, 1315)

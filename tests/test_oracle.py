@@ -1,0 +1,132 @@
+"""The oracle is pinned before anything is checked against it (CPU only).
+
+Golden vectors in tests/golden/ were produced by running the reference itself
+(tests/golden/make_golden.py): ``_pool_worker`` / ``_doSafePoW`` (src/proofofwork.py:90-111),
+``protocol.isProofOfWorkSufficient`` (src/protocol.py:258-286).
+"""
+import hashlib
+import os
+import random
+
+import pytest
+
+from oracle import oracle
+
+U64 = 1 << 64
+
+
+def test_c_sha512_matches_hashlib(coracle):
+    rng = random.Random(7)
+    for L in list(range(0, 300)) + [1000, 4095, 4096, 16384]:
+        d = rng.randbytes(L)
+        assert coracle.sha512(d) == hashlib.sha512(d).digest(), L
+
+
+def test_trial_kats_python_and_c(golden, coracle):
+    kats = golden('trial_kats.json')['kats']
+    assert len(kats) > 300
+    for k in kats:
+        ih = bytes.fromhex(k['ih'])
+        assert oracle.trial(k['nonce'], ih) == k['trial']
+        assert coracle.trial(k['nonce'], ih) == k['trial']
+
+
+def test_survey_appendix_trial_values(coracle):
+    # SURVEY.md Appendix A, computed independently during the survey
+    ih0 = bytes(64)
+    hello = hashlib.sha512(b'hello').digest()
+    assert coracle.trial(0, ih0) == 15384050719303346949
+    assert coracle.trial(1, ih0) == 2274854268764994929
+    assert coracle.trial(1 << 32, ih0) == 6525330889464198002
+    assert coracle.trial(U64 - 1, ih0) == 2198939099669698234
+    assert coracle.trial(1, hello) == 13542169780345634238
+    assert coracle.trial(1 << 63, hello) == 16364079262595905430
+
+
+def test_first_nonce_kats_c_oracle(golden, coracle):
+    for k in golden('first_nonce_kats.json')['kats']:
+        ih = bytes.fromhex(k['ih'])
+        if k['nonce'] > 2_000_000:
+            continue  # the slow vectors are covered by test_first_nonce_slow_kats_mt
+        assert coracle.search(ih, k['target']) == (k['trial'], k['nonce']), k['note']
+
+
+def test_first_nonce_slow_kats_mt(golden, coracle):
+    for k in golden('first_nonce_kats.json')['kats']:
+        if k['nonce'] <= 2_000_000 or k['nonce'] > 50_000_000:
+            continue
+        ih = bytes.fromhex(k['ih'])
+        res, done = coracle.search_mt(ih, k['target'], 1, 1 << 40, threads=os.cpu_count() or 4)
+        assert res == (k['trial'], k['nonce']), k['note']
+        assert done >= k['nonce'] - 1
+
+
+def test_first_nonce_kats_python_restatement(golden):
+    for k in golden('first_nonce_kats.json')['kats']:
+        if k['nonce'] > 20000:
+            continue
+        ih = bytes.fromhex(k['ih'])
+        assert oracle.safe_pow(k['target'], ih) == [k['trial'], k['nonce']]
+
+
+def test_batch_kats(golden, coracle):
+    d = golden('batch_kats.json')
+    rng = random.Random(d['seed'])
+    for k in d['kats']:
+        payload = rng.randbytes(k['L'])
+        ih = hashlib.sha512(payload).digest()
+        assert ih.hex() == k['ih']
+        tgt = oracle.target_from_formula(k['L'], d['ttl'], d['ntpb'], d['extra'])
+        assert tgt == k['target']
+        assert coracle.search(ih, tgt) == (k['trial'], k['nonce'])
+
+
+def test_search_budget_and_resume(coracle):
+    ih = hashlib.sha512(b'hello').digest()
+    assert coracle.search(ih, U64 // 1000, 1, 1314) is None
+    assert coracle.search(ih, U64 // 1000, 1315, 1) == (2417842470843601, 1315)
+
+
+def test_search_mt_exact_vs_sequential(coracle):
+    rng = random.Random(11)
+    for _ in range(12):
+        ih = rng.randbytes(64)
+        tgt = U64 // rng.choice([50, 500, 5000, 50000])
+        seq = coracle.search(ih, tgt)
+        mt, _ = coracle.search_mt(ih, tgt, 1, 1 << 30, threads=4)
+        assert seq == mt
+
+
+def test_search_top_of_nonce_space(coracle):
+    ih = hashlib.sha512(b'edge').digest()
+    start = U64 - 300
+    tv = [coracle.trial(n, ih) for n in range(start, U64)]
+    m = min(tv)
+    want = start + tv.index(m)
+    assert coracle.search(ih, m, start, 1000) == (m, want)
+    res, done = coracle.search_mt(ih, m, start, 1 << 20, threads=3)
+    assert res == (m, want)
+    # nothing at or below target 0 in the last 300 nonces: budget stops at 2^64-1
+    assert coracle.search(ih, 0, start, 1000) is None
+    assert coracle.search_mt(ih, 0, start, 1 << 20, threads=3)[1] == 300
+
+
+@pytest.mark.skipif(not oracle.have_ref(), reason='oracle/_ref/bitmsghash.so not built')
+def test_reference_c_library_returns_a_valid_nonce():
+    """The reference's BitmessagePOW is nondeterministic and strict-<:
+    only validity is checked, never equality with _doSafePoW."""
+    ref = oracle.RefBitmsghash()
+    ih = hashlib.sha512(b'hello').digest()
+    tv, nonce = ref.pow(U64 // 1000, ih)
+    assert tv < U64 // 1000 and nonce >= 1
+    assert oracle.trial(nonce, ih) == tv
+
+
+def test_config_targets_formula(golden):
+    for t in golden('config_targets.json')['targets']:
+        if t['kind'] == 'singleWorker':
+            got = oracle.target_from_formula(t['L'], t['ttl'], t['ntpb'], t['extra'])
+            assert got == t['target']
+    c1 = [t for t in golden('config_targets.json')['targets'] if t['L'] == 1024 and t.get('ttl') == 345600
+          and t['ntpb'] == 1000][0]
+    assert c1['target'] == 1447073009577
