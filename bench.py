@@ -298,6 +298,16 @@ def main():
     runner = {'c1': run_c1_bench, 'c2': run_batch_bench, 'c3': run_c3_bench, 'c4': run_batch_bench,
               'c5': run_batch_bench}[args.config]
     r = runner(args, dist)
+    line = summarize(args, dist, r, lib.bmpow_version().decode())
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+        line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_threads)
+    if dist.rank == 0:
+        print(json.dumps(line), flush=True)
+    dist.close()
+
+
+def summarize(args, dist, r, lib_version):
+    """Whole-job line: max-over-ranks wall time, sum-over-ranks work (every rank calls it)."""
     st = r['stats']
     el_max = dist.reduce(r['elapsed'], 'max')
     useful = dist.reduce(r['useful'], 'sum')
@@ -320,7 +330,7 @@ def main():
         'data': 'synthetic',
         'config': {'workload': r['desc'], 'objects_per_rank_per_step': r['objects'] // max(args.steps, 1),
                    'parallelism': 'object-sharded dp%d (one process per GPU, no collective)' % dist.world,
-                   'block': 256, 'lib': lib.bmpow_version().decode()},
+                   'block': 256, 'lib': lib_version},
         'objects_per_s': round(objects / el_max, 3),
         'performed_ghs': round(performed / el_max / 1e9, 4),
         'wasted_frac': round(1.0 - useful / performed, 5) if performed else None,
@@ -336,11 +346,7 @@ def main():
             'avg_launch_ms': round(kernel_ms / max(launches, 1), 3), 'launches': int(launches),
             'kernel_busy_frac': round(kernel_ms * 1e-3 / r['elapsed'], 4),
         }
-    if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
-        line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_threads)
-    if dist.rank == 0:
-        print(json.dumps(line), flush=True)
-    dist.close()
+    return line
 
 
 if __name__ == '__main__':

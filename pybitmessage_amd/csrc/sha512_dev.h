@@ -75,13 +75,56 @@ BM_DEV uint64_t shr(uint64_t x) {
   return mk64(__builtin_amdgcn_alignbit(h, l, N), h >> N);
 }
 
+// ---- 3-input bitwise functions as one v_bitop3_b32 per 32-bit half ----
+// Measured on MI355X (tools/ubench_valu.hip): v_bitop3_b32 issues at ~77 lane-ops/clk/CU,
+// v_xor_b32 at ~118 and v_bfi_b32 at ~63, so one bitop3 (1/77) beats the xor pair the
+// compiler selects for a^b^c (2/118) and the bfi it selects for Ch.  hipcc does not form
+// bitop3 for two-op trees by itself, hence the builtin.  LUT bits: S0 = 0xF0, S1 = 0xCC,
+// S2 = 0xAA.  Operands that are compile-time constants fold through plain C instead (the
+// builtin is opaque to constant folding).
+template <uint8_t LUT>
+BM_DEV uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
+  if (__builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c)) {
+    uint32_t r = 0;
+    for (int i = 0; i < 32; ++i) {
+      const int idx = (((a >> i) & 1) << 2) | (((b >> i) & 1) << 1) | ((c >> i) & 1);
+      r |= (uint32_t)((LUT >> idx) & 1) << i;
+    }
+    return r;
+  }
+  return __builtin_amdgcn_bitop3_b32(a, b, c, LUT);
+}
+
+// A 64-bit value rebuilt from two 32-bit halves is ((u64)hi << 32) | lo to LLVM, which
+// rewrites the OR as an ADD and then reassociates every following 64-bit add into separate
+// lo/hi adds (measured: +35% v_lshl_add_u64 and ~850 extra v_mov per trial).  An empty asm
+// with a read-write VGPR-pair operand makes the pair opaque at zero instruction cost.
+BM_DEV uint64_t opaque(uint64_t x) {
+  if (__builtin_constant_p(x)) return x;
+  asm("" : "+v"(x));
+  return x;
+}
+
+template <uint8_t LUT>
+BM_DEV uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
+  return opaque(mk64(bitop3<LUT>(lo32(a), lo32(b), lo32(c)), bitop3<LUT>(hi32(a), hi32(b), hi32(c))));
+}
+
+BM_DEV uint64_t xor3(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0x96>(a, b, c); }
+
 // FIPS 180-4 4.1.3 functions.
-BM_DEV uint64_t Sig0(uint64_t a) { return rotr<28>(a) ^ rotr<34>(a) ^ rotr<39>(a); }
-BM_DEV uint64_t Sig1(uint64_t e) { return rotr<14>(e) ^ rotr<18>(e) ^ rotr<41>(e); }
-BM_DEV uint64_t sig0(uint64_t w) { return rotr<1>(w) ^ rotr<8>(w) ^ shr<7>(w); }
-BM_DEV uint64_t sig1(uint64_t w) { return rotr<19>(w) ^ rotr<61>(w) ^ shr<6>(w); }
-BM_DEV uint64_t Ch(uint64_t e, uint64_t f, uint64_t g) { return g ^ (e & (f ^ g)); }
-BM_DEV uint64_t Maj(uint64_t a, uint64_t b, uint64_t c) { return (a & b) | (c & (a | b)); }
+BM_DEV uint64_t Sig0(uint64_t a) { return xor3(rotr<28>(a), rotr<34>(a), rotr<39>(a)); }
+BM_DEV uint64_t Sig1(uint64_t e) { return xor3(rotr<14>(e), rotr<18>(e), rotr<41>(e)); }
+BM_DEV uint64_t sig0(uint64_t w) {
+  if (__builtin_constant_p(w)) return (w >> 1 | w << 63) ^ (w >> 8 | w << 56) ^ (w >> 7);
+  return xor3(rotr<1>(w), rotr<8>(w), shr<7>(w));
+}
+BM_DEV uint64_t sig1(uint64_t w) {
+  if (__builtin_constant_p(w)) return (w >> 19 | w << 45) ^ (w >> 61 | w << 3) ^ (w >> 6);
+  return xor3(rotr<19>(w), rotr<61>(w), shr<6>(w));
+}
+BM_DEV uint64_t Ch(uint64_t e, uint64_t f, uint64_t g) { return bitop3_64<0xCA>(e, f, g); }
+BM_DEV uint64_t Maj(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0xE8>(a, b, c); }
 
 // constexpr twins (host + device) for compile-time folding of IV-only expressions.
 constexpr uint64_t crotr(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }

@@ -1,0 +1,68 @@
+"""Multi-rank bench plumbing on CPU (gloo, world_size 2): object sharding by rank and the
+whole-job aggregation (max-over-ranks time, sum-over-ranks work).  The data path has no
+collective; gloo carries only timing."""
+import json
+import os
+import socket
+import types
+
+import pytest
+
+torch = pytest.importorskip('torch')
+import torch.multiprocessing as mp  # noqa: E402
+
+import bench  # noqa: E402
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, outdir):
+    os.environ.update({'RANK': str(rank), 'LOCAL_RANK': str(rank), 'WORLD_SIZE': str(world),
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
+    d = bench.Dist()
+    objs, _ = bench.make_objects('c2', d.rank, 8)
+    stats = types.SimpleNamespace(trials=1000 * (rank + 1), kernel_ms=10.0 * (rank + 1), launches=2)
+    r = {'desc': 'test', 'objects': 8, 'useful': 900.0 * (rank + 1), 'elapsed': 1.0 + rank, 'stats': stats}
+    args = types.SimpleNamespace(steps=1, warmup=0)
+    d.barrier()
+    line = bench.summarize(args, d, r, 'test-lib')
+    with open(os.path.join(outdir, 'rank%d.json' % rank), 'w') as f:
+        json.dump({'line': line, 'first_ih': objs[0][1].hex()}, f)
+    d.close()
+
+
+def test_two_rank_aggregation(tmp_path):
+    port = _free_port()
+    mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = json.load(open(tmp_path / 'rank0.json'))
+    r1 = json.load(open(tmp_path / 'rank1.json'))
+    line = r0['line']
+    assert line['n_gpus'] == 2 and line['scaling'] == 'weak'
+    # value = (900 + 1800) useful trials / max(1.0, 2.0) s, in GH/s
+    assert line['value'] == round(2700 / 2.0 / 1e9, 4)
+    assert line['objects_per_s'] == round(16 / 2.0, 3)
+    assert line['performed_ghs'] == round(3000 / 2.0 / 1e9, 4)
+    assert r1['line']['value'] == line['value']  # every rank sees the same reduction
+    # each rank works on its own batch (seed + rank): no object is solved twice
+    assert r0['first_ih'] != r1['first_ih']
+
+
+def test_c2_workload_is_deterministic():
+    a, da = bench.make_objects('c2', 0, 16)
+    b, _ = bench.make_objects('c2', 0, 16)
+    assert a == b and 'C2' in da
+    full, _ = bench.make_objects('c2', 0)
+    assert len(full) == 1024
+    assert full[:16] == a
+    # targets follow the singleWorker formula with TTL 4 d at default difficulty
+    from pybitmessage_amd.targets import object_target
+    import random
+    rng = random.Random(bench.SEED)
+    L = rng.randrange(512, 16385)
+    assert a[0][0] == int(object_target(L, 345600))
