@@ -346,7 +346,26 @@ def summarize(args, dist, r, lib_version):
             'avg_launch_ms': round(kernel_ms / max(launches, 1), 3), 'launches': int(launches),
             'kernel_busy_frac': round(kernel_ms * 1e-3 / r['elapsed'], 4),
         }
+        pmc = pmc_traffic()
+        if pmc:
+            line['roofline'].update(pmc)
     return line
+
+
+def pmc_traffic():
+    """HBM bytes per bm_search_kernel launch from the committed rocprofv3 PMC passes
+    (tools/profile_pmc.sh -> tools/pmc_summary.py -> profiles/pmc_latest.json): FETCH_SIZE
+    doubled (gfx950 under-count, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, KB -> bytes.  The
+    algorithmic traffic is ~0 (9 words per workgroup); the counters bound the real traffic."""
+    path = os.path.join(ROOT, 'profiles', 'pmc_latest.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)['derived']
+    return {'traffic': d.get('hbm_bytes_per_launch_upper'),
+            'traffic_source': 'profiles/pmc_latest.json (C3 launches of 2^28 trials)',
+            'valu_instr_per_trial_pmc': round(d.get('valu_instr_per_trial', 0), 1),
+            'eff_clock_ghz_pmc': round(d.get('eff_clock_ghz', 0), 3)}
 
 
 if __name__ == '__main__':
