@@ -38,9 +38,19 @@ METRIC = "double-SHA512 PoW trials/sec (GH/s, node) at 1/2/4/8 GPUs; objects PoW
 SEED = 20250216
 #: algorithmic int32 lane-ops per trial: 2 blocks x (80 x 34 + 64 x 22 + 16)
 OPS_PER_TRIAL = 8288
-#: integer VALU peak, T lane-ops/s: 256 CUs x 64 lane-ops/clk (the VOP3-class issue rate of
-#: v_alignbit_b32 / v_lshl_add_u64 / v_bfi_b32, measured 38.7 T by tools/ubench_valu.hip) x 2.4 GHz
-PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
+#: vector-ALU peak, T int32 lane-ops/s: 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz -- the rate
+#: behind MI355X_MICROARCH.md's 157.3 TFLOPS FP32 vector peak (one wave64 VALU op per 2 cycles).
+PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
+#: BASELINE.md section 3 priced the roofline at 64 lanes/clk/CU (39.32 T); kept for comparison
+BASELINE_MD_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
+#: issued instructions per trial of bm_search_kernel (tools/isa_census.py on the gfx950 ISA) and
+#: their measured issue rates, lane-ops/clk/CU (tools/ubench_valu.hip, profiles/r01_ubench_valu.json).
+#: v_alignbit_b32, v_lshl_add_u64 and v_bitop3_b32 have no full-rate encoding, so the trial's
+#: instruction mix, not PEAK_TOPS, is the ceiling this kernel can reach.
+ISA_MIX = {'v_alignbit_b32': (3041, 63.2), 'v_bitop3_b32': (1722, 76.6), 'v_lshl_add_u64': (1434, 63.1),
+           'v_lshrrev_b32': (229, 117.8), 'other': (50, 117.8)}
+#: CU-clocks per trial = sum(count / rate); x 256 CUs -> trials per clock of the chip
+ISSUE_CLK_PER_TRIAL_PER_CU = sum(c / r for c, r in ISA_MIX.values())
 
 
 def object_target(L, ttl, ntpb=1000, extra=1000):
@@ -337,18 +347,25 @@ def summarize(args, dist, r, lib_version):
     }
     if kernel_ms > 0:
         achieved = OPS_PER_TRIAL * st.trials / (kernel_ms * 1e-3) / 1e12
+        kernel_ghs = st.trials / (kernel_ms * 1e-3) / 1e9
         line['roofline'] = {
             'bound': 'valu', 'kernel': 'bm_search_kernel',
             'achieved': round(achieved, 3), 'peak': round(PEAK_TOPS, 3),
             'unit': 'T int32 lane-ops/s (8,288 algorithmic ops per trial)',
             'frac': round(achieved / PEAK_TOPS, 4), 'traffic': None,
-            'kernel_ghs': round(st.trials / (kernel_ms * 1e-3) / 1e9, 4),
+            'kernel_ghs': round(kernel_ghs, 4),
             'avg_launch_ms': round(kernel_ms / max(launches, 1), 3), 'launches': int(launches),
             'kernel_busy_frac': round(kernel_ms * 1e-3 / r['elapsed'], 4),
+            'frac_vs_baseline_md_peak': round(achieved / BASELINE_MD_PEAK_TOPS, 4),
         }
         pmc = pmc_traffic()
         if pmc:
             line['roofline'].update(pmc)
+        clk = (pmc or {}).get('eff_clock_ghz_pmc') or 2.4
+        ceiling = 256 * clk * 1e9 / ISSUE_CLK_PER_TRIAL_PER_CU / 1e9
+        line['roofline']['issue_ceiling'] = {
+            'ghs': round(ceiling, 4), 'clock_ghz': clk, 'frac': round(kernel_ghs / ceiling, 4),
+            'basis': 'per-trial instruction mix of the gfx950 ISA x measured issue rates (bench.ISA_MIX)'}
     return line
 
 
