@@ -230,6 +230,88 @@ def run_c1_bench(args, dist):
             'objects': args.steps, 'useful': float(nonce) * args.steps, 'elapsed': elapsed, 'stats': st}
 
 
+def verify_objects(n, rank):
+    """Receive-side flood: finished objects as they arrive from the network,
+    half acks (54 B), a quarter pubkey-size (208 B), a quarter msgs (L ~ U[512, 16384])."""
+    rng = random.Random(SEED + 1000 + rank)
+    objs = []
+    for i in range(n):
+        r = i % 4
+        L = 46 if r in (0, 1) else (200 if r == 2 else rng.randrange(512, 16385))
+        objs.append(rng.randbytes(8) + (1700000000 + 345600).to_bytes(8, 'big') + rng.randbytes(L - 8))
+    return objs
+
+
+def run_verify_bench(args, dist):
+    """POW values of a resident flood, one bv_pow_kernel pass per step (bmpow_vbatch_run)."""
+    import ctypes
+
+    from pybitmessage_amd import _lib, targets, verify
+    n = args.objects or 200000
+    objs = verify_objects(n, dist.rank)
+    payload_bytes = sum(len(o) - 8 for o in objs)
+    lib = _lib.get()
+    with verify.VerifyBatch(objs) as vb:
+        first = vb.run()
+        for i in range(0, n, max(1, n // 500)):  # spot-check against hashlib
+            assert int(first[i]) == targets.pow_value(objs[i]), i
+        for _ in range(args.warmup):
+            vb.run(want=False)
+        dist.barrier()
+        lib.bmpow_reset_stats()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            vb.run(want=False)
+        dist.barrier()
+        elapsed = time.perf_counter() - t0
+    st = _lib.BmpowStats()
+    lib.bmpow_get_stats(ctypes.byref(st))
+    return {'desc': 'verify: %d received objects (50%% acks, 25%% pubkeys, 25%% msgs 0.5-16 KB), POW of each '
+                    '(protocol.isProofOfWorkSufficient hashing) resident in HBM' % n,
+            'objects': n * args.steps, 'elapsed': elapsed, 'stats': st, 'payload_bytes': payload_bytes * args.steps}
+
+
+def summarize_verify(args, dist, r, lib_version):
+    st = r['stats']
+    el_max = dist.reduce(r['elapsed'], 'max')
+    objects = dist.reduce(r['objects'], 'sum')
+    nbytes = dist.reduce(r['payload_bytes'], 'sum')
+    line = {
+        'metric': 'received objects verified/sec (protocol.isProofOfWorkSufficient POW, GPU batch)',
+        'value': round(objects / el_max, 1), 'unit': 'objects/s', 'n_gpus': dist.world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(el_max * 1e3 / args.steps, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u64', 'data': 'synthetic',
+        'config': {'workload': r['desc'], 'parallelism': 'object-sharded dp%d' % dist.world, 'lib': lib_version},
+        'payload_GBps': round(nbytes / el_max / 1e9, 3),
+    }
+    if st.verify_kernel_ms > 0:
+        # algorithmic ops: 4,144 per 128-B payload block (SURVEY 8(d) per-block count) + 8,288 for
+        # the outer double hash of each object
+        ops = 4144 * st.verify_blocks + OPS_PER_TRIAL * st.verify_objects
+        achieved = ops / (st.verify_kernel_ms * 1e-3) / 1e12
+        line['roofline'] = {'bound': 'valu', 'kernel': 'bv_pow_kernel', 'achieved': round(achieved, 3),
+                            'peak': round(PEAK_TOPS, 3), 'unit': 'T int32 lane-ops/s', 'frac': round(achieved / PEAK_TOPS, 4),
+                            'traffic': None, 'blocks_per_s': round(st.verify_blocks / (st.verify_kernel_ms * 1e-3), 1),
+                            'avg_launch_ms': round(st.verify_kernel_ms / max(args.steps, 1), 3),
+                            'kernel_busy_frac': round(st.verify_kernel_ms * 1e-3 / r['elapsed'], 4)}
+    return line
+
+
+def cpu_verify_baseline(seconds):
+    """The reference's per-object check restated with hashlib (targets.pow_value is the
+    protocol.py:280-282 expression), one core, on the same flood."""
+    from pybitmessage_amd import targets
+    objs = verify_objects(20000, 0)
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        targets.pow_value(objs[k % len(objs)])
+        k += 1
+    el = time.perf_counter() - t0
+    return {'value': round(k / el, 1), 'unit': 'objects/s', 'cores': 1, 'kind': 'port',
+            'sample': '%d objects of the same flood hashed by hashlib (OpenSSL) in %.1f s, 1 thread' % (k, el)}
+
+
 # ----------------------------------------------------------------------------------------
 # CPU baseline (rank 0, N=1): the reference's own BitmessagePOW built from its source
 # ----------------------------------------------------------------------------------------
@@ -285,7 +367,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--config', default='c2', choices=['c1', 'c2', 'c3', 'c4', 'c5'])
+    ap.add_argument('--config', default='c2', choices=['c1', 'c2', 'c3', 'c4', 'c5', 'verify'])
     ap.add_argument('--objects', type=int, default=None, help='override the object count (c2/c4/c5)')
     ap.add_argument('--c3-log2', type=int, default=36)
     ap.add_argument('--step-trials', type=int, default=0, help='per-launch trial budget per GPU (0 = lib default)')
@@ -305,6 +387,15 @@ def main():
     if args.step_trials:
         lib.bmpow_set_step_trials(args.step_trials)
 
+    if args.config == 'verify':
+        r = run_verify_bench(args, dist)
+        line = summarize_verify(args, dist, r, lib.bmpow_version().decode())
+        if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+            line['cpu_baseline'] = cpu_verify_baseline(min(args.cpu_seconds, 10.0))
+        if dist.rank == 0:
+            print(json.dumps(line), flush=True)
+        dist.close()
+        return
     runner = {'c1': run_c1_bench, 'c2': run_batch_bench, 'c3': run_c3_bench, 'c4': run_batch_bench,
               'c5': run_batch_bench}[args.config]
     r = runner(args, dist)

@@ -123,6 +123,42 @@ BMPOW_API int bmpow_batch_reset(bmpow_batch *b, const uint64_t *start);
 
 BMPOW_API void bmpow_batch_destroy(bmpow_batch *b);
 
+/* ---- receive-side verification (replaces protocol.isProofOfWorkSufficient,
+ *      src/protocol.py:258-286, called once per received object from
+ *      src/network/bmobject.py:71-76) ----
+ *
+ * Objects are finished objects as they travel: nonce (8 bytes, big-endian) || payload, passed
+ * as one concatenated buffer `objs` with byte offsets[0..n] (object i = objs[offsets[i] ..
+ * offsets[i+1])).  POW(i) = BE64(SHA512(SHA512(obj[0:8] || SHA512(obj[8:])))[0:8])
+ * (protocol.py:280-282), computed one object per GPU lane, objects spread over the active
+ * devices. */
+
+/* POW values of n objects (each >= 8 bytes).  Returns 0 or < 0. */
+BMPOW_API int bmpow_pow_values(size_t n, const uint8_t *objs, const uint64_t *offsets, uint64_t *pow_out);
+
+/* isProofOfWorkSufficient for n objects: ntpb[i]/extra[i] (NULL = 0; raised to the network
+ * defaults 1000/1000 as protocol.py:272-275 does), recv_time[i] (NULL or 0 = now, :277);
+ * TTL = expiresTime (obj[8:16]) - recv_time, at least 300 s; ok_out[i] = 1 when
+ * POW <= 2^64 / (ntpb * (len + extra + TTL * (len + extra) / 2^16)) in the reference's IEEE
+ * double arithmetic, 0 when not, 2 when the object is shorter than 16 bytes (the reference
+ * raises struct.error there).  Returns 0 or < 0. */
+BMPOW_API int bmpow_verify_batch(size_t n, const uint8_t *objs, const uint64_t *offsets, const uint64_t *ntpb,
+                                 const uint64_t *extra, const int64_t *recv_time, uint8_t *ok_out);
+
+/* The verdict arithmetic alone, on the host (no device): 1 when `pow` is sufficient for an
+ * object of `len` bytes (nonce included) with expiresTime `expires`, received at `recv_time`
+ * (0 = now), else 0 -- the comparison bmpow_verify_batch applies (protocol.py:272-286). */
+BMPOW_API int bmpow_pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, int64_t recv_time,
+                                   uint64_t expires);
+
+/* Device-resident verification session: pad, sort and upload the objects once, then hash
+ * them repeatedly (bench.py times bmpow_vbatch_run with the payloads resident in HBM). */
+typedef struct bmpow_vbatch bmpow_vbatch;
+BMPOW_API bmpow_vbatch *bmpow_vbatch_create(size_t n, const uint8_t *objs, const uint64_t *offsets);
+/* One pass over every object; pow_out (n, input order) may be NULL.  Returns 0 or < 0. */
+BMPOW_API int bmpow_vbatch_run(bmpow_vbatch *vb, uint64_t *pow_out);
+BMPOW_API void bmpow_vbatch_destroy(bmpow_vbatch *vb);
+
 /* ---- instrumentation (bench.py's roofline leg) ---- */
 typedef struct bmpow_stats {
     uint64_t launches;        /* search-kernel launches (summed over shards) */
@@ -131,6 +167,11 @@ typedef struct bmpow_stats {
                                  launching stream */
     double max_shard_kernel_ms; /* max over shards of their summed kernel time */
     uint64_t steps;           /* host scheduler steps */
+    /* receive-side verification (bmpow_pow_values / bmpow_verify_batch / bmpow_vbatch_run) */
+    uint64_t verify_launches; /* bv_pow_kernel launches (summed over shards) */
+    uint64_t verify_objects;  /* objects hashed */
+    uint64_t verify_blocks;   /* 128-B SHA-512 blocks of payload hashed (padding included) */
+    double verify_kernel_ms;  /* max over shards per run, summed over runs (HIP events) */
 } bmpow_stats;
 
 BMPOW_API int bmpow_get_stats(bmpow_stats *out);

@@ -42,7 +42,9 @@ class BmpowUnavailable(BmpowError):
 class BmpowStats(ctypes.Structure):
     _fields_ = [('launches', ctypes.c_uint64), ('trials', ctypes.c_uint64),
                 ('kernel_ms', ctypes.c_double), ('max_shard_kernel_ms', ctypes.c_double),
-                ('steps', ctypes.c_uint64)]
+                ('steps', ctypes.c_uint64), ('verify_launches', ctypes.c_uint64),
+                ('verify_objects', ctypes.c_uint64), ('verify_blocks', ctypes.c_uint64),
+                ('verify_kernel_ms', ctypes.c_double)]
 
 
 # (name, restype, argtypes) for every symbol include/bmpow.h declares
@@ -71,6 +73,13 @@ SIGNATURES = [
     ('bmpow_reset_stats', None, []),
     ('bmpow_get_step_trials', _u64, []),
     ('bmpow_set_step_trials', None, [_u64]),
+    ('bmpow_pow_values', ctypes.c_int, [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64]),
+    ('bmpow_verify_batch', ctypes.c_int,
+     [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _p64, ctypes.POINTER(ctypes.c_int64), _pu8]),
+    ('bmpow_pow_sufficient', ctypes.c_int, [_u64, _u64, _u64, _u64, ctypes.c_int64, _u64]),
+    ('bmpow_vbatch_create', _vp, [ctypes.c_size_t, ctypes.c_char_p, _p64]),
+    ('bmpow_vbatch_run', ctypes.c_int, [_vp, _p64]),
+    ('bmpow_vbatch_destroy', None, [_vp]),
     ('BitmessagePOW', ctypes.c_ulonglong, [ctypes.c_char_p, ctypes.c_ulonglong]),
 ]
 

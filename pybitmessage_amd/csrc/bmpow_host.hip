@@ -22,6 +22,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -406,6 +407,185 @@ int scratch_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, const u
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------
+// Receive-side verification session.  Layout per shard, device resident:
+//   pool[blocks]  : every payload (object[8:]) SHA-512-padded to whole 128-B blocks, objects
+//                   back to back in sorted order (so one lane reads one contiguous run)
+//   obj[k]        : {first block, block count, nonce} of the k-th object in sorted order
+//   pow[k]        : result
+// Objects are sorted by block count (descending) so a wave's lanes iterate alike, and the
+// sorted list is cut into per-shard slices of equal block totals.
+// ---------------------------------------------------------------------------------------
+struct bmpow_vbatch {
+  size_t n = 0;
+  struct Part {
+    size_t shard = 0;
+    std::vector<uint32_t> orig;  // sorted position -> input index
+    uint64_t blocks = 0;
+    bv_obj* d_obj = nullptr;
+    uint4* d_pool = nullptr;
+    uint64_t* d_pow = nullptr;
+    uint64_t* h_pow = nullptr;  // pinned
+  };
+  std::vector<Part> parts;
+  uint64_t blocks = 0;
+};
+
+namespace {
+
+struct Span {
+  const uint8_t* p;
+  uint64_t len;  // >= 8
+};
+
+uint64_t load_be64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int j = 0; j < 8; ++j) v = (v << 8) | p[j];
+  return v;
+}
+
+// blocks of SHA-512 padding for an m-byte message: m + 1 (0x80) + 16 (bit length) rounded up
+uint64_t padded_blocks(uint64_t m) { return (m + 17 + 127) / 128; }
+
+void pad_into(const uint8_t* msg, uint64_t m, uint8_t* dst, uint64_t nblk) {
+  const uint64_t total = nblk * 128;
+  std::memcpy(dst, msg, m);
+  std::memset(dst + m, 0, total - m);
+  dst[m] = 0x80;
+  const uint64_t bits_lo = m << 3, bits_hi = m >> 61;  // 128-bit big-endian bit length
+  for (int j = 0; j < 8; ++j) {
+    dst[total - 16 + j] = (uint8_t)(bits_hi >> (56 - 8 * j));
+    dst[total - 8 + j] = (uint8_t)(bits_lo >> (56 - 8 * j));
+  }
+}
+
+void vbatch_free(bmpow_vbatch* vb) {
+  for (auto& pt : vb->parts) {
+    if (pt.shard < g_shards.size()) (void)hipSetDevice(g_shards[pt.shard].dev);
+    if (pt.d_obj) (void)hipFree(pt.d_obj);
+    if (pt.d_pool) (void)hipFree(pt.d_pool);
+    if (pt.d_pow) (void)hipFree(pt.d_pow);
+    if (pt.h_pow) (void)hipHostFree(pt.h_pow);
+  }
+  vb->parts.clear();
+}
+
+int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs) {
+  const size_t n = objs.size();
+  if (n > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many objects");
+  vb->n = n;
+  std::vector<uint32_t> nblk(n);
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t b = padded_blocks(objs[i].len - 8);
+    if (b > 0xffffffffULL) return set_err(BMPOW_E_ARG, "object too large");
+    nblk[i] = (uint32_t)b;
+    total += b;
+  }
+  if (total > 0xffffffffULL) return set_err(BMPOW_E_ARG, "payload pool above 2^32 blocks (512 GiB)");
+  vb->blocks = total;
+  std::vector<uint32_t> order(n);
+  for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return nblk[a] > nblk[b]; });
+  const size_t S = g_shards.size();
+  size_t k = 0;
+  uint64_t acc = 0;
+  for (size_t s = 0; s < S && k < n; ++s) {
+    bmpow_vbatch::Part pt;
+    pt.shard = s;
+    const uint64_t goal = total * (s + 1) / S;
+    while (k < n && (acc < goal || s == S - 1)) {
+      pt.orig.push_back(order[k]);
+      pt.blocks += nblk[order[k]];
+      acc += nblk[order[k]];
+      ++k;
+    }
+    if (!pt.orig.empty()) vb->parts.push_back(std::move(pt));
+  }
+  for (auto& pt : vb->parts) {
+    Shard& sh = g_shards[pt.shard];
+    HIPTRY(hipSetDevice(sh.dev));
+    const size_t m = pt.orig.size();
+    std::vector<bv_obj> ho(m);
+    std::vector<uint8_t> pool(pt.blocks * 128);
+    uint64_t blk = 0;
+    for (size_t j = 0; j < m; ++j) {
+      const Span& sp = objs[pt.orig[j]];
+      const uint32_t nb = nblk[pt.orig[j]];
+      pad_into(sp.p + 8, sp.len - 8, pool.data() + blk * 128, nb);
+      ho[j].blk = (uint32_t)blk;
+      ho[j].nblk = nb;
+      ho[j].nonce = load_be64(sp.p);
+      blk += nb;
+    }
+    HIPTRY(hipMalloc(&pt.d_obj, m * sizeof(bv_obj)));
+    HIPTRY(hipMalloc(&pt.d_pool, std::max<size_t>(pool.size(), 16)));
+    HIPTRY(hipMalloc(&pt.d_pow, m * sizeof(uint64_t)));
+    HIPTRY(hipHostMalloc(&pt.h_pow, m * sizeof(uint64_t), hipHostMallocDefault));
+    HIPTRY(hipMemcpy(pt.d_obj, ho.data(), m * sizeof(bv_obj), hipMemcpyHostToDevice));
+    HIPTRY(hipMemcpy(pt.d_pool, pool.data(), pool.size(), hipMemcpyHostToDevice));
+  }
+  return 0;
+}
+
+int vbatch_run_locked(bmpow_vbatch* vb, uint64_t* pow_out) {
+  for (auto& pt : vb->parts) {
+    Shard& sh = g_shards[pt.shard];
+    HIPTRY(hipSetDevice(sh.dev));
+    HIPTRY(hipEventRecord(sh.ev0, sh.stream));
+    HIPTRY(bv_launch_pow(sh.stream, pt.d_obj, (uint32_t)pt.orig.size(), pt.d_pool, pt.d_pow));
+    HIPTRY(hipEventRecord(sh.ev1, sh.stream));
+    HIPTRY(hipMemcpyAsync(pt.h_pow, pt.d_pow, pt.orig.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, sh.stream));
+  }
+  double mx = 0;
+  for (auto& pt : vb->parts) {
+    Shard& sh = g_shards[pt.shard];
+    HIPTRY(hipSetDevice(sh.dev));
+    HIPTRY(hipStreamSynchronize(sh.stream));
+    float ms = 0;
+    HIPTRY(hipEventElapsedTime(&ms, sh.ev0, sh.ev1));
+    mx = std::max<double>(mx, ms);
+    g_stats.verify_launches++;
+    if (pow_out)
+      for (size_t j = 0; j < pt.orig.size(); ++j) pow_out[pt.orig[j]] = pt.h_pow[j];
+  }
+  g_stats.verify_kernel_ms += mx;
+  g_stats.verify_objects += vb->n;
+  g_stats.verify_blocks += vb->blocks;
+  return 0;
+}
+
+int spans_from(size_t n, const uint8_t* objs, const uint64_t* offsets, std::vector<Span>& out) {
+  if (n && (!objs || !offsets)) return set_err(BMPOW_E_ARG, "null pointer");
+  out.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i] + 8) return set_err(BMPOW_E_ARG, "object shorter than its 8-byte nonce");
+    out[i] = {objs + offsets[i], offsets[i + 1] - offsets[i]};
+  }
+  return 0;
+}
+
+// protocol.isProofOfWorkSufficient's comparison (src/protocol.py:272-286) in the reference's
+// arithmetic: Python ints until the true division by 2**16 (correctly rounded: the exact
+// 128-bit product converted once, then an exact power-of-two scale), IEEE doubles after,
+// and an exact int-vs-float comparison at the end.
+int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, int64_t recv, uint64_t eol) {
+  if (ntpb < 1000) ntpb = 1000;
+  if (extra < 1000) extra = 1000;
+  __int128 ttl = (__int128)eol - (__int128)recv;
+  if (ttl < 300) ttl = 300;
+  const unsigned __int128 le = (unsigned __int128)len + extra;
+  const unsigned __int128 prod = (unsigned __int128)ttl * le;
+  const double q = (double)prod / 65536.0;
+  const double x = (double)le + q;
+  const double y = (double)ntpb * x;
+  const double t = 18446744073709551616.0 / y;
+  if (t >= 18446744073709551616.0) return 1;
+  return pow <= (uint64_t)t ? 1 : 0;
+}
+
+}  // namespace
+
 // =======================================================================================
 // C ABI
 // =======================================================================================
@@ -630,6 +810,96 @@ void bmpow_batch_destroy(bmpow_batch* b) {
   if (!b) return;
   batch_free_dev(b);
   delete b;
+}
+
+bmpow_vbatch* bmpow_vbatch_create(size_t n, const uint8_t* objs, const uint64_t* offsets) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (init_locked() < 0) return nullptr;
+  std::vector<Span> spans;
+  if (spans_from(n, objs, offsets, spans) < 0) return nullptr;
+  bmpow_vbatch* vb = new bmpow_vbatch();
+  if (vbatch_build(vb, spans) < 0) {
+    vbatch_free(vb);
+    delete vb;
+    return nullptr;
+  }
+  return vb;
+}
+
+int bmpow_vbatch_run(bmpow_vbatch* vb, uint64_t* pow_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!vb) return set_err(BMPOW_E_STATE, "null verification batch");
+  for (auto& pt : vb->parts)
+    if (pt.shard >= g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
+  return vbatch_run_locked(vb, pow_out);
+}
+
+void bmpow_vbatch_destroy(bmpow_vbatch* vb) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!vb) return;
+  vbatch_free(vb);
+  delete vb;
+}
+
+int bmpow_pow_values(size_t n, const uint8_t* objs, const uint64_t* offsets, uint64_t* pow_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (n == 0) return 0;
+  if (!pow_out) return set_err(BMPOW_E_ARG, "null pointer");
+  std::vector<Span> spans;
+  rc = spans_from(n, objs, offsets, spans);
+  if (rc < 0) return rc;
+  bmpow_vbatch vb;
+  rc = vbatch_build(&vb, spans);
+  if (rc == 0) rc = vbatch_run_locked(&vb, pow_out);
+  vbatch_free(&vb);
+  return rc;
+}
+
+int bmpow_verify_batch(size_t n, const uint8_t* objs, const uint64_t* offsets, const uint64_t* ntpb,
+                       const uint64_t* extra, const int64_t* recv_time, uint8_t* ok_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (n == 0) return 0;
+  if (!objs || !offsets || !ok_out) return set_err(BMPOW_E_ARG, "null pointer");
+  std::vector<Span> spans;
+  std::vector<size_t> idx;
+  for (size_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i]) return set_err(BMPOW_E_ARG, "offsets are not ascending");
+    const uint64_t len = offsets[i + 1] - offsets[i];
+    if ((ntpb && ntpb[i] >= (1ULL << 62)) || (extra && extra[i] >= (1ULL << 62)))
+      return set_err(BMPOW_E_ARG, "nonceTrialsPerByte / payloadLengthExtraBytes above 2^62");
+    if (len < 16) {
+      ok_out[i] = 2;  // the reference's unpack('>Q', data[8:16]) raises struct.error
+      continue;
+    }
+    spans.push_back({objs + offsets[i], len});
+    idx.push_back(i);
+  }
+  std::vector<uint64_t> pow(spans.size());
+  if (!spans.empty()) {
+    bmpow_vbatch vb;
+    rc = vbatch_build(&vb, spans);
+    if (rc == 0) rc = vbatch_run_locked(&vb, pow.data());
+    vbatch_free(&vb);
+    if (rc < 0) return rc;
+  }
+  const int64_t now = (int64_t)std::time(nullptr);
+  for (size_t j = 0; j < spans.size(); ++j) {
+    const size_t i = idx[j];
+    const int64_t recv = (recv_time && recv_time[i]) ? recv_time[i] : now;
+    ok_out[i] = (uint8_t)pow_sufficient(pow[j], spans[j].len, ntpb ? ntpb[i] : 0, extra ? extra[i] : 0, recv,
+                                        load_be64(spans[j].p + 8));
+  }
+  return 0;
+}
+
+int bmpow_pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, int64_t recv_time,
+                         uint64_t expires) {
+  if (ntpb >= (1ULL << 62) || extra >= (1ULL << 62)) return set_err(BMPOW_E_ARG, "difficulty above 2^62");
+  return pow_sufficient(pow, len, ntpb, extra, recv_time ? recv_time : (int64_t)std::time(nullptr), expires);
 }
 
 int bmpow_get_stats(bmpow_stats* out) {

@@ -31,6 +31,18 @@ struct bm_result {
   uint64_t trial;
 };
 
+// Receive-side verification (bv_*): one finished object (nonce || payload) per lane.  The
+// payload is stored SHA-512-padded in a pool of 128-B blocks; objects are sorted by block
+// count (descending) on the host so the lanes of a wave loop the same number of times.
+#define BV_BLOCK 64
+struct bv_obj {
+  uint32_t blk;    // first 128-B block of the padded payload in the pool
+  uint32_t nblk;   // padded blocks (>= 1)
+  uint64_t nonce;  // BE64(object[0:8])
+};
+
+hipError_t bv_launch_pow(hipStream_t st, const bv_obj* objs, uint32_t n, const uint4* pool, uint64_t* pow_out);
+
 hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, const bm_obj* objs, const bm_item* items,
                             uint32_t nitems, unsigned long long* best, unsigned long long* trials_done);
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,

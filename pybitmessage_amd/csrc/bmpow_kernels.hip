@@ -76,6 +76,19 @@ BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
   return s2[0] + IV(0);
 }
 
+// One SHA-512 compression of a runtime block into the chaining state h.
+BM_DEV void compress(uint64_t (&h)[8], uint64_t (&w)[16]) {
+  uint64_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = h[i];
+  rounds<0, 80>(s, w);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] += s[i];
+}
+
+// Big-endian 64-bit word from a little-endian 16-byte load: bytes b0..b3 are in x, b4..b7 in y.
+BM_DEV uint64_t be64(uint32_t x, uint32_t y) { return mk64(__builtin_bswap32(y), __builtin_bswap32(x)); }
+
 }  // namespace bm
 
 using namespace bm;
@@ -158,6 +171,37 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_trials_kernel(const bm_obj* __res
 }
 
 // ---------------------------------------------------------------------------------------
+// Receive-side PoW value, reference src/protocol.py:280-282:
+//   POW = BE64(SHA512(SHA512(object[0:8] || SHA512(object[8:])))[0:8])
+// One lane per object.  The inner SHA512(object[8:]) runs over the host-padded blocks of the
+// pool (16-B loads, byte-swapped into the big-endian schedule words); its digest words are the
+// initialHash words of the trial function, so the outer double hash is trial_of(H, nonce).
+// Integer-VALU bound: ~3,300 VALU instructions per 128-B block, 0 bytes re-read.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(BV_BLOCK) void bv_pow_kernel(const bv_obj* __restrict__ objs, uint32_t n,
+                                                          const uint4* __restrict__ pool,
+                                                          uint64_t* __restrict__ pow_out) {
+  const uint32_t k = blockIdx.x * BV_BLOCK + threadIdx.x;
+  if (k >= n) return;
+  const bv_obj o = objs[k];
+  uint64_t h[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] = IV(i);
+  const uint4* p = pool + (uint64_t)o.blk * 8;
+  for (uint32_t b = 0; b < o.nblk; ++b, p += 8) {
+    uint64_t w[16];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint4 v = p[j];
+      w[2 * j] = be64(v.x, v.y);
+      w[2 * j + 1] = be64(v.z, v.w);
+    }
+    compress(h, w);
+  }
+  pow_out[k] = trial_of(h, o.nonce);
+}
+
+// ---------------------------------------------------------------------------------------
 // Launch wrappers (C++ linkage, used by bmpow_host.hip).
 // ---------------------------------------------------------------------------------------
 hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, const bm_obj* objs, const bm_item* items,
@@ -172,6 +216,13 @@ hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* 
   const uint32_t bs = 64;
   hipLaunchKernelGGL(bm_resolve_kernel, dim3((nitems + bs - 1) / bs), dim3(bs), 0, st, objs, items, nitems,
                      best, res);
+  return hipGetLastError();
+}
+
+hipError_t bv_launch_pow(hipStream_t st, const bv_obj* objs, uint32_t n, const uint4* pool, uint64_t* pow_out) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(bv_pow_kernel, dim3((n + BV_BLOCK - 1) / BV_BLOCK), dim3(BV_BLOCK), 0, st, objs, n, pool,
+                     pow_out);
   return hipGetLastError();
 }
 

@@ -22,6 +22,10 @@ or device raises :class:`BmpowUnavailable` (the reference silently degraded to P
 import ctypes
 import hashlib
 import logging
+import os
+import subprocess
+import sys
+import tempfile
 from struct import pack, unpack
 
 from . import _lib
@@ -186,12 +190,74 @@ def run_batch(objects, step_trials=0):
 
 def init():
     """Load ``libbmpow_hip.so`` and select the gfx950 devices (reference ``:336-394``).
-    Returns the number of device shards; logs and returns 0 when unavailable."""
+    Returns the number of device shards; when the library is not built, tries
+    :func:`buildCPoW` once (the reference's build-on-demand, ``:393-394``); logs and returns 0
+    when still unavailable."""
     try:
         return _device_count()
     except BmpowUnavailable as e:
+        if not os.path.exists(_lib.lib_path()) and buildCPoW():
+            return init()
         logger.error('HIP PoW unavailable: %s', e)
         return 0
+
+
+def buildCPoW():
+    """Build the native module on demand (reference ``buildCPoW``, ``:262-285``, which ran
+    ``make -C bitmsghash``): ``make -C pybitmessage_amd/csrc`` with hipcc for gfx950.
+    Returns True when the library exists afterwards."""
+    if os.path.exists(_lib.lib_path()):
+        return True
+    csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'csrc')
+    try:
+        subprocess.call(['make', '-C', csrc])
+    except OSError as e:
+        logger.error('Failed to build the HIP PoW module: %s', e)
+        return False
+    ok = os.path.exists(_lib.lib_path())
+    logger.info('HIP PoW module %s', 'built successfully' if ok else 'failed to build')
+    return ok
+
+
+class LogOutput(object):  # pylint: disable=too-few-public-methods
+    """Capture file-descriptor-1 output of native code for the scope of a ``with`` block and
+    log it line by line (reference ``LogOutput``, ``:27-69``; the reference wraps the C
+    library call in it, ``:158``).  ``libbmpow_hip.so`` prints nothing, so the HIP path does
+    not need it; it is kept for callers and tests of the reference interface."""
+
+    def __init__(self, prefix='PoW'):
+        self.prefix = prefix
+        self._saved = None
+        self._tmp = None
+
+    def __enter__(self):
+        try:
+            sys.stdout.flush()
+        except (AttributeError, ValueError, OSError):
+            pass
+        try:
+            self._saved = os.dup(1)  # native code writes to fd 1 whatever sys.stdout is
+        except OSError:
+            return self  # no fd 1 (e.g. a windowed app): nothing to capture
+        self._tmp = tempfile.TemporaryFile(mode='w+b')
+        os.dup2(self._tmp.fileno(), 1)
+        return self
+
+    def __exit__(self, exc_type, exc_val, exc_tb):
+        if self._saved is None:
+            return False
+        try:
+            sys.stdout.flush()
+        except (AttributeError, ValueError, OSError):
+            pass
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        self._saved = None
+        self._tmp.seek(0)
+        for line in self._tmp.read().decode('utf-8', 'replace').splitlines():
+            logger.info('%s: %s', self.prefix, line)
+        self._tmp.close()
+        return False
 
 
 def _device_count():

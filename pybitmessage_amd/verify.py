@@ -1,0 +1,105 @@
+"""Batched receive-side PoW verification on the GPU.
+
+The reference checks every received object with ``protocol.isProofOfWorkSufficient``
+(``src/protocol.py:258-286``), one object and three SHA-512s at a time, from the network
+thread (``network/bmobject.py:71-76``) and again at the recipient's difficulty in
+``class_objectProcessor.py:624-629``.  Here a whole inventory flood is checked in one launch
+of ``bv_pow_kernel`` (one object per lane, payload SHA-512 + the double hash of the trial
+function) through ``bmpow_verify_batch``; the verdict uses the reference's exact IEEE-double
+target arithmetic (host side of the C ABI).  No CPU fallback: without the HIP library the
+calls raise :class:`BmpowUnavailable`.
+"""
+import ctypes
+import struct
+
+import numpy as np
+
+from . import _lib
+
+P64 = ctypes.POINTER(ctypes.c_uint64)
+
+
+def _pack(objects):
+    objs = [bytes(o) for o in objects]
+    offsets = np.zeros(len(objs) + 1, dtype=np.uint64)
+    np.cumsum([len(o) for o in objs], out=offsets[1:])
+    return b''.join(objs), offsets, objs
+
+
+def _per_object(value, n, dtype):
+    arr = np.asarray(value if np.ndim(value) else [value] * n, dtype=dtype)
+    if arr.shape != (n,):
+        raise ValueError('expected a scalar or %d values' % n)
+    return np.ascontiguousarray(arr)
+
+
+def pow_values(objects):
+    """``POW`` of each finished object (nonce || payload), ``protocol.py:280-282``."""
+    data, offsets, objs = _pack(objects)
+    n = len(objs)
+    if n == 0:
+        return []
+    for o in objs:
+        if len(o) < 8:
+            raise struct.error('unpack requires a buffer of 8 bytes')
+    lib = _lib.get()
+    out = np.zeros(n, dtype=np.uint64)
+    _lib.check(lib, lib.bmpow_pow_values(n, data, offsets.ctypes.data_as(P64), out.ctypes.data_as(P64)),
+               'bmpow_pow_values')
+    return [int(v) for v in out]
+
+
+def isProofOfWorkSufficient_batch(objects, nonceTrialsPerByte=0, payloadLengthExtraBytes=0, recvTime=0):
+    """``[protocol.isProofOfWorkSufficient(o, nonceTrialsPerByte, payloadLengthExtraBytes,
+    recvTime) for o in objects]`` with one GPU launch.  Each difficulty argument and
+    ``recvTime`` may be a scalar or one value per object (``recvTime`` 0 = now, as in the
+    reference).  An object shorter than 16 bytes raises ``struct.error`` as the reference's
+    ``unpack('>Q', data[8:16])`` does."""
+    data, offsets, objs = _pack(objects)
+    n = len(objs)
+    if n == 0:
+        return []
+    ntpb = _per_object(nonceTrialsPerByte, n, np.uint64)
+    extra = _per_object(payloadLengthExtraBytes, n, np.uint64)
+    recv = _per_object([int(r) for r in recvTime] if np.ndim(recvTime) else int(recvTime), n, np.int64)
+    lib = _lib.get()
+    ok = np.zeros(n, dtype=np.uint8)
+    _lib.check(lib, lib.bmpow_verify_batch(n, data, offsets.ctypes.data_as(P64), ntpb.ctypes.data_as(P64),
+                                           extra.ctypes.data_as(P64),
+                                           recv.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                           ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
+               'bmpow_verify_batch')
+    if (ok == 2).any():
+        raise struct.error('unpack requires a buffer of 8 bytes')
+    return [bool(v) for v in ok]
+
+
+class VerifyBatch(object):
+    """Objects padded, sorted and resident in HBM; :meth:`run` hashes all of them again
+    (``bmpow_vbatch_*``, used by bench.py's verification leg)."""
+
+    def __init__(self, objects):
+        data, offsets, objs = _pack(objects)
+        self.n = len(objs)
+        self.lib = _lib.get()
+        self.handle = self.lib.bmpow_vbatch_create(self.n, data, offsets.ctypes.data_as(P64))
+        if not self.handle:
+            raise _lib.BmpowError(_lib.E_HIP, 'bmpow_vbatch_create: %s' % self.lib.bmpow_last_error().decode())
+
+    def run(self, want=True):
+        out = np.zeros(self.n, dtype=np.uint64) if want else None
+        _lib.check(self.lib, self.lib.bmpow_vbatch_run(self.handle, out.ctypes.data_as(P64) if want else None),
+                   'bmpow_vbatch_run')
+        return out
+
+    def close(self):
+        if self.handle:
+            self.lib.bmpow_vbatch_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+        return False

@@ -1,0 +1,302 @@
+"""Batched proof-of-work worker -- the PoW half of the reference's ``class_singleWorker``
+(SURVEY.md 8(f) row 1).
+
+The reference worker is strictly serial: every outgoing object (msg, broadcast, pubkey v2/3/4,
+getpubkey, onionpeer, ack) goes through ``_doPOWDefaults`` (``class_singleWorker.py:219-250``)
+or the msg-specific block (``:1256-1290``), one ``proofofwork.run`` at a time, and each msg
+nests its ack's PoW inside its own assembly (``:1220`` -> ``generateFullAckMessage``
+``:1495-1519``).  Here the same per-object unit -- target formula, ``initialHash =
+sha512(payload)``, ``pack('>Q', nonce) + payload`` -- runs as batches on the GPU:
+
+* :func:`pow_objects` -- many objects, one device batch (``proofofwork.iter_batch``);
+* :func:`full_ack_messages` / :func:`send_msgs` -- the ack-then-msg dependency as two batched
+  phases: every ack first, then every msg that embeds one;
+* :class:`PowService` -- one long-lived device batch fed by several producer threads (the
+  singleWorker thread and the API thread both call ``run``, ``api.py:1304,1350``).
+
+Every nonce is the ``_doSafePoW`` answer, so the finished objects are byte-identical to the
+serial worker's.  There is no CPU fallback (see ``proofofwork``).
+"""
+import ctypes
+import hashlib
+import logging
+import random
+import struct
+import threading
+import time
+from concurrent.futures import Future
+from struct import pack
+
+from . import _lib
+from . import proofofwork
+from . import state
+from . import targets
+
+logger = logging.getLogger('default')
+
+#: ``protocol.Header`` (``protocol.py:63``) and the network magic (``:298``)
+_HEADER = struct.Struct('!L12sL4s')
+MAGIC = 0xE9BEB4D9
+#: object type numbers (``protocol.py`` OBJECT_*; ``class_singleWorker.py:1305``)
+OBJECT_GETPUBKEY, OBJECT_PUBKEY, OBJECT_MSG, OBJECT_BROADCAST = 0, 1, 2, 3
+#: the largest object the worker may send (``class_singleWorker.py:1296``)
+MAX_OBJECT_SIZE = 2 ** 18
+
+
+class PowObject(object):
+    """One object awaiting PoW: the unit of ``_doPOWDefaults`` (``:219-250``) or of the msg
+    block (``:1256-1276``, recipient-specific ``ntpb``/``extra``)."""
+
+    __slots__ = ('payload', 'ttl', 'ntpb', 'extra', 'tag')
+
+    def __init__(self, payload, ttl, ntpb=targets.networkDefaultProofOfWorkNonceTrialsPerByte,
+                 extra=targets.networkDefaultPayloadLengthExtraBytes, tag=None):
+        self.payload = bytes(payload)
+        self.ttl = ttl
+        self.ntpb = ntpb
+        self.extra = extra
+        self.tag = tag
+
+    @property
+    def target(self):
+        """The float the reference passes to ``run`` (``:222-230``, ``:1256-1264``)."""
+        return targets.object_target(len(self.payload), self.ttl, self.ntpb, self.extra)
+
+    @property
+    def initial_hash(self):
+        """``hashlib.sha512(payload).digest()`` (``:231``, ``:1275``)."""
+        return hashlib.sha512(self.payload).digest()
+
+
+def pow_objects(objects, step_trials=0, on_done=None):
+    """PoW every object in one device batch.  Returns ``pack('>Q', nonce) + payload`` per
+    object, in input order (``:249``, ``:1290``).  ``on_done(index, trialValue, nonce)`` is
+    called as each object finishes (the reference logs "Found proof of work" there,
+    ``:237-240``).  Raises ``StopIteration("Interrupted")`` on ``state.shutdown``."""
+    objs = list(objects)
+    if not objs:
+        return []
+    if state.shutdown != 0:
+        raise RuntimeError('No active exception to reraise')  # run()'s bare raise, proofofwork.py:291-292
+    out = [None] * len(objs)
+    t0 = time.time()
+    try:
+        for i, tv, nonce in proofofwork.iter_batch([(o.target, o.initial_hash) for o in objs], step_trials):
+            out[i] = pack('>Q', nonce) + objs[i].payload
+            logger.info('Found proof of work %s Nonce: %s (object %d of %d, %.1f s into the batch)',
+                        tv, nonce, i + 1, len(objs), time.time() - t0)
+            if on_done is not None:
+                on_done(i, tv, nonce)
+    except proofofwork.PowInterrupted:
+        raise StopIteration('Interrupted')
+    return out
+
+
+def pow_payload(payload, ttl, step_trials=0):
+    """``_doPOWDefaults(payload, TTL)`` (``:219-250``) for one object through the batch path."""
+    return pow_objects([PowObject(payload, ttl)], step_trials)[0]
+
+
+# ------------------------------------------------------------------------------------------
+# acks (generateFullAckMessage, :1495-1519) and packets (protocol.CreatePacket, :292-300)
+# ------------------------------------------------------------------------------------------
+def ack_ttl(ttl, rng=random):
+    """TTL bucket of an ack (``:1503-1510``): 1 day, 1 week or 4 weeks, whichever the msg TTL
+    is closest below, plus uniform jitter in [-300, 300)."""
+    if ttl < 24 * 60 * 60:
+        ttl = 24 * 60 * 60
+    elif ttl < 7 * 24 * 60 * 60:
+        ttl = 7 * 24 * 60 * 60
+    else:
+        ttl = 28 * 24 * 60 * 60
+    return int(ttl + rng.randrange(-300, 300))
+
+
+def ack_object(ackdata, ttl, rng=random, now=None):
+    """The ack's PoW object: ``pack('>Q', embeddedTime) + ackdata`` with the bucketed TTL
+    (``:1510-1517``)."""
+    ttl = ack_ttl(ttl, rng)
+    embedded = int((time.time() if now is None else now) + ttl)
+    return PowObject(pack('>Q', embedded) + bytes(ackdata), ttl)
+
+
+def create_packet(command, payload=b''):
+    """``protocol.CreatePacket`` (``protocol.py:292-300``): 24-byte header (magic, command
+    NUL-padded to 12 bytes, length, first 4 bytes of sha512(payload)) + payload."""
+    if isinstance(command, str):
+        command = command.encode('ascii')
+    return _HEADER.pack(MAGIC, command, len(payload), hashlib.sha512(payload).digest()[0:4]) + payload
+
+
+def inventory_hash(obj):
+    """``addresses.calculateInventoryHash``: first 32 bytes of sha512(sha512(object))."""
+    return hashlib.sha512(hashlib.sha512(obj).digest()).digest()[0:32]
+
+
+def full_ack_messages(acks, rng=random, now=None, step_trials=0):
+    """Phase 1 of a batched send: ``generateFullAckMessage`` for every ``(ackdata, msgTTL)``
+    at once.  Returns the finished ``object`` packets in input order."""
+    objs = [ack_object(ackdata, ttl, rng, now) for ackdata, ttl in acks]
+    return [create_packet('object', o) for o in pow_objects(objs, step_trials)]
+
+
+def send_msgs(jobs, build_msg, rng=random, now=None, step_trials=0):
+    """Batched ``sendMsg`` PoW (``:717-1373``) in two phases.
+
+    ``jobs``: ``[(ackdata_or_None, ttl, ctx), ...]``.  Phase 1 PoWs every ack
+    (``ackdata`` None = no ack, ``fullAckPayload = ''``, ``:1203-1215``).  Then
+    ``build_msg(ctx, fullAckPayload) -> (encryptedPayload, ttl, ntpb, extra)`` assembles,
+    signs and encrypts each msg (out of scope here, ``:1222-1255``) and phase 2 PoWs every msg
+    at the recipient's difficulty.  Returns the finished msg objects (nonce || payload) in
+    job order; objects above 256 KiB are returned as None, as the worker drops them
+    (``:1296-1302``)."""
+    jobs = list(jobs)
+    want_ack = [k for k, (ackdata, _, _) in enumerate(jobs) if ackdata is not None]
+    packets = full_ack_messages([(jobs[k][0], jobs[k][1]) for k in want_ack], rng, now, step_trials)
+    ack_of = dict(zip(want_ack, packets))
+    msgs = []
+    for k, (_, _, ctx) in enumerate(jobs):
+        payload, ttl, ntpb, extra = build_msg(ctx, ack_of.get(k, b''))
+        msgs.append(PowObject(payload, ttl, ntpb, extra, tag=k))
+    done = pow_objects(msgs, step_trials)
+    return [o if len(o) <= MAX_OBJECT_SIZE else None for o in done]
+
+
+# ------------------------------------------------------------------------------------------
+# continuous batching across producer threads
+# ------------------------------------------------------------------------------------------
+class _Entry(object):
+    __slots__ = ('ih', 'target', 'next', 'future')
+
+    def __init__(self, ih, target, future):
+        self.ih = ih
+        self.target = target
+        self.next = 1
+        self.future = future
+
+
+class PowService(object):
+    """A device batch that producers join at any time.
+
+    ``submit(target, initialHash)`` returns a ``concurrent.futures.Future`` that resolves to
+    ``[trialValue, nonce]`` (the ``run`` answer) or raises ``StopIteration('Interrupted')``
+    when ``state.shutdown`` is set.  One service thread drives ``bmpow_search_batch``: each
+    call is one bounded step over every pending object (its ``next_start`` carries the
+    resume point), so an object submitted mid-flight joins the next step (~45 ms on one
+    MI355X) instead of waiting for the objects ahead of it, and producers never contend for
+    the device.  Replaces concurrent blocking ``run`` calls from the worker and API threads
+    (``class_singleWorker.py:236,1276``, ``api.py:1304,1350``)."""
+
+    def __init__(self, step_trials=0):
+        self.step_trials = step_trials
+        self._cv = threading.Condition()
+        self._incoming = []
+        self._stopping = False
+        self._thread = None
+        self.calls = 0
+        self.solved = 0
+
+    def start(self):
+        with self._cv:
+            if self._thread is None:
+                self._stopping = False
+                self._thread = threading.Thread(target=self._loop, name='PowService')
+                self._thread.daemon = True
+                self._thread.start()
+        return self
+
+    def stop(self, timeout=None):
+        with self._cv:
+            self._stopping = True
+            self._cv.notify_all()
+            th = self._thread
+        if th is not None:
+            th.join(timeout)
+        self._thread = None
+
+    def submit(self, target, initialHash):
+        fut = Future()
+        ih = proofofwork._ih_bytes(initialHash)
+        t, ok = proofofwork._clamp_target(target)
+        if not ok:
+            fut.set_exception(ValueError('negative target: no nonce can satisfy it'))
+            return fut
+        with self._cv:
+            if self._stopping or self._thread is None:
+                raise RuntimeError('PowService is not running')
+            self._incoming.append(_Entry(ih, t, fut))
+            self._cv.notify_all()
+        return fut
+
+    def run(self, target, initialHash):
+        """Blocking ``proofofwork.run`` through the shared batch."""
+        if state.shutdown != 0:
+            raise RuntimeError('No active exception to reraise')
+        return self.submit(target, initialHash).result()
+
+    def _fail(self, entries, exc):
+        for e in entries:
+            if not e.future.done():
+                e.future.set_exception(exc)
+
+    def _loop(self):
+        import numpy as np
+        active = []
+        try:
+            lib = _lib.get()
+        except Exception as e:  # noqa: BLE001 -- no device: every submitter sees why
+            lib, lib_err = None, e
+        while True:
+            with self._cv:
+                while not self._incoming and not active and not self._stopping:
+                    self._cv.wait(0.5)
+                if self._stopping:
+                    self._fail(active + self._incoming, RuntimeError('PowService stopped'))
+                    self._incoming = []
+                    return
+                active.extend(self._incoming)
+                self._incoming = []
+            if lib is None:
+                self._fail(active, lib_err)
+                active = []
+                continue
+            if state.shutdown != 0:
+                self._fail(active, StopIteration('Interrupted'))
+                active = []
+                continue
+            n = len(active)
+            ihs = b''.join(e.ih for e in active)
+            tg = np.array([e.target for e in active], dtype=np.uint64)
+            nxt = np.array([e.next for e in active], dtype=np.uint64)
+            nonce = np.zeros(n, dtype=np.uint64)
+            trial = np.zeros(n, dtype=np.uint64)
+            done = np.zeros(n, dtype=np.uint8)
+            p64 = ctypes.POINTER(ctypes.c_uint64)
+            try:
+                _lib.check(lib, lib.bmpow_search_batch(n, ihs, tg.ctypes.data_as(p64), nxt.ctypes.data_as(p64),
+                                                       self.step_trials, nonce.ctypes.data_as(p64),
+                                                       trial.ctypes.data_as(p64),
+                                                       done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
+                           'bmpow_search_batch')
+            except Exception as e:  # noqa: BLE001
+                self._fail(active, e)
+                active = []
+                continue
+            self.calls += 1
+            keep = []
+            for i, e in enumerate(active):
+                if done[i] == _lib.DONE_FOUND:
+                    tv, nn = int(trial[i]), int(nonce[i])
+                    try:
+                        proofofwork._verify(e.target, e.ih, tv, nn)
+                    except Exception as err:  # noqa: BLE001
+                        e.future.set_exception(err)
+                        continue
+                    self.solved += 1
+                    e.future.set_result([tv, nn])
+                elif done[i] == _lib.DONE_EXHAUSTED:
+                    e.future.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
+                else:
+                    e.next = int(nxt[i])
+                    keep.append(e)
+            active = keep

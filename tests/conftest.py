@@ -40,3 +40,16 @@ def gpulib():
     """libbmpow_hip.so initialised on the GPU (gpu tests only)."""
     from pybitmessage_amd import _lib
     return _lib.get()
+
+
+@pytest.fixture
+def shards(gpulib):
+    """Run a test body under several shard layouts, restoring one shard per device after."""
+    import ctypes
+
+    def use(ids):
+        arr = (ctypes.c_int * len(ids))(*ids)
+        assert gpulib.bmpow_set_devices(arr, len(ids)) == len(ids)
+    yield use
+    gpulib.bmpow_set_devices(None, 0)
+    gpulib.bmpow_set_step_trials(1 << 28)

@@ -31,17 +31,6 @@ def gpu_search(lib, ih, target, start=1, max_trials=1 << 40):
     return (t.value, n.value) if rc == _lib.FOUND else None
 
 
-@pytest.fixture
-def shards(gpulib):
-    """Run a test body under several shard layouts, restoring one shard per device after."""
-    def use(ids):
-        arr = (ctypes.c_int * len(ids))(*ids)
-        assert gpulib.bmpow_set_devices(arr, len(ids)) == len(ids)
-    yield use
-    gpulib.bmpow_set_devices(None, 0)
-    gpulib.bmpow_set_step_trials(1 << 28)
-
-
 # ---------------- trial function ----------------
 def test_trial_kats_bit_exact(gpulib, golden):
     kats = golden('trial_kats.json')['kats']

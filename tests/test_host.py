@@ -35,9 +35,11 @@ def test_header_declares_the_boundary():
     syms = declared_symbols()
     for s in ['bmpow_init', 'bmpow_search', 'bmpow_search_batch', 'bmpow_trials', 'bmpow_abort',
               'bmpow_batch_create', 'bmpow_batch_step', 'bmpow_batch_results', 'bmpow_batch_destroy',
-              'bmpow_set_devices', 'bmpow_last_error', 'BitmessagePOW']:
+              'bmpow_set_devices', 'bmpow_last_error', 'BitmessagePOW', 'bmpow_pow_values',
+              'bmpow_verify_batch', 'bmpow_pow_sufficient', 'bmpow_vbatch_create', 'bmpow_vbatch_run',
+              'bmpow_vbatch_destroy']:
         assert s in syms
-    assert len(syms) == 22
+    assert len(syms) == 28
 
 
 def test_library_exports_every_declared_symbol(rawlib):

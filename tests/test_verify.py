@@ -1,0 +1,149 @@
+"""Receive-side verification: the GPU POW values and verdicts of
+``bmpow_pow_values`` / ``bmpow_verify_batch`` against fixtures judged by the reference's
+``protocol.isProofOfWorkSufficient`` (tests/golden/make_verify_golden.py) and against hashlib.
+
+CPU part: the fixtures pin the hashlib restatement and the C ABI's host-side verdict
+arithmetic (``bmpow_pow_sufficient``, no device).  GPU part (``-m gpu``): the kernel."""
+import ctypes
+import hashlib
+import os
+import random
+import struct
+from struct import pack
+
+import numpy as np
+import pytest
+
+from pybitmessage_amd import _lib, targets
+from tests.conftest import GOLDEN
+from tests.golden.make_verify_golden import regen
+
+
+@pytest.fixture(scope='module')
+def kats(golden):
+    if not os.path.exists(os.path.join(GOLDEN, 'verify_kats.json')):
+        pytest.skip('verify_kats.json not generated')
+    return golden('verify_kats.json')
+
+
+@pytest.fixture(scope='module')
+def hostlib():
+    return _lib.load()
+
+
+def sufficient_host(lib, obj, ntpb, extra, recv):
+    return lib.bmpow_pow_sufficient(targets.pow_value(obj), len(obj), ntpb, extra, recv,
+                                    struct.unpack('>Q', obj[8:16])[0])
+
+
+# ------------------------------------------------------------------ CPU (no device)
+def test_pow_restatement_matches_reference(kats):
+    for k in kats['pow_kats']:
+        assert targets.pow_value(regen(k, False)) == k['pow'], k['L']
+
+
+def test_c_oracle_sha512_multiblock(coracle, kats):
+    for k in kats['pow_kats']:
+        obj = regen(k, False)
+        assert coracle.sha512(obj[8:]) == hashlib.sha512(obj[8:]).digest()
+
+
+def test_host_verdict_arithmetic_matches_reference(hostlib, kats):
+    """The exact flip points (recvTime, ntpb, extra) found with the reference function."""
+    for k in kats['verdict_kats']:
+        obj = regen(k, True)
+        assert targets.pow_value(obj) == k['pow']
+        for c in k['checks']:
+            assert sufficient_host(hostlib, obj, c['ntpb'], c['extra'], c['recvTime']) == int(c['ok']), (k['L'], c)
+            assert targets.isProofOfWorkSufficient(obj, c['ntpb'], c['extra'], c['recvTime']) == c['ok']
+
+
+def test_host_verdict_random_vs_restatement(hostlib):
+    rng = random.Random(11)
+    for _ in range(3000):
+        L = rng.choice([16, 100, 1000, 70000, 262144])
+        eol = rng.randrange(0, 1 << 62)
+        recv = rng.choice([1, rng.randrange(1, 1 << 40), eol - rng.randrange(-10 ** 6, 10 ** 9) if eol > 10 ** 9 else 5])
+        ntpb = rng.choice([0, 1000, 1001, rng.randrange(1, 1 << 40)])
+        extra = rng.choice([0, 1000, rng.randrange(1, 1 << 40)])
+        # a POW near the target so both outcomes occur
+        le = L + max(extra, 1000)
+        ttl = max(eol - recv, 300)
+        t = 2 ** 64 / (max(ntpb, 1000) * (le + ((ttl * le) / (2 ** 16))))
+        pw = min(max(int(t) + rng.randrange(-2, 3), 0), (1 << 64) - 1)
+        want = pw <= t
+        assert hostlib.bmpow_pow_sufficient(pw, L, ntpb, extra, recv, eol) == int(want), (pw, L, ntpb, extra, recv, eol)
+
+
+# ------------------------------------------------------------------ GPU
+gpu = pytest.mark.gpu
+
+
+@gpu
+def test_gpu_pow_values_match_reference(gpulib, kats):
+    from pybitmessage_amd import verify
+    objs = [regen(k, False) for k in kats['pow_kats']]
+    assert verify.pow_values(objs) == [k['pow'] for k in kats['pow_kats']]
+
+
+@gpu
+def test_gpu_verdicts_match_reference(gpulib, kats):
+    from pybitmessage_amd import verify
+    objs, ntpb, extra, recv, want = [], [], [], [], []
+    for k in kats['verdict_kats']:
+        obj = regen(k, True)
+        for c in k['checks']:
+            objs.append(obj)
+            ntpb.append(c['ntpb'])
+            extra.append(c['extra'])
+            recv.append(c['recvTime'])
+            want.append(c['ok'])
+        objs.append(pack('>Q', k['nonce'] + 1) + obj[8:])
+        ntpb.append(1000)
+        extra.append(1000)
+        recv.append(k['recvTime'])
+        want.append(k['next_nonce_ok'])
+    assert verify.isProofOfWorkSufficient_batch(objs, ntpb, extra, recv) == want
+
+
+@gpu
+def test_gpu_pow_random_flood_vs_hashlib(gpulib):
+    from pybitmessage_amd import verify
+    rng = random.Random(5)
+    objs = []
+    for _ in range(3000):
+        L = rng.choice([8, 9, 16, 46 + 8, 119, 120, 127, 128, 200, 1000, rng.randrange(8, 5000)])
+        objs.append(rng.randbytes(L))
+    objs.append(bytes(8) + rng.randbytes(300000))  # one long lane among short ones
+    assert verify.pow_values(objs) == [targets.pow_value(o) for o in objs]
+
+
+@gpu
+def test_gpu_verify_session_and_shards(gpulib, shards):
+    from pybitmessage_amd import verify
+    rng = random.Random(8)
+    objs = [rng.randbytes(rng.randrange(16, 3000)) for _ in range(500)]
+    want = np.array([targets.pow_value(o) for o in objs], dtype=np.uint64)
+    for layout in ([0], [0, 0], [0, 0, 0]):
+        shards(layout)
+        with verify.VerifyBatch(objs) as vb:
+            assert np.array_equal(vb.run(), want)
+            assert np.array_equal(vb.run(), want)  # resident: a second pass gives the same
+    st = _lib.BmpowStats()
+    gpulib.bmpow_get_stats(ctypes.byref(st))
+    assert st.verify_launches > 0 and st.verify_objects >= 500
+
+
+@gpu
+def test_gpu_verify_edge_cases(gpulib):
+    from pybitmessage_amd import verify
+    assert verify.pow_values([]) == []
+    assert verify.isProofOfWorkSufficient_batch([]) == []
+    with pytest.raises(struct.error):
+        verify.isProofOfWorkSufficient_batch([bytes(16), bytes(15)])
+    with pytest.raises(struct.error):
+        verify.pow_values([bytes(7)])
+    # recvTime 0 means now: an object expiring far in the past gets TTL 300 either way
+    obj = bytes(8) + pack('>Q', 1) + bytes(30)
+    assert verify.isProofOfWorkSufficient_batch([obj], recvTime=0) == \
+        [targets.isProofOfWorkSufficient(obj, 0, 0, 0)]

@@ -1,0 +1,288 @@
+"""Batched worker, the openclpow-compatible module and LogOutput.
+
+CPU tests drive the host logic against test doubles of the device layer that answer from the
+C oracle (the doubles live here in tests/; the product has no fallback).  GPU tests run the
+same flows on the device and compare with the oracle."""
+import ctypes
+import hashlib
+import logging
+import random
+import subprocess
+import threading
+import time
+from struct import pack, unpack
+
+import numpy as np
+import pytest
+
+from pybitmessage_amd import _lib, hippow, proofofwork, state, targets, worker
+
+U64 = (1 << 64) - 1
+
+
+# ------------------------------------------------------------------ test doubles
+@pytest.fixture
+def oracle_batch(monkeypatch, coracle):
+    """proofofwork.iter_batch answered by the C oracle (index order, like one big step)."""
+    calls = []
+
+    def fake_iter(objects, step_trials=0):
+        objs = list(objects)
+        calls.append(len(objs))
+        for i, (t, ih) in enumerate(objs):
+            if state.shutdown:
+                raise proofofwork.PowInterrupted('Interrupted')
+            tv, nonce = coracle.search(proofofwork._ih_bytes(ih), proofofwork._clamp_target(t)[0])
+            yield i, tv, nonce
+    monkeypatch.setattr(proofofwork, 'iter_batch', fake_iter)
+    yield calls
+    state.shutdown = 0
+
+
+class BatchLib(object):
+    """bmpow_search_batch double: each call advances every pending object by WINDOW nonces,
+    searched with the C oracle, exactly the resume contract of include/bmpow.h."""
+    WINDOW = 3000
+
+    def __init__(self, coracle):
+        self.co = coracle
+        self.calls = 0
+        self.sizes = []
+
+    def bmpow_search_batch(self, n, ihs, tg, nxt, budget, nonce, trial, done):
+        self.calls += 1
+        self.sizes.append(n)
+        view = lambda p, t: np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(t)), shape=(n,))  # noqa: E731
+        tg, nxt = view(tg, ctypes.c_uint64), view(nxt, ctypes.c_uint64)
+        nonce, trial, done = view(nonce, ctypes.c_uint64), view(trial, ctypes.c_uint64), view(done, ctypes.c_uint8)
+        pending = 0
+        for i in range(n):
+            if done[i]:
+                continue
+            r = self.co.search(ihs[64 * i:64 * i + 64], int(tg[i]), int(nxt[i]), self.WINDOW)
+            if r is None:
+                nxt[i] += self.WINDOW
+                pending += 1
+            else:
+                trial[i], nonce[i] = r
+                nxt[i] = r[1] + 1
+                done[i] = _lib.DONE_FOUND
+        time.sleep(0.002)
+        return pending
+
+    def bmpow_last_error(self):
+        return b''
+
+
+@pytest.fixture
+def batchlib(monkeypatch, coracle):
+    lib = BatchLib(coracle)
+    monkeypatch.setattr(_lib, 'get', lambda: lib)
+    yield lib
+    state.shutdown = 0
+
+
+# ------------------------------------------------------------------ CPU: host logic
+def test_powobject_matches_singleworker_formula(golden):
+    for t in golden('config_targets.json')['targets']:
+        if t['kind'] != 'singleWorker':
+            continue
+        o = worker.PowObject(bytes(t['L']), t['ttl'], t['ntpb'], t['extra'])
+        assert o.target.hex() == t['target_float']
+        assert o.initial_hash == hashlib.sha512(bytes(t['L'])).digest()
+
+
+def test_ack_ttl_buckets():
+    r = random.Random(1)
+    for ttl, bucket in [(3600, 86400), (86399, 86400), (86400, 604800), (604799, 604800),
+                        (604800, 2419200), (2419200, 2419200)]:
+        v = worker.ack_ttl(ttl, r)
+        assert bucket - 300 <= v < bucket + 300
+
+
+def test_create_packet_layout():
+    p = worker.create_packet('object', b'abc')
+    magic, cmd, ln, ck = unpack('!L12sL4s', p[:24])
+    assert magic == 0xE9BEB4D9 and cmd == b'object' + bytes(6) and ln == 3
+    assert ck == hashlib.sha512(b'abc').digest()[:4] and p[24:] == b'abc'
+
+
+def test_pow_objects_order_and_bytes(oracle_batch, coracle, golden):
+    kats = golden('batch_kats.json')
+    rng = random.Random(kats['seed'])
+    objs = [worker.PowObject(rng.randbytes(k['L']), kats['ttl'], kats['ntpb'], kats['extra']) for k in kats['kats']]
+    seen = []
+    out = worker.pow_objects(objs, on_done=lambda i, tv, n: seen.append(i))
+    assert oracle_batch == [len(objs)]  # one batch for all objects
+    for o, k, fin in zip(objs, kats['kats'], out):
+        assert o.initial_hash.hex() == k['ih'] and int(o.target) == k['target']
+        assert fin == pack('>Q', k['nonce']) + o.payload
+    assert sorted(seen) == list(range(len(objs)))
+
+
+def test_send_msgs_two_phases(oracle_batch):
+    """All acks in one batch first, every msg (embedding its ack) in a second batch."""
+    rng = random.Random(4)
+    jobs = [(rng.randbytes(38), 3600, {'k': k}) if k % 3 else (None, 3600, {'k': k}) for k in range(7)]
+    built = []
+
+    def build_msg(ctx, ack):
+        built.append((ctx['k'], ack))
+        return b'msg%d' % ctx['k'] + ack, 3600, 10, 10
+    now = 1700000000
+    out = worker.send_msgs(jobs, build_msg, rng=random.Random(9), now=now)
+    assert oracle_batch == [4, 7]
+    for (k, ack), (ackdata, _, _) in zip(built, jobs):
+        if ackdata is None:
+            assert ack == b''
+        else:
+            assert ack[24 + 8 + 8:] == ackdata  # header, nonce, embeddedTime
+            body = ack[24:]
+            assert targets.pow_value(body) <= int(targets.object_target(len(body) - 8,
+                                                                         unpack('>Q', body[8:16])[0] - now))
+    for k, o in enumerate(out):
+        assert o[8:] == b'msg%d' % k + built[k][1]
+
+
+def test_pow_objects_interrupted(oracle_batch):
+    state.shutdown = 0
+    objs = [worker.PowObject(b'x' * 10, 3600, 10, 10)] * 3
+
+    def stop(i, tv, n):
+        state.shutdown = 1
+    with pytest.raises(StopIteration):
+        worker.pow_objects(objs, on_done=stop)
+
+
+def test_powservice_concurrent_producers(batchlib, coracle):
+    svc = worker.PowService().start()
+    try:
+        rng = random.Random(2)
+        jobs = [(U64 // rng.choice([50, 2000, 9000]), rng.randbytes(64)) for _ in range(24)]
+        results = {}
+
+        def producer(lo, hi):
+            for j in range(lo, hi):
+                results[j] = svc.run(*jobs[j])
+        ths = [threading.Thread(target=producer, args=(a, a + 6)) for a in range(0, 24, 6)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(60)
+        for j, (t, ih) in enumerate(jobs):
+            assert results[j] == list(coracle.search(ih, t))
+        assert max(batchlib.sizes) > 1  # producers shared device calls
+    finally:
+        svc.stop(5)
+
+
+def test_powservice_shutdown_and_errors(batchlib):
+    svc = worker.PowService().start()
+    try:
+        fut = svc.submit(0, bytes(64))  # target 0: never found
+        time.sleep(0.05)
+        state.shutdown = 1
+        with pytest.raises(StopIteration):
+            fut.result(10)
+        state.shutdown = 0
+        with pytest.raises(ValueError):
+            svc.submit(-1, bytes(64)).result(1)
+    finally:
+        state.shutdown = 0
+        svc.stop(5)
+    with pytest.raises(RuntimeError):
+        svc.submit(1, bytes(64))
+
+
+def test_logoutput_captures_native_stdout(caplog):
+    """Mirror of the reference's src/tests/test_log.py:13-21."""
+    with caplog.at_level(logging.INFO, logger='default'):
+        with proofofwork.LogOutput():
+            subprocess.call(['echo', 'HELLO'])
+    assert any('PoW: HELLO' in r.getMessage() for r in caplog.records)
+
+
+def test_hippow_without_device(monkeypatch):
+    def unavailable():
+        raise _lib.BmpowUnavailable(_lib.E_NODEV, 'no device')
+    monkeypatch.setattr(_lib, 'get', unavailable)
+    hippow.initCL()
+    assert not hippow.openclAvailable() and not hippow.openclEnabled()
+    assert hippow.do_opencl_pow('00' * 64, 2 ** 60) == 0  # reference: 0 when no GPU is enabled
+
+
+# ------------------------------------------------------------------ GPU
+gpu = pytest.mark.gpu
+
+
+@gpu
+def test_gpu_pow_objects_vs_oracle(gpulib, coracle, golden):
+    kats = golden('batch_kats.json')
+    rng = random.Random(kats['seed'])
+    objs = [worker.PowObject(rng.randbytes(k['L']), kats['ttl'], kats['ntpb'], kats['extra']) for k in kats['kats']]
+    out = worker.pow_objects(objs)
+    assert out == [pack('>Q', k['nonce']) + o.payload for o, k in zip(objs, kats['kats'])]
+
+
+@gpu
+def test_gpu_send_msgs_and_verify(gpulib):
+    """Two-phase send on the GPU; every finished ack and msg passes the receive-side check."""
+    from pybitmessage_amd import verify
+    rng = random.Random(12)
+    now = int(time.time())
+    jobs = [(rng.randbytes(38), 3600, k) for k in range(6)]
+
+    def build_msg(k, ack):
+        payload = pack('>Q', now + 3600) + b'\x00\x00\x00\x02\x01\x01' + rng.randbytes(50) + ack
+        return payload, 3600, 1000, 1000
+    msgs = worker.send_msgs(jobs, build_msg, rng=random.Random(3), now=now)
+    acks = [m[8 + 8 + 6 + 50:] for m in msgs]
+    assert all(a[:4] == pack('!L', worker.MAGIC) for a in acks)
+    assert verify.isProofOfWorkSufficient_batch(msgs, recvTime=now) == [True] * 6
+    assert verify.isProofOfWorkSufficient_batch([a[24:] for a in acks], recvTime=now) == [True] * 6
+
+
+@gpu
+def test_gpu_powservice(gpulib, coracle):
+    svc = worker.PowService().start()
+    try:
+        rng = random.Random(21)
+        jobs = [(U64 // rng.choice([100, 30000, 300000]), rng.randbytes(64)) for _ in range(40)]
+        futs = []
+        for t, ih in jobs:
+            futs.append(svc.submit(t, ih))
+            time.sleep(rng.random() * 0.01)  # arrivals while earlier objects are in flight
+        for f, (t, ih) in zip(futs, jobs):
+            assert f.result(120) == list(coracle.search(ih, t))
+    finally:
+        svc.stop(10)
+
+
+@gpu
+def test_gpu_hippow_openclpow_vector(gpulib, golden):
+    """src/tests/test_openclpow.py:22-31 through the openclpow-compatible module, with the
+    exact-answer assertion the reference test lacks."""
+    hippow.initCL()
+    assert hippow.openclAvailable() and hippow.openclEnabled()
+    k = [k for k in golden('first_nonce_kats.json')['kats'] if '224121278' in k['note']][0]
+    nonce = hippow.do_opencl_pow(k['ih'], k['target'])
+    assert nonce == k['nonce'] == 224121278
+    ih = bytes.fromhex(k['ih'])
+    tv, = unpack('>Q', hashlib.sha512(hashlib.sha512(pack('>Q', nonce) + ih).digest()).digest()[0:8])
+    assert (nonce - tv) < k['target'] and tv <= k['target']
+    hippow.initCL('NVIDIA Corporation')  # another vendor selected: present but not enabled
+    assert hippow.openclAvailable() and not hippow.openclEnabled()
+    assert hippow.do_opencl_pow(k['ih'], k['target']) == 0
+    hippow.initCL()
+
+
+@gpu
+def test_gpu_hippow_shutdown(gpulib):
+    hippow.initCL()
+    t = threading.Timer(0.3, lambda: setattr(state, 'shutdown', 1))
+    t.start()
+    try:
+        with pytest.raises(Exception, match='Interrupted'):
+            hippow.do_opencl_pow('00' * 64, 0)
+    finally:
+        state.shutdown = 0
