@@ -10,7 +10,7 @@
 //     lane l of iteration i hashes nonce  chunk_first + i*BM_BLOCK + l;
 //   * a hit does atomicMin(best[obj], nonce) -- the per-object minimum over the launch;
 //   * exact first-nonce semantics: a chunk whose first nonce is above best[obj] cannot
-//     hold the minimum, so it is skipped (checked at chunk start and every few iterations
+//     hold the minimum, so it is skipped (checked at chunk start and after every iteration
 //     with an agent-scope load: the early exit never skips a nonce below the answer);
 //   * pure integer VALU -- no LDS, no MFMA, no HBM traffic beyond ~100 B per workgroup.
 #include <hip/hip_runtime.h>
@@ -96,7 +96,15 @@ using namespace bm;
 // ---------------------------------------------------------------------------------------
 // Search kernel.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __restrict__ objs,
+#ifndef BM_MIN_WAVES
+#define BM_MIN_WAVES 1
+#endif
+#if BM_MIN_WAVES > 0
+#define BM_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(BM_MIN_WAVES, 8)))
+#else
+#define BM_WAVES_ATTR
+#endif
+__global__ __launch_bounds__(BM_BLOCK) BM_WAVES_ATTR void bm_search_kernel(const bm_obj* __restrict__ objs,
                                                              const bm_item* __restrict__ items,
                                                              uint32_t nitems,
                                                              unsigned long long* __restrict__ best,
@@ -126,13 +134,16 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __res
   for (uint32_t i = 0; i < BM_ITERS; ++i) {
     const uint64_t base = (uint64_t)i * BM_BLOCK;
     if (base >= cnt) break;
-    if ((i & 3) == 3 &&
-        __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < first + base) break;
+    // Early exit, one iteration of granularity at no stall: the running minimum is read
+    // before this iteration's hashing (its latency hides behind ~6,500 VALU instructions)
+    // and tested after it.  A value older by one iteration is only conservative.
+    const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t j = base + threadIdx.x;
     const uint64_t nonce = first + j;
     const uint64_t tv = trial_of(ihw, nonce);
     if (j < cnt && tv <= target) atomicMin(bestp, (unsigned long long)nonce);
     done += (cnt - base < BM_BLOCK) ? (uint32_t)(cnt - base) : BM_BLOCK;
+    if (seen < first + base + BM_BLOCK) break;  // every later nonce of this chunk is above it
   }
   if (threadIdx.x == 0) atomicAdd(trials_done, (unsigned long long)done);
 }
