@@ -159,6 +159,39 @@ BMPOW_API bmpow_vbatch *bmpow_vbatch_create(size_t n, const uint8_t *objs, const
 BMPOW_API int bmpow_vbatch_run(bmpow_vbatch *vb, uint64_t *pow_out);
 BMPOW_API void bmpow_vbatch_destroy(bmpow_vbatch *vb);
 
+/* ---- RIPE-prefix address search (replaces the key-generation loops of
+ *      src/class_addressGenerator.py:130-148 (random) and :238-271 (deterministic)) ----
+ *
+ * Try k derives two secp256k1 private keys, multiplies them by G (src/highlevelcrypto.py:111-140,
+ * pointMult) and computes ripe = RIPEMD160(SHA512(pubSigning || pubEncryption)) over the
+ * 65-byte uncompressed keys; the search returns the first k whose ripe starts with null_bytes
+ * zero bytes (numberOfNullBytesDemandedOnFrontOfRipeHash). */
+typedef struct bmpow_address {
+    uint64_t k;                   /* the try index found */
+    uint8_t ripe[20];
+    uint8_t priv_signing[32];
+    uint8_t priv_encryption[32];
+    uint8_t pub_signing[65];      /* 04 || X || Y */
+    uint8_t pub_encryption[65];
+} bmpow_address;
+
+/* pointMult for n private keys (n x 32 bytes, big-endian) -> n x 65-byte keys; a zero key gives
+ * 65 zero bytes.  Returns 0 or < 0. */
+BMPOW_API int bmpow_pubkeys(size_t n, const uint8_t *privkeys, uint8_t *pubkeys_out);
+
+/* Deterministic addresses (createDeterministicAddresses / getDeterministicAddress / chans):
+ * privSigning = SHA512(passphrase || varint(2k))[:32], privEncryption = SHA512(passphrase ||
+ * varint(2k+1))[:32], k in [start, start + max_tries).  Returns BMPOW_FOUND (out filled) with
+ * the first k, BMPOW_NOT_FOUND, or < 0.  The reference continues the next address at k + 1. */
+BMPOW_API int bmpow_address_search(const uint8_t *passphrase, size_t len, uint64_t start, uint64_t max_tries,
+                                   int null_bytes, bmpow_address *out);
+
+/* Random addresses (createRandomAddress): the given signing key is kept; the encryption key of
+ * try k is SHA512(seed || varint(k))[:32] (the caller draws `seed` from a CSPRNG, as the
+ * reference draws each key from OpenSSL.rand).  Same return convention. */
+BMPOW_API int bmpow_address_search_random(const uint8_t priv_signing[32], const uint8_t *seed, size_t seed_len,
+                                          uint64_t start, uint64_t max_tries, int null_bytes, bmpow_address *out);
+
 /* ---- instrumentation (bench.py's roofline leg) ---- */
 typedef struct bmpow_stats {
     uint64_t launches;        /* search-kernel launches (summed over shards) */
@@ -172,6 +205,10 @@ typedef struct bmpow_stats {
     uint64_t verify_objects;  /* objects hashed */
     uint64_t verify_blocks;   /* 128-B SHA-512 blocks of payload hashed (padding included) */
     double verify_kernel_ms;  /* max over shards per run, summed over runs (HIP events) */
+    /* RIPE-prefix address search (bmpow_address_search*) */
+    uint64_t addr_launches;   /* search steps */
+    uint64_t addr_tries;      /* tries launched (each: 2 SHA-512, 2 k*G, SHA-512, RIPEMD-160) */
+    double addr_kernel_ms;    /* max over shards per step, summed (HIP events) */
 } bmpow_stats;
 
 BMPOW_API int bmpow_get_stats(bmpow_stats *out);

@@ -44,7 +44,15 @@ class BmpowStats(ctypes.Structure):
                 ('kernel_ms', ctypes.c_double), ('max_shard_kernel_ms', ctypes.c_double),
                 ('steps', ctypes.c_uint64), ('verify_launches', ctypes.c_uint64),
                 ('verify_objects', ctypes.c_uint64), ('verify_blocks', ctypes.c_uint64),
-                ('verify_kernel_ms', ctypes.c_double)]
+                ('verify_kernel_ms', ctypes.c_double), ('addr_launches', ctypes.c_uint64),
+                ('addr_tries', ctypes.c_uint64), ('addr_kernel_ms', ctypes.c_double)]
+
+
+class BmpowAddress(ctypes.Structure):
+    """``bmpow_address`` (include/bmpow.h): one found try of the address search."""
+    _fields_ = [('k', ctypes.c_uint64), ('ripe', ctypes.c_uint8 * 20), ('priv_signing', ctypes.c_uint8 * 32),
+                ('priv_encryption', ctypes.c_uint8 * 32), ('pub_signing', ctypes.c_uint8 * 65),
+                ('pub_encryption', ctypes.c_uint8 * 65)]
 
 
 # (name, restype, argtypes) for every symbol include/bmpow.h declares
@@ -80,6 +88,11 @@ SIGNATURES = [
     ('bmpow_vbatch_create', _vp, [ctypes.c_size_t, ctypes.c_char_p, _p64]),
     ('bmpow_vbatch_run', ctypes.c_int, [_vp, _p64]),
     ('bmpow_vbatch_destroy', None, [_vp]),
+    ('bmpow_pubkeys', ctypes.c_int, [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p]),
+    ('bmpow_address_search', ctypes.c_int,
+     [ctypes.c_char_p, ctypes.c_size_t, _u64, _u64, ctypes.c_int, ctypes.POINTER(BmpowAddress)]),
+    ('bmpow_address_search_random', ctypes.c_int,
+     [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, _u64, _u64, ctypes.c_int, ctypes.POINTER(BmpowAddress)]),
     ('BitmessagePOW', ctypes.c_ulonglong, [ctypes.c_char_p, ctypes.c_ulonglong]),
 ]
 

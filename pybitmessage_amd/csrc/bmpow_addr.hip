@@ -1,0 +1,282 @@
+// bmpow_addr.hip -- RIPE-prefix address search on gfx950.
+//
+// Reference: src/class_addressGenerator.py:238-271 (deterministic addresses: try k = 0, 1, ...
+// with privSigning = SHA512(passphrase || varint(2k))[:32], privEncryption =
+// SHA512(passphrase || varint(2k+1))[:32], ripe = RIPEMD160(SHA512(pubSigning || pubEncryption))
+// until ripe starts with numberOfNullBytesDemandedOnFrontOfRipeHash zero bytes) and :130-148
+// (random addresses: fixed signing key, fresh encryption keys).
+//
+// One lane per try: two SHA-512 key derivations (from a per-passphrase midstate; the tail
+// block is patched per lane with its varint), two fixed-base scalar multiplications
+// (secp256k1_dev.h), SHA-512 over the two 65-byte keys, RIPEMD-160, prefix test,
+// atomicMin(best, k).  Exact first-try semantics as the search kernel: a lane whose k is
+// above a hit already recorded exits early; the host reports a hit only after the launch that
+// covers every k below it has completed.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bmpow_kernels.h"
+#include "ripemd160_dev.h"
+#include "secp256k1_dev.h"
+#include "sha512_dev.h"
+
+using namespace bm;
+using ec::fe;
+using ec::ge;
+using ec::gej;
+
+namespace {
+
+// SHA-512 of (passphrase || varint(m)) given the midstate over the passphrase's full 128-byte
+// blocks and the template block(s) holding its tail bytes (prm->tail_len of them).
+BM_DEV void key_hash(uint64_t (&h)[8], const ar_params* __restrict__ prm, uint64_t m) {
+  // varint(m) || 0x80 as a big-endian byte string in (hi, lo), top aligned
+  uint64_t shi, slo = 0;
+  uint32_t vlen;
+  if (m < 253) {
+    shi = (m << 56) | (0x80ULL << 48);
+    vlen = 1;
+  } else if (m < 65536) {
+    shi = (0xfdULL << 56) | (m << 40) | (0x80ULL << 32);
+    vlen = 3;
+  } else if (m < 4294967296ULL) {
+    shi = (0xfeULL << 56) | (m << 24) | (0x80ULL << 16);
+    vlen = 5;
+  } else {
+    shi = (0xffULL << 56) | (m >> 8);
+    slo = (m << 56) | (0x80ULL << 48);
+    vlen = 9;
+  }
+  const uint32_t r = prm->tail_len;  // < 128
+  const uint32_t q = r >> 3, sh = 8 * (r & 7);
+  const uint64_t v0 = shi >> sh;
+  const uint64_t v1 = sh ? ((shi << (64 - sh)) | (slo >> sh)) : slo;
+  const uint64_t v2 = sh ? (slo << (64 - sh)) : 0;
+  const uint32_t nblk = (r + vlen + 1 + 16 + 127) / 128;  // 1 or 2
+  const uint64_t bits = 8 * (prm->total_len + vlen);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] = prm->mid[i];
+#pragma unroll 1
+  for (uint32_t b = 0; b < nblk; ++b) {  // one compress body for both tail blocks
+    uint64_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const uint32_t jj = 16 * b + j;
+      uint64_t x = prm->tmpl[jj];
+      x |= (jj == q) ? v0 : ((jj == q + 1) ? v1 : ((jj == q + 2) ? v2 : 0));
+      if (j == 15 && b + 1 == nblk) x |= bits;
+      w[j] = x;
+    }
+    compress(h, w);
+  }
+}
+
+// SHA-512 over 0x04||Xs||Ys||0x04||Xe||Ye (130 bytes, two blocks), then RIPEMD-160.
+BM_DEV void ripe_of(uint32_t (&rh)[5], const uint64_t (&xs)[4], const uint64_t (&ys)[4], const uint64_t (&xe)[4],
+                    const uint64_t (&ye)[4]) {
+  uint64_t w[16];
+  w[0] = (0x04ULL << 56) | (xs[0] >> 8);
+  w[1] = (xs[0] << 56) | (xs[1] >> 8);
+  w[2] = (xs[1] << 56) | (xs[2] >> 8);
+  w[3] = (xs[2] << 56) | (xs[3] >> 8);
+  w[4] = (xs[3] << 56) | (ys[0] >> 8);
+  w[5] = (ys[0] << 56) | (ys[1] >> 8);
+  w[6] = (ys[1] << 56) | (ys[2] >> 8);
+  w[7] = (ys[2] << 56) | (ys[3] >> 8);
+  w[8] = (ys[3] << 56) | (0x04ULL << 48) | (xe[0] >> 16);
+  w[9] = (xe[0] << 48) | (xe[1] >> 16);
+  w[10] = (xe[1] << 48) | (xe[2] >> 16);
+  w[11] = (xe[2] << 48) | (xe[3] >> 16);
+  w[12] = (xe[3] << 48) | (ye[0] >> 16);
+  w[13] = (ye[0] << 48) | (ye[1] >> 16);
+  w[14] = (ye[1] << 48) | (ye[2] >> 16);
+  w[15] = (ye[2] << 48) | (ye[3] >> 16);
+  uint64_t h[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] = IV(i);
+  const uint64_t tail0 = (ye[3] << 48) | (0x80ULL << 40);
+#pragma unroll 1
+  for (int b = 0; b < 2; ++b) {  // one compress body for both blocks
+    compress(h, w);
+    w[0] = tail0;
+#pragma unroll
+    for (int i = 1; i < 15; ++i) w[i] = 0;
+    w[15] = 130 * 8;
+  }
+  rmd::of_sha512_digest(rh, h);
+}
+
+BM_DEV bool prefix_ok(const uint32_t (&rh)[5], uint32_t null_bytes) {
+  // ripe bytes are h0..h4 little-endian: byte i = (h[i/4] >> 8*(i%4)) & 0xff
+#pragma unroll
+  for (int i = 0; i < 20; ++i)
+    if ((uint32_t)i < null_bytes && ((rh[i >> 2] >> (8 * (i & 3))) & 0xff) != 0) return false;
+  return true;
+}
+
+// The keys of one try.  mode 0 (deterministic): signing from m = 2k, encryption from 2k+1.
+// mode 1 (random): fixed signing key prm->pub_s; encryption key from m = k of a random seed.
+BM_DEV bool try_keys(const ar_params* __restrict__ prm, const ge* __restrict__ table, uint64_t k,
+                     uint64_t (&hs)[8], uint64_t (&he)[8], ge& ps, ge& pe) {
+  const uint32_t first = prm->mode == 0 ? 0 : 1;  // mode 1: the signing key is given
+  if (first) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) hs[i] = 0;
+    ps = prm->pub_s;
+  }
+  bool ok = true;
+#pragma unroll 1
+  for (uint32_t which = first; which < 2; ++which) {  // one hash + one scalar-mult body for both keys
+    const uint64_t m = prm->mode == 0 ? 2 * k + which : k;
+    uint64_t h[8];
+    key_hash(h, prm, m);
+    const uint64_t kw[4] = {h[0], h[1], h[2], h[3]};
+    ge r;
+    ok = ok && ec::scalar_mult_base(r, table, kw);
+    if (which == 0) {
+      ps = r;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) hs[i] = h[i];
+    } else {
+      pe = r;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) he[i] = h[i];
+    }
+  }
+  return ok;
+}
+
+BM_DEV void ripe_of_points(uint32_t (&rh)[5], const ge& ps, const ge& pe) {
+  uint64_t xs[4], ys[4], xe[4], ye[4];
+  ec::fe_to_be64(xs, ps.x);
+  ec::fe_to_be64(ys, ps.y);
+  ec::fe_to_be64(xe, pe.x);
+  ec::fe_to_be64(ye, pe.y);
+  ripe_of(rh, xs, ys, xe, ye);
+}
+
+}  // namespace
+
+// table[i*256 + v] = v * 2^(8i) * G (affine), v = 1..255.  One thread per entry.
+__global__ __launch_bounds__(64) void ar_table_kernel(ge* __restrict__ table) {
+  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
+  if (t >= 32 * 256) return;
+  const uint32_t i = t >> 8, v = t & 255;
+  if (v == 0) return;
+  gej b;
+  b.inf = false;
+  // G
+  const uint32_t gx[8] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu,
+                          0xCE870B07u, 0x55A06295u, 0xF9DCBBACu, 0x79BE667Eu};
+  const uint32_t gy[8] = {0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                          0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+  for (int j = 0; j < 8; ++j) {
+    b.x.d[j] = gx[j];
+    b.y.d[j] = gy[j];
+  }
+  ec::fe_set(b.z, 1);
+  for (uint32_t d = 0; d < 8 * i; ++d) ec::gej_double(b, b);  // 2^(8i) * G
+  ge ba;
+  ec::gej_to_ge(ba, b);
+  gej acc;
+  acc.inf = true;
+  for (int bit = 7; bit >= 0; --bit) {  // v * B, MSB first
+    ec::gej_double(acc, acc);
+    if ((v >> bit) & 1) ec::gej_add_ge(acc, acc, ba);
+  }
+  ec::gej_to_ge(table[t], acc);
+}
+
+// Search: lane g tries k = start + g (g < count).  best: running minimum k with a hit.
+// With out != nullptr the launch instead reports everything about the single try k = start
+// (keys, public keys, ripe) -- the resolve step, sharing this kernel's code.
+__global__ __launch_bounds__(64) void ar_search_kernel(const ar_params* __restrict__ prm, const ge* __restrict__ table,
+                                                       uint64_t start, uint32_t count,
+                                                       unsigned long long* __restrict__ best,
+                                                       ar_result* __restrict__ out) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= count) return;
+  const uint64_t k = start + g;
+  if (!out && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) return;
+  uint64_t hs[8], he[8];
+  ge ps, pe;
+  const bool ok = try_keys(prm, table, k, hs, he, ps, pe);
+  uint32_t rh[5] = {0, 0, 0, 0, 0};
+  if (ok) ripe_of_points(rh, ps, pe);
+  if (out) {
+    out->k = k;
+    out->ok = ok ? 1u : 0u;
+    for (int i = 0; i < 4; ++i) {
+      out->priv_s[i] = hs[i];
+      out->priv_e[i] = he[i];
+    }
+    out->pub_s = ps;
+    out->pub_e = pe;
+    for (int i = 0; i < 5; ++i) out->ripe[i] = rh[i];
+    return;
+  }
+  if (ok && prefix_ok(rh, prm->null_bytes)) atomicMin(best, (unsigned long long)k);
+}
+
+// pointMult parity probe: pub[i] = privs[i] * G (privs as 4 big-endian words each).
+__global__ __launch_bounds__(64) void ar_pubkey_kernel(const uint64_t* __restrict__ privs, uint32_t n,
+                                                       const ge* __restrict__ table, ge* __restrict__ pubs,
+                                                       uint32_t* __restrict__ ok) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= n) return;
+  const uint64_t kw[4] = {privs[4 * g], privs[4 * g + 1], privs[4 * g + 2], privs[4 * g + 3]};
+  ge r;
+  ok[g] = ec::scalar_mult_base(r, table, kw) ? 1u : 0u;
+  pubs[g] = r;
+}
+
+// Midstate of the passphrase's first nfull 128-byte blocks (one thread).
+__global__ void ar_midstate_kernel(const uint8_t* __restrict__ pass, uint64_t nfull, uint64_t* __restrict__ mid) {
+  if (blockIdx.x != 0 || threadIdx.x != 0) return;
+  uint64_t h[8];
+  for (int i = 0; i < 8; ++i) h[i] = IV(i);
+  for (uint64_t b = 0; b < nfull; ++b) {
+    uint64_t w[16];
+    for (int j = 0; j < 16; ++j) {
+      uint64_t x = 0;
+      for (int q = 0; q < 8; ++q) x = (x << 8) | pass[b * 128 + 8 * j + q];
+      w[j] = x;
+    }
+    compress(h, w);
+  }
+  for (int i = 0; i < 8; ++i) mid[i] = h[i];
+}
+
+// ---------------------------------------------------------------------------------------
+// Launch wrappers (C++ linkage, used by bmpow_host.hip).
+// ---------------------------------------------------------------------------------------
+hipError_t ar_launch_table(hipStream_t st, ge* table) {
+  hipLaunchKernelGGL(ar_table_kernel, dim3(32 * 256 / 64), dim3(64), 0, st, table);
+  return hipGetLastError();
+}
+
+hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, const ge* table, uint64_t start, uint32_t count,
+                            unsigned long long* best) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(ar_search_kernel, dim3((count + 63) / 64), dim3(64), 0, st, prm, table, start, count, best,
+                     (ar_result*)nullptr);
+  return hipGetLastError();
+}
+
+hipError_t ar_launch_resolve(hipStream_t st, const ar_params* prm, const ge* table, uint64_t k, ar_result* out) {
+  hipLaunchKernelGGL(ar_search_kernel, dim3(1), dim3(64), 0, st, prm, table, k, 1u, (unsigned long long*)nullptr,
+                     out);
+  return hipGetLastError();
+}
+
+hipError_t ar_launch_pubkeys(hipStream_t st, const uint64_t* privs, uint32_t n, const ge* table, ge* pubs,
+                             uint32_t* ok) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(ar_pubkey_kernel, dim3((n + 63) / 64), dim3(64), 0, st, privs, n, table, pubs, ok);
+  return hipGetLastError();
+}
+
+hipError_t ar_launch_midstate(hipStream_t st, const uint8_t* pass, uint64_t nfull, uint64_t* mid) {
+  hipLaunchKernelGGL(ar_midstate_kernel, dim3(1), dim3(64), 0, st, pass, nfull, mid);
+  return hipGetLastError();
+}

@@ -69,6 +69,8 @@ struct Shard {
   std::vector<uint32_t> item_obj;
   // stats
   double kernel_ms = 0.0;
+  // address search: the fixed-base comb table (v * 2^(8i) * G), built on first use
+  ec::ge* d_table = nullptr;
 };
 
 std::vector<Shard> g_shards;
@@ -102,6 +104,7 @@ void free_shard(Shard& s) {
   if (s.h_items) (void)hipHostFree(s.h_items);
   if (s.h_res) (void)hipHostFree(s.h_res);
   if (s.h_trials) (void)hipHostFree(s.h_trials);
+  if (s.d_table) (void)hipFree(s.d_table);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
   if (s.stream) (void)hipStreamDestroy(s.stream);
@@ -586,6 +589,184 @@ int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, in
 
 }  // namespace
 
+// ---------------------------------------------------------------------------------------
+// RIPE-prefix address search (bmpow_addr.hip).  Steps cover contiguous ranges of try indices
+// [next, next + S*step), one slice per shard; a hit is reported only after the step that
+// covers every smaller try has completed, so the answer is the first k, as the reference's
+// sequential loop finds it.  Step sizes ramp up from about the expected number of tries
+// (256^null_bytes) so a 1-byte search costs one small launch.
+// ---------------------------------------------------------------------------------------
+namespace {
+
+constexpr uint64_t kAddrMaxStep = 1ULL << 20;  // tries per shard per launch (~tens of ms)
+
+int ensure_table(Shard& sh) {
+  if (sh.d_table) return 0;
+  HIPTRY(hipSetDevice(sh.dev));
+  HIPTRY(hipMalloc(&sh.d_table, 32 * 256 * sizeof(ec::ge)));
+  HIPTRY(hipMemsetAsync(sh.d_table, 0, 32 * 256 * sizeof(ec::ge), sh.stream));
+  HIPTRY(ar_launch_table(sh.stream, sh.d_table));
+  HIPTRY(hipStreamSynchronize(sh.stream));
+  return 0;
+}
+
+void be_words_from_bytes(const uint8_t* b, uint64_t (&w)[4]) {
+  for (int i = 0; i < 4; ++i) w[i] = load_be64(b + 8 * i);
+}
+
+void bytes_from_be_words(const uint64_t* w, int n, uint8_t* out) {
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < 8; ++j) out[8 * i + j] = (uint8_t)(w[i] >> (56 - 8 * j));
+}
+
+void point_bytes(const ec::ge& p, uint8_t* out) {  // 04 || X || Y, big-endian
+  out[0] = 0x04;
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 4; ++j) {
+      out[1 + 4 * i + j] = (uint8_t)(p.x.d[7 - i] >> (24 - 8 * j));
+      out[33 + 4 * i + j] = (uint8_t)(p.y.d[7 - i] >> (24 - 8 * j));
+    }
+}
+
+struct AddrShard {
+  ar_params* d_prm = nullptr;
+  uint8_t* d_seed = nullptr;
+  unsigned long long* d_best = nullptr;
+  ar_result* d_res = nullptr;
+  uint64_t* d_priv = nullptr;
+  uint32_t* d_ok = nullptr;
+};
+
+void addr_free(std::vector<AddrShard>& v) {
+  for (size_t s = 0; s < v.size() && s < g_shards.size(); ++s) {
+    (void)hipSetDevice(g_shards[s].dev);
+    if (v[s].d_prm) (void)hipFree(v[s].d_prm);
+    if (v[s].d_seed) (void)hipFree(v[s].d_seed);
+    if (v[s].d_best) (void)hipFree(v[s].d_best);
+    if (v[s].d_res) (void)hipFree(v[s].d_res);
+    if (v[s].d_priv) (void)hipFree(v[s].d_priv);
+    if (v[s].d_ok) (void)hipFree(v[s].d_ok);
+  }
+  v.clear();
+}
+
+int addr_search_locked(uint32_t mode, const uint8_t* seed, size_t len, const uint8_t* priv_s, uint64_t start,
+                       uint64_t max_tries, int null_bytes, bmpow_address* out, std::vector<AddrShard>& as) {
+  if (null_bytes < 0 || null_bytes > 20) return set_err(BMPOW_E_ARG, "null_bytes must be in [0, 20]");
+  if (!out || (len && !seed) || (mode == 1 && !priv_s)) return set_err(BMPOW_E_ARG, "null pointer");
+  if (max_tries == 0) return BMPOW_NOT_FOUND;
+  if (mode == 0 && start > (kU64Max >> 1)) return set_err(BMPOW_E_ARG, "try index above 2^63 (nonce 2k overflows)");
+  ar_params hp;
+  std::memset(&hp, 0, sizeof hp);
+  hp.total_len = len;
+  hp.tail_len = (uint32_t)(len % 128);
+  hp.null_bytes = (uint32_t)null_bytes;
+  hp.mode = mode;
+  const uint64_t nfull = len / 128;
+  for (uint32_t i = 0; i < hp.tail_len; ++i) {
+    const uint64_t byte = seed[nfull * 128 + i];
+    hp.tmpl[i >> 3] |= byte << (56 - 8 * (i & 7));
+  }
+  uint64_t pw[4] = {0, 0, 0, 0};
+  if (mode == 1) be_words_from_bytes(priv_s, pw);
+  const size_t S = g_shards.size();
+  as.assign(S, AddrShard());
+  for (size_t s = 0; s < S; ++s) {
+    Shard& sh = g_shards[s];
+    int rc = ensure_table(sh);
+    if (rc < 0) return rc;
+    AddrShard& a = as[s];
+    HIPTRY(hipMalloc(&a.d_prm, sizeof(ar_params)));
+    HIPTRY(hipMalloc(&a.d_seed, std::max<size_t>(len, 1)));
+    HIPTRY(hipMalloc(&a.d_best, sizeof(unsigned long long)));
+    HIPTRY(hipMalloc(&a.d_res, sizeof(ar_result)));
+    HIPTRY(hipMalloc(&a.d_priv, 4 * sizeof(uint64_t)));
+    HIPTRY(hipMalloc(&a.d_ok, sizeof(uint32_t)));
+    HIPTRY(hipMemcpyAsync(a.d_prm, &hp, sizeof hp, hipMemcpyHostToDevice, sh.stream));
+    if (len) HIPTRY(hipMemcpyAsync(a.d_seed, seed, len, hipMemcpyHostToDevice, sh.stream));
+    HIPTRY(hipMemsetAsync(a.d_best, 0xFF, sizeof(unsigned long long), sh.stream));
+    HIPTRY(ar_launch_midstate(sh.stream, a.d_seed, nfull, (uint64_t*)a.d_prm));  // mid[] is at offset 0
+    if (mode == 1) {
+      HIPTRY(hipMemcpyAsync(a.d_priv, pw, sizeof pw, hipMemcpyHostToDevice, sh.stream));
+      HIPTRY(ar_launch_pubkeys(sh.stream, a.d_priv, 1, sh.d_table, &a.d_prm->pub_s, a.d_ok));
+    }
+  }
+  for (auto& sh : g_shards) {
+    HIPTRY(hipSetDevice(sh.dev));
+    HIPTRY(hipStreamSynchronize(sh.stream));
+  }
+  if (mode == 1) {
+    uint32_t ok = 0;
+    HIPTRY(hipSetDevice(g_shards[0].dev));
+    HIPTRY(hipMemcpy(&ok, as[0].d_ok, sizeof ok, hipMemcpyDeviceToHost));
+    if (!ok) return set_err(BMPOW_E_ARG, "signing private key is zero");
+  }
+  const uint64_t end = (kU64Max - start < max_tries) ? kU64Max : start + max_tries;
+  uint64_t step = 4096;
+  for (int b = 0; b < null_bytes && step < kAddrMaxStep; ++b) step = std::min<uint64_t>(step * 256, kAddrMaxStep);
+  step = std::max<uint64_t>(step / 4, 4096);
+  uint64_t next = start;
+  while (next < end) {
+    if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
+    uint64_t lo[64], cnt[64];
+    for (size_t s = 0; s < S && s < 64; ++s) {
+      lo[s] = next + s * step;
+      cnt[s] = lo[s] >= end ? 0 : std::min<uint64_t>(step, end - lo[s]);
+      if (lo[s] < next) cnt[s] = 0;  // wrapped
+      Shard& sh = g_shards[s];
+      HIPTRY(hipSetDevice(sh.dev));
+      HIPTRY(hipEventRecord(sh.ev0, sh.stream));
+      HIPTRY(ar_launch_search(sh.stream, as[s].d_prm, sh.d_table, lo[s], (uint32_t)cnt[s], as[s].d_best));
+      HIPTRY(hipEventRecord(sh.ev1, sh.stream));
+    }
+    uint64_t best = kU64Max;
+    size_t best_s = 0;
+    double mx = 0;
+    for (size_t s = 0; s < S && s < 64; ++s) {
+      Shard& sh = g_shards[s];
+      HIPTRY(hipSetDevice(sh.dev));
+      HIPTRY(hipStreamSynchronize(sh.stream));
+      float ms = 0;
+      HIPTRY(hipEventElapsedTime(&ms, sh.ev0, sh.ev1));
+      mx = std::max<double>(mx, ms);
+      unsigned long long b = 0;
+      HIPTRY(hipMemcpy(&b, as[s].d_best, sizeof b, hipMemcpyDeviceToHost));
+      g_stats.addr_tries += cnt[s];
+      if (b < best) {
+        best = b;
+        best_s = s;
+      }
+    }
+    g_stats.addr_kernel_ms += mx;
+    g_stats.addr_launches++;
+    if (best != kU64Max) {
+      Shard& sh = g_shards[best_s];
+      HIPTRY(hipSetDevice(sh.dev));
+      HIPTRY(ar_launch_resolve(sh.stream, as[best_s].d_prm, sh.d_table, best, as[best_s].d_res));
+      ar_result r;
+      HIPTRY(hipMemcpyAsync(&r, as[best_s].d_res, sizeof r, hipMemcpyDeviceToHost, sh.stream));
+      HIPTRY(hipStreamSynchronize(sh.stream));
+      if (!r.ok) return set_err(BMPOW_E_HIP, "resolve of the found try failed");
+      std::memset(out, 0, sizeof *out);
+      out->k = r.k;
+      for (int i = 0; i < 5; ++i)
+        for (int j = 0; j < 4; ++j) out->ripe[4 * i + j] = (uint8_t)(r.ripe[i] >> (8 * j));
+      if (mode == 0) bytes_from_be_words(r.priv_s, 4, out->priv_signing);
+      else std::memcpy(out->priv_signing, priv_s, 32);
+      bytes_from_be_words(r.priv_e, 4, out->priv_encryption);
+      point_bytes(r.pub_s, out->pub_signing);
+      point_bytes(r.pub_e, out->pub_encryption);
+      return BMPOW_FOUND;
+    }
+    const uint64_t span = step * std::min<size_t>(S, 64);
+    next = (kU64Max - next < span) ? end : next + span;
+    step = std::min<uint64_t>(step * 2, kAddrMaxStep);
+  }
+  return BMPOW_NOT_FOUND;
+}
+
+}  // namespace
+
 // =======================================================================================
 // C ABI
 // =======================================================================================
@@ -900,6 +1081,69 @@ int bmpow_pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t ext
                          uint64_t expires) {
   if (ntpb >= (1ULL << 62) || extra >= (1ULL << 62)) return set_err(BMPOW_E_ARG, "difficulty above 2^62");
   return pow_sufficient(pow, len, ntpb, extra, recv_time ? recv_time : (int64_t)std::time(nullptr), expires);
+}
+
+int bmpow_pubkeys(size_t n, const uint8_t* privkeys, uint8_t* pubkeys_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (n == 0) return 0;
+  if (!privkeys || !pubkeys_out) return set_err(BMPOW_E_ARG, "null pointer");
+  if (n > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many keys");
+  Shard& sh = g_shards[0];
+  rc = ensure_table(sh);
+  if (rc < 0) return rc;
+  std::vector<uint64_t> w(4 * n);
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t k[4];
+    be_words_from_bytes(privkeys + 32 * i, k);
+    for (int j = 0; j < 4; ++j) w[4 * i + j] = k[j];
+  }
+  std::vector<ec::ge> pubs(n);
+  std::vector<uint32_t> ok(n);
+  uint64_t* d_w = nullptr;
+  ec::ge* d_p = nullptr;
+  uint32_t* d_ok = nullptr;
+  HIPTRY(hipSetDevice(sh.dev));
+  hipError_t e = hipMalloc(&d_w, w.size() * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMalloc(&d_p, n * sizeof(ec::ge));
+  if (e == hipSuccess) e = hipMalloc(&d_ok, n * sizeof(uint32_t));
+  if (e == hipSuccess) e = hipMemcpyAsync(d_w, w.data(), w.size() * sizeof(uint64_t), hipMemcpyHostToDevice, sh.stream);
+  if (e == hipSuccess) e = ar_launch_pubkeys(sh.stream, d_w, (uint32_t)n, sh.d_table, d_p, d_ok);
+  if (e == hipSuccess) e = hipMemcpyAsync(pubs.data(), d_p, n * sizeof(ec::ge), hipMemcpyDeviceToHost, sh.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(ok.data(), d_ok, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sh.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
+  (void)hipFree(d_w);
+  (void)hipFree(d_p);
+  (void)hipFree(d_ok);
+  if (e != hipSuccess) return set_err(BMPOW_E_HIP, std::string("bmpow_pubkeys: ") + hipGetErrorString(e));
+  for (size_t i = 0; i < n; ++i) {
+    if (ok[i]) point_bytes(pubs[i], pubkeys_out + 65 * i);
+    else std::memset(pubkeys_out + 65 * i, 0, 65);
+  }
+  return 0;
+}
+
+int bmpow_address_search(const uint8_t* passphrase, size_t len, uint64_t start, uint64_t max_tries, int null_bytes,
+                         bmpow_address* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  std::vector<AddrShard> as;
+  rc = addr_search_locked(0, passphrase, len, nullptr, start, max_tries, null_bytes, out, as);
+  addr_free(as);
+  return rc;
+}
+
+int bmpow_address_search_random(const uint8_t priv_signing[32], const uint8_t* seed, size_t seed_len, uint64_t start,
+                                uint64_t max_tries, int null_bytes, bmpow_address* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  std::vector<AddrShard> as;
+  rc = addr_search_locked(1, seed, seed_len, priv_signing, start, max_tries, null_bytes, out, as);
+  addr_free(as);
+  return rc;
 }
 
 int bmpow_get_stats(bmpow_stats* out) {

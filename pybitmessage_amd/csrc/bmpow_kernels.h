@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "secp256k1_dev.h"
+
 // One workgroup = BM_BLOCK lanes x BM_ITERS nonces = one CHUNK of a work item.
 #ifndef BM_ITERS
 #define BM_ITERS 32
@@ -49,3 +51,31 @@ hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* 
                              const unsigned long long* best, bm_result* res);
 hipError_t bm_launch_trials(hipStream_t st, const bm_obj* obj, const uint64_t* nonces, uint64_t n,
                             uint64_t* out);
+
+// RIPE-prefix address search (ar_*, bmpow_addr.hip).  Parameters are uniform per search.
+struct ar_params {
+  uint64_t mid[8];     // SHA-512 state after the key seed's full 128-byte blocks (device-written)
+  uint64_t tmpl[32];   // the seed's tail bytes (tail_len of them) as big-endian words, zero elsewhere
+  uint64_t total_len;  // key-seed bytes (passphrase, or the random seed)
+  uint32_t tail_len;   // total_len % 128
+  uint32_t null_bytes; // leading zero bytes demanded of the ripe
+  uint32_t mode;       // 0: deterministic (keys from 2k, 2k+1); 1: fixed signing key, encryption key from k
+  uint32_t pad;
+  ec::ge pub_s;        // mode 1: the signing public key (device-written)
+};
+
+struct ar_result {
+  uint64_t k;
+  uint64_t priv_s[4], priv_e[4];  // 32-byte private keys as big-endian words
+  ec::ge pub_s, pub_e;
+  uint32_t ripe[5];               // RIPEMD-160 state words (bytes little-endian)
+  uint32_t ok;
+};
+
+hipError_t ar_launch_table(hipStream_t st, ec::ge* table);
+hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, const ec::ge* table, uint64_t start, uint32_t count,
+                            unsigned long long* best);
+hipError_t ar_launch_resolve(hipStream_t st, const ar_params* prm, const ec::ge* table, uint64_t k, ar_result* out);
+hipError_t ar_launch_pubkeys(hipStream_t st, const uint64_t* privs, uint32_t n, const ec::ge* table, ec::ge* pubs,
+                             uint32_t* ok);
+hipError_t ar_launch_midstate(hipStream_t st, const uint8_t* pass, uint64_t nfull, uint64_t* mid);

@@ -19,79 +19,20 @@
 #include "bmpow_kernels.h"
 #include "sha512_dev.h"
 
-namespace bm {
-
-// ---------------------------------------------------------------------------------------
-// Generic fully-unrolled SHA-512 rounds.  State slot of a at round T is (-T) & 7; every
-// index below is a compile-time constant after template expansion, so s[] and w[] live in
-// VGPR/SGPR pairs (verified: no scratch in the ISA).
-// ---------------------------------------------------------------------------------------
-template <int T>
-BM_DEV void round_step(uint64_t (&s)[8], uint64_t (&w)[16]) {
-  constexpr int A = (8 - (T & 7)) & 7;
-  constexpr int B = (A + 1) & 7, C = (A + 2) & 7, D = (A + 3) & 7;
-  constexpr int E = (A + 4) & 7, F = (A + 5) & 7, G = (A + 6) & 7, H = (A + 7) & 7;
-  if constexpr (T >= 16) {
-    // grouped so the terms that do not depend on the nonce (per-object or compile-time)
-    // are summed first and hoisted out of the nonce loop by LICM
-    w[T & 15] = (w[(T - 7) & 15] + sig0(w[(T - 15) & 15]) + w[(T - 16) & 15]) + sig1(w[(T - 2) & 15]);
-  }
-  const uint64_t t1 = s[H] + Sig1(s[E]) + Ch(s[E], s[F], s[G]) + (K(T) + w[T & 15]);
-  s[D] += t1;
-  s[H] = t1 + Sig0(s[A]) + Maj(s[A], s[B], s[C]);
-}
-
-template <int T, int END>
-BM_DEV void rounds(uint64_t (&s)[8], uint64_t (&w)[16]) {
-  if constexpr (T < END) {
-    round_step<T>(s, w);
-    rounds<T + 1, END>(s, w);
-  }
-}
-
-// trial(n, ih) with ih given as 8 big-endian words.  Round 0 of each block is folded:
-// from the IV with W0 unknown, a1 = W0 + A1C and e1 = W0 + E1C.
-BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
-  uint64_t w[16];
-  w[0] = nonce;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w[1 + i] = ihw[i];
-  w[9] = PAD;
-#pragma unroll
-  for (int i = 10; i < 15; ++i) w[i] = 0;
-  w[15] = 72 * 8;
-  // state after the folded round 0 (round 1 has A = 7: a=s7 b=s0 c=s1 d=s2 e=s3 f=s4 g=s5 h=s6)
-  uint64_t s[8] = {IV(0), IV(1), IV(2), nonce + E1C, IV(4), IV(5), IV(6), nonce + A1C};
-  rounds<1, 80>(s, w);
-  // after 80 rounds A = 0: s[i] holds a..h in order
-  uint64_t w2[16];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w2[i] = s[i] + IV(i);
-  w2[8] = PAD;
-#pragma unroll
-  for (int i = 9; i < 15; ++i) w2[i] = 0;
-  w2[15] = 64 * 8;
-  uint64_t s2[8] = {IV(0), IV(1), IV(2), w2[0] + E1C, IV(4), IV(5), IV(6), w2[0] + A1C};
-  rounds<1, 80>(s2, w2);
-  return s2[0] + IV(0);
-}
-
-// One SHA-512 compression of a runtime block into the chaining state h.
-BM_DEV void compress(uint64_t (&h)[8], uint64_t (&w)[16]) {
-  uint64_t s[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) s[i] = h[i];
-  rounds<0, 80>(s, w);
-#pragma unroll
-  for (int i = 0; i < 8; ++i) h[i] += s[i];
-}
-
-// Big-endian 64-bit word from a little-endian 16-byte load: bytes b0..b3 are in x, b4..b7 in y.
-BM_DEV uint64_t be64(uint32_t x, uint32_t y) { return mk64(__builtin_bswap32(y), __builtin_bswap32(x)); }
-
-}  // namespace bm
-
 using namespace bm;
+
+// Out-of-line trial for the small kernels (resolve, trials): one compiled copy of the ~6,500-
+// instruction body instead of one inlined per kernel (the search kernel keeps its own inline
+// copy, with the per-object words hoisted out of its nonce loop).
+__device__ __noinline__ uint64_t trial_ool(uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3, uint64_t w4,
+                                           uint64_t w5, uint64_t w6, uint64_t w7, uint64_t nonce) {
+  const uint64_t ihw[8] = {w0, w1, w2, w3, w4, w5, w6, w7};
+  return trial_of(ihw, nonce);
+}
+
+__device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce) {
+  return trial_ool(o->w[0], o->w[1], o->w[2], o->w[3], o->w[4], o->w[5], o->w[6], o->w[7], nonce);
+}
 
 // ---------------------------------------------------------------------------------------
 // Search kernel.
@@ -160,12 +101,7 @@ __global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item
   bm_result r;
   r.nonce = n;
   r.trial = 0;
-  if (n != ~0ULL) {
-    uint64_t ihw[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ihw[i] = objs[obj].w[i];
-    r.trial = trial_of(ihw, n);
-  }
+  if (n != ~0ULL) r.trial = trial_obj(objs + obj, n);
   res[k] = r;
 }
 
@@ -175,41 +111,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_trials_kernel(const bm_obj* __res
                                                              uint64_t n, uint64_t* __restrict__ out) {
   const uint64_t k = (uint64_t)blockIdx.x * BM_BLOCK + threadIdx.x;
   if (k >= n) return;
-  uint64_t ihw[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) ihw[i] = obj->w[i];
-  out[k] = trial_of(ihw, nonces[k]);
-}
-
-// ---------------------------------------------------------------------------------------
-// Receive-side PoW value, reference src/protocol.py:280-282:
-//   POW = BE64(SHA512(SHA512(object[0:8] || SHA512(object[8:])))[0:8])
-// One lane per object.  The inner SHA512(object[8:]) runs over the host-padded blocks of the
-// pool (16-B loads, byte-swapped into the big-endian schedule words); its digest words are the
-// initialHash words of the trial function, so the outer double hash is trial_of(H, nonce).
-// Integer-VALU bound: ~3,300 VALU instructions per 128-B block, 0 bytes re-read.
-// ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BV_BLOCK) void bv_pow_kernel(const bv_obj* __restrict__ objs, uint32_t n,
-                                                          const uint4* __restrict__ pool,
-                                                          uint64_t* __restrict__ pow_out) {
-  const uint32_t k = blockIdx.x * BV_BLOCK + threadIdx.x;
-  if (k >= n) return;
-  const bv_obj o = objs[k];
-  uint64_t h[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) h[i] = IV(i);
-  const uint4* p = pool + (uint64_t)o.blk * 8;
-  for (uint32_t b = 0; b < o.nblk; ++b, p += 8) {
-    uint64_t w[16];
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const uint4 v = p[j];
-      w[2 * j] = be64(v.x, v.y);
-      w[2 * j + 1] = be64(v.z, v.w);
-    }
-    compress(h, w);
-  }
-  pow_out[k] = trial_of(h, o.nonce);
+  out[k] = trial_obj(obj, nonces[k]);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -227,13 +129,6 @@ hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* 
   const uint32_t bs = 64;
   hipLaunchKernelGGL(bm_resolve_kernel, dim3((nitems + bs - 1) / bs), dim3(bs), 0, st, objs, items, nitems,
                      best, res);
-  return hipGetLastError();
-}
-
-hipError_t bv_launch_pow(hipStream_t st, const bv_obj* objs, uint32_t n, const uint4* pool, uint64_t* pow_out) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(bv_pow_kernel, dim3((n + BV_BLOCK - 1) / BV_BLOCK), dim3(BV_BLOCK), 0, st, objs, n, pool,
-                     pow_out);
   return hipGetLastError();
 }
 

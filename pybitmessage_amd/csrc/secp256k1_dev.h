@@ -1,0 +1,314 @@
+// secp256k1_dev.h -- gfx950 field and group arithmetic for the RIPE-prefix address search.
+//
+// The reference turns a private key into a public key with OpenSSL EC_POINT_mul on secp256k1
+// (src/highlevelcrypto.py:111-140, pointMult).  Here one lane computes k*G for its own k:
+//   * field elements mod p = 2^256 - 2^32 - 977 as 8 x 32-bit little-endian limbs, always fully
+//     reduced; products by v_mad_u64_u32 (operand scanning), reduction by 2^256 = 2^32 + 977;
+//   * k*G by a fixed-base comb: 32 byte windows, table[i][v] = v * 2^(8i) * G in affine
+//     coordinates (512 KB, built once per device by ar_table_kernel, L2 resident), so one
+//     scalar multiplication is 32 mixed Jacobian+affine additions and one inversion;
+//   * inversion by Fermat (a^(p-2)) with the 255-squaring / 15-multiplication addition chain
+//     for the exponent's bit pattern [223 ones][0][22 ones][0000101101].
+#pragma once
+#include <stdint.h>
+
+#ifndef BM_DEV
+#define BM_DEV __device__ __forceinline__
+#endif
+
+namespace ec {
+
+struct fe {
+  uint32_t d[8];
+};
+
+struct ge {  // affine point (table entry); 64 B
+  fe x, y;
+};
+
+struct gej {  // Jacobian point; inf marks the point at infinity
+  fe x, y, z;
+  bool inf;
+};
+
+// 2^256 - p = 2^32 + 977
+constexpr uint32_t C0 = 977;
+
+BM_DEV void fe_set(fe& r, uint32_t v) {
+  r.d[0] = v;
+#pragma unroll
+  for (int i = 1; i < 8; ++i) r.d[i] = 0;
+}
+
+BM_DEV bool fe_is_zero(const fe& a) {
+  uint32_t o = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o |= a.d[i];
+  return o == 0;
+}
+
+// r = t mod p for t < 2^256 + small carry c (c in {0,1} after the callers' folds): returns
+// t - p when t >= p.  t >= p  <=>  t + (2^256 - p) carries out of 256 bits.
+BM_DEV void fe_cond_sub_p(fe& r, const uint32_t (&t)[8], uint32_t carry) {
+  uint32_t u[8];
+  uint64_t c = (uint64_t)t[0] + C0;
+  u[0] = (uint32_t)c;
+  c = (c >> 32) + (uint64_t)t[1] + 1;
+  u[1] = (uint32_t)c;
+  c >>= 32;
+#pragma unroll
+  for (int i = 2; i < 8; ++i) {
+    c += t[i];
+    u[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  const bool ge_p = (c | carry) != 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r.d[i] = ge_p ? u[i] : t[i];
+}
+
+BM_DEV void fe_add(fe& r, const fe& a, const fe& b) {
+  uint32_t t[8];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (uint64_t)a.d[i] + b.d[i];
+    t[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  fe_cond_sub_p(r, t, (uint32_t)c);
+}
+
+BM_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
+  uint32_t t[8];
+  uint32_t bw = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint64_t v = (uint64_t)a.d[i] - b.d[i] - bw;
+    t[i] = (uint32_t)v;
+    bw = (uint32_t)(v >> 32) & 1;
+  }
+  // on borrow add p back: t + p = t - (2^32 + 977) mod 2^256
+  const uint32_t m = 0u - bw;
+  uint64_t v = (uint64_t)t[0] - (C0 & m);
+  r.d[0] = (uint32_t)v;
+  uint32_t b2 = (uint32_t)(v >> 32) & 1;
+  v = (uint64_t)t[1] - (1u & m) - b2;
+  r.d[1] = (uint32_t)v;
+  b2 = (uint32_t)(v >> 32) & 1;
+#pragma unroll
+  for (int i = 2; i < 8; ++i) {
+    v = (uint64_t)t[i] - b2;
+    r.d[i] = (uint32_t)v;
+    b2 = (uint32_t)(v >> 32) & 1;
+  }
+}
+
+// r = 2a, 3a, 8a as additions (cheap, exact)
+BM_DEV void fe_dbl(fe& r, const fe& a) { fe_add(r, a, a); }
+
+BM_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
+  uint32_t p[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) p[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      c += (uint64_t)a.d[i] * b.d[j] + p[i + j];  // <= (2^32-1)^2 + 2(2^32-1) < 2^64
+      p[i + j] = (uint32_t)c;
+      c >>= 32;
+    }
+    p[i + 8] = (uint32_t)c;
+  }
+  // fold the high half: L + H * (2^32 + 977)
+  uint32_t t[8];
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (uint64_t)p[i] + (uint64_t)p[8 + i] * C0 + (i ? p[7 + i] : 0u);
+    t[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  c += p[15];  // the H * 2^32 term's top limb; now value = t + c * 2^256, c < 2^34
+  // fold c * (2^32 + 977)
+  uint64_t d = (uint64_t)t[0] + c * C0;
+  t[0] = (uint32_t)d;
+  d = (d >> 32) + (uint64_t)t[1] + c;
+  t[1] = (uint32_t)d;
+  d >>= 32;
+#pragma unroll
+  for (int i = 2; i < 8; ++i) {
+    d += t[i];
+    t[i] = (uint32_t)d;
+    d >>= 32;
+  }
+  // d in {0,1}: one more fold of 2^256 (t is tiny when it happens)
+  const uint32_t m = 0u - (uint32_t)d;
+  uint64_t e = (uint64_t)t[0] + (C0 & m);
+  t[0] = (uint32_t)e;
+  e = (e >> 32) + (uint64_t)t[1] + (1u & m);
+  t[1] = (uint32_t)e;
+  e >>= 32;
+#pragma unroll
+  for (int i = 2; i < 8; ++i) {
+    e += t[i];
+    t[i] = (uint32_t)e;
+    e >>= 32;
+  }
+  fe_cond_sub_p(r, t, (uint32_t)e);
+}
+
+BM_DEV void fe_sqr(fe& r, const fe& a) { fe_mul(r, a, a); }
+
+// a^(p-2) = a^-1 (a != 0).  The exponent is [223 ones][0][22 ones][0000101101]; the 255-
+// squaring / 15-multiplication addition chain (runs of 2^n - 1 ones: 1, 2, 3, 6, 9, 11, 22, 44,
+// 88, 176, 220, 223) runs as a rolled loop of (squarings, multiplier) steps so the kernel holds
+// one squaring and one multiplication body instead of 37 inlined copies.
+BM_DEV void fe_inv(fe& r, const fe& a) {
+  // step s: t = t^(2^N[s]) * mult[M[s]]; mult: 0 a, 1 x2, 2 x3, 3 x11, 4 x22, 5 x44, 6 x88
+  constexpr uint8_t N[15] = {1, 1, 3, 3, 2, 11, 22, 44, 88, 44, 3, 23, 5, 3, 2};
+  constexpr uint8_t M[15] = {0, 0, 2, 2, 1, 3, 4, 5, 6, 5, 2, 4, 0, 1, 0};
+  fe t = a, x2 = a, x3 = a, x11 = a, x22 = a, x44 = a, x88 = a;
+#pragma unroll 1
+  for (int s = 0; s < 15; ++s) {
+#pragma unroll 1
+    for (int i = 0; i < N[s]; ++i) fe_mul(t, t, t);
+    const int m = M[s];
+    fe f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      f.d[j] = m == 0 ? a.d[j]
+             : m == 1 ? x2.d[j]
+             : m == 2 ? x3.d[j]
+             : m == 3 ? x11.d[j]
+             : m == 4 ? x22.d[j]
+             : m == 5 ? x44.d[j]
+                      : x88.d[j];
+    fe_mul(t, t, f);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      x2.d[j] = s == 0 ? t.d[j] : x2.d[j];
+      x3.d[j] = s == 1 ? t.d[j] : x3.d[j];
+      x11.d[j] = s == 4 ? t.d[j] : x11.d[j];
+      x22.d[j] = s == 5 ? t.d[j] : x22.d[j];
+      x44.d[j] = s == 6 ? t.d[j] : x44.d[j];
+      x88.d[j] = s == 7 ? t.d[j] : x88.d[j];
+    }
+  }
+  r = t;
+}
+
+// ---- group law (y^2 = x^3 + 7, a = 0) ----
+
+// dbl-2009-l: 2M + 5S
+BM_DEV void gej_double(gej& r, const gej& p) {
+  if (p.inf || fe_is_zero(p.y)) {
+    r.inf = true;
+    return;
+  }
+  fe A, B, C, D, E, F, t;
+  fe_sqr(A, p.x);
+  fe_sqr(B, p.y);
+  fe_sqr(C, B);
+  fe_add(t, p.x, B);
+  fe_sqr(t, t);
+  fe_sub(t, t, A);
+  fe_sub(t, t, C);
+  fe_dbl(D, t);
+  fe_dbl(E, A);
+  fe_add(E, E, A);
+  fe_sqr(F, E);
+  fe_mul(r.z, p.y, p.z);  // before r.x/r.y overwrite p (r may alias p)
+  fe_dbl(r.z, r.z);
+  fe_dbl(t, D);
+  fe_sub(r.x, F, t);
+  fe_sub(t, D, r.x);
+  fe_mul(t, E, t);
+  fe_dbl(C, C);
+  fe_dbl(C, C);
+  fe_dbl(C, C);
+  fe_sub(r.y, t, C);
+  r.inf = false;
+}
+
+// r = p + q with q affine (8M + 3S); handles p = inf, p = q, p = -q.
+BM_DEV void gej_add_ge(gej& r, const gej& p, const ge& q) {
+  if (p.inf) {
+    r.x = q.x;
+    r.y = q.y;
+    fe_set(r.z, 1);
+    r.inf = false;
+    return;
+  }
+  fe z1z1, u2, s2, h, rr, hh, hhh, v, t;
+  fe_sqr(z1z1, p.z);
+  fe_mul(u2, q.x, z1z1);
+  fe_mul(s2, q.y, p.z);
+  fe_mul(s2, s2, z1z1);
+  fe_sub(h, u2, p.x);
+  fe_sub(rr, s2, p.y);
+  if (fe_is_zero(h)) {
+    if (fe_is_zero(rr)) {
+      gej_double(r, p);
+    } else {
+      r.inf = true;
+    }
+    return;
+  }
+  fe_sqr(hh, h);
+  fe_mul(hhh, h, hh);
+  fe_mul(v, p.x, hh);
+  fe_mul(r.z, p.z, h);
+  fe_mul(t, p.y, hhh);  // Y1 * HHH, before r.y overwrites p.y
+  fe x3;
+  fe_sqr(x3, rr);
+  fe_sub(x3, x3, hhh);
+  fe_sub(x3, x3, v);
+  fe_sub(x3, x3, v);
+  fe_sub(v, v, x3);
+  fe_mul(v, rr, v);
+  fe_sub(r.y, v, t);
+  r.x = x3;
+  r.inf = false;
+}
+
+// Jacobian -> affine (p not at infinity)
+BM_DEV void gej_to_ge(ge& r, const gej& p) {
+  fe zi, zi2;
+  fe_inv(zi, p.z);
+  fe_sqr(zi2, zi);
+  fe_mul(r.x, p.x, zi2);
+  fe_mul(zi2, zi2, zi);
+  fe_mul(r.y, p.y, zi2);
+}
+
+// k*G for the 256-bit scalar given as 4 big-endian 64-bit words (k = w0*2^192 + ... + w3),
+// i.e. the first 32 bytes of a SHA-512 digest read as a big-endian integer (BN_bin2bn).
+// Returns false for k = 0 (the point at infinity).
+BM_DEV bool scalar_mult_base(ge& r, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
+  gej acc;
+  acc.inf = true;
+#pragma unroll 1
+  for (int i = 0; i < 32; ++i) {
+    const uint32_t v = (uint32_t)(kw[3 - (i >> 3)] >> (8 * (i & 7))) & 0xff;  // byte i, LSB first
+    if (v) {
+      const ge q = table[i * 256 + v];
+      gej_add_ge(acc, acc, q);
+    }
+  }
+  if (acc.inf) return false;
+  gej_to_ge(r, acc);
+  return true;
+}
+
+// 4 big-endian 64-bit words of a field element (the 32-byte big-endian serialization)
+BM_DEV void fe_to_be64(uint64_t (&w)[4], const fe& a) {
+  w[0] = ((uint64_t)a.d[7] << 32) | a.d[6];
+  w[1] = ((uint64_t)a.d[5] << 32) | a.d[4];
+  w[2] = ((uint64_t)a.d[3] << 32) | a.d[2];
+  w[3] = ((uint64_t)a.d[1] << 32) | a.d[0];
+}
+
+}  // namespace ec

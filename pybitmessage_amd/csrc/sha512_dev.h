@@ -80,18 +80,12 @@ BM_DEV uint64_t shr(uint64_t x) {
 // v_xor_b32 at ~118 and v_bfi_b32 at ~63, so one bitop3 (1/77) beats the xor pair the
 // compiler selects for a^b^c (2/118) and the bfi it selects for Ch.  hipcc does not form
 // bitop3 for two-op trees by itself, hence the builtin.  LUT bits: S0 = 0xF0, S1 = 0xCC,
-// S2 = 0xAA.  Operands that are compile-time constants fold through plain C instead (the
-// builtin is opaque to constant folding).
+// S2 = 0xAA.
 template <uint8_t LUT>
 BM_DEV uint32_t bitop3(uint32_t a, uint32_t b, uint32_t c) {
-  if (__builtin_constant_p(a) && __builtin_constant_p(b) && __builtin_constant_p(c)) {
-    uint32_t r = 0;
-    for (int i = 0; i < 32; ++i) {
-      const int idx = (((a >> i) & 1) << 2) | (((b >> i) & 1) << 1) | ((c >> i) & 1);
-      r |= (uint32_t)((LUT >> idx) & 1) << i;
-    }
-    return r;
-  }
+  // No constant-folding path: a __builtin_constant_p branch here is resolved only late in the
+  // pipeline, so every call dragged a folding body through inlining and scheduling (the
+  // SHA-512 compression took ~5 min to compile).  No call site has three constant operands.
   return __builtin_amdgcn_bitop3_b32(a, b, c, LUT);
 }
 
@@ -142,5 +136,74 @@ constexpr uint64_t A1C = T1C + cSig0(IV(0)) + cMaj(IV(0), IV(1), IV(2));
 constexpr uint64_t E1C = IV(3) + T1C;
 
 constexpr uint64_t PAD = 0x8000000000000000ULL;
+
+// ---------------------------------------------------------------------------------------
+// Generic fully-unrolled SHA-512 rounds.  State slot of a at round T is (-T) & 7; every
+// index below is a compile-time constant after template expansion, so s[] and w[] live in
+// VGPR/SGPR pairs (verified: no scratch in the ISA).
+// ---------------------------------------------------------------------------------------
+template <int T>
+BM_DEV void round_step(uint64_t (&s)[8], uint64_t (&w)[16]) {
+  constexpr int A = (8 - (T & 7)) & 7;
+  constexpr int B = (A + 1) & 7, C = (A + 2) & 7, D = (A + 3) & 7;
+  constexpr int E = (A + 4) & 7, F = (A + 5) & 7, G = (A + 6) & 7, H = (A + 7) & 7;
+  if constexpr (T >= 16) {
+    // grouped so the terms that do not depend on the nonce (per-object or compile-time)
+    // are summed first and hoisted out of the nonce loop by LICM
+    w[T & 15] = (w[(T - 7) & 15] + sig0(w[(T - 15) & 15]) + w[(T - 16) & 15]) + sig1(w[(T - 2) & 15]);
+  }
+  const uint64_t t1 = s[H] + Sig1(s[E]) + Ch(s[E], s[F], s[G]) + (K(T) + w[T & 15]);
+  s[D] += t1;
+  s[H] = t1 + Sig0(s[A]) + Maj(s[A], s[B], s[C]);
+}
+
+template <int T, int END>
+BM_DEV void rounds(uint64_t (&s)[8], uint64_t (&w)[16]) {
+  if constexpr (T < END) {
+    round_step<T>(s, w);
+    rounds<T + 1, END>(s, w);
+  }
+}
+
+// trial(n, ih) with ih given as 8 big-endian words.  Round 0 of each block is folded:
+// from the IV with W0 unknown, a1 = W0 + A1C and e1 = W0 + E1C.
+BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
+  uint64_t w[16];
+  w[0] = nonce;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[1 + i] = ihw[i];
+  w[9] = PAD;
+#pragma unroll
+  for (int i = 10; i < 15; ++i) w[i] = 0;
+  w[15] = 72 * 8;
+  // state after the folded round 0 (round 1 has A = 7: a=s7 b=s0 c=s1 d=s2 e=s3 f=s4 g=s5 h=s6)
+  uint64_t s[8] = {IV(0), IV(1), IV(2), nonce + E1C, IV(4), IV(5), IV(6), nonce + A1C};
+  rounds<1, 80>(s, w);
+  // after 80 rounds A = 0: s[i] holds a..h in order
+  uint64_t w2[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w2[i] = s[i] + IV(i);
+  w2[8] = PAD;
+#pragma unroll
+  for (int i = 9; i < 15; ++i) w2[i] = 0;
+  w2[15] = 64 * 8;
+  uint64_t s2[8] = {IV(0), IV(1), IV(2), w2[0] + E1C, IV(4), IV(5), IV(6), w2[0] + A1C};
+  rounds<1, 80>(s2, w2);
+  return s2[0] + IV(0);
+}
+
+// One SHA-512 compression of a runtime block into the chaining state h.
+BM_DEV void compress(uint64_t (&h)[8], uint64_t (&w)[16]) {
+  uint64_t s[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = h[i];
+  rounds<0, 80>(s, w);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] += s[i];
+}
+
+// Big-endian 64-bit word from a little-endian 16-byte load: bytes b0..b3 are in x, b4..b7 in y.
+BM_DEV uint64_t be64(uint32_t x, uint32_t y) { return mk64(__builtin_bswap32(y), __builtin_bswap32(x)); }
+
 
 }  // namespace bm
