@@ -312,6 +312,81 @@ def cpu_verify_baseline(seconds):
             'sample': '%d objects of the same flood hashed by hashlib (OpenSSL) in %.1f s, 1 thread' % (k, el)}
 
 
+ADDR_PASSPHRASE = b'bmpow address-search benchmark'
+
+
+def run_addr_bench(args, dist):
+    """Deterministic address search (class_addressGenerator.py:238-271) at --null-bytes
+    (default 3: ~16.7M expected tries, a "vanity" request the reference would take hours on),
+    repeated from try 0 each step; useful tries = found k + 1 (the sequential loop's count)."""
+    import ctypes
+
+    from pybitmessage_amd import _lib, addressgen
+    lib = _lib.get()
+    pp = ADDR_PASSPHRASE + b' rank %d' % dist.rank
+    nb = args.null_bytes
+    for _ in range(args.warmup):
+        f = addressgen.search_deterministic(pp, nb)
+    dist.barrier()
+    lib.bmpow_reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        f = addressgen.search_deterministic(pp, nb)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = _lib.BmpowStats()
+    lib.bmpow_get_stats(ctypes.byref(st))
+    assert f.ripe[:nb] == b'\x00' * nb
+    return {'desc': 'addrgen: deterministic address search, %d null bytes, passphrase %r, found k=%d' % (nb, pp, f.k),
+            'tries': float(f.k + 1) * args.steps, 'elapsed': elapsed, 'stats': st, 'k': f.k}
+
+
+def summarize_addr(args, dist, r, lib_version):
+    st = r['stats']
+    el_max = dist.reduce(r['elapsed'], 'max')
+    tries = dist.reduce(r['tries'], 'sum')
+    launched = dist.reduce(st.addr_tries, 'sum')
+    line = {
+        'metric': 'address-search tries/sec (2 x secp256k1 k*G + SHA-512 + RIPEMD-160 per try)',
+        'value': round(tries / el_max, 1), 'unit': 'tries/s', 'n_gpus': dist.world, 'steps': args.steps,
+        'warmup': args.warmup, 'ms_per_step': round(el_max * 1e3 / args.steps, 3), 'higher_is_better': True,
+        'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32', 'data': 'synthetic',
+        'config': {'workload': r['desc'], 'parallelism': 'dp%d' % dist.world, 'lib': lib_version},
+        'launched_tries_per_s': round(launched / el_max, 1),
+    }
+    if st.addr_kernel_ms > 0:
+        line['kernel'] = {'name': 'ar_search_kernel', 'tries_per_s': round(st.addr_tries / (st.addr_kernel_ms * 1e-3), 1),
+                          'launches': int(st.addr_launches), 'kernel_ms': round(st.addr_kernel_ms, 3),
+                          'kernel_busy_frac': round(st.addr_kernel_ms * 1e-3 / r['elapsed'], 4)}
+    return line
+
+
+def cpu_addr_baseline(seconds):
+    """One core: the reference's per-try work with the same library calls it makes -- OpenSSL
+    EC_POINT_mul for both keys (oracle.addrgen_oracle.OpenSSLPointMult), hashlib SHA-512, and
+    RIPEMD-160 (hashlib when OpenSSL's legacy provider is loaded, else the oracle's)."""
+    import hashlib as hl
+
+    from oracle import addrgen_oracle as ao
+    pm = ao.OpenSSLPointMult()
+    try:
+        hl.new('ripemd160')
+        rmd = lambda m: hl.new('ripemd160', m).digest()  # noqa: E731
+        which = 'hashlib'
+    except ValueError:
+        rmd, which = ao.ripemd160, 'pure-Python restatement'
+    t0 = time.perf_counter()
+    k = 0
+    while time.perf_counter() - t0 < seconds:
+        ps, pe = ao.try_keys(ADDR_PASSPHRASE, k)
+        rmd(hl.sha512(pm(ps) + pm(pe)).digest())
+        k += 1
+    el = time.perf_counter() - t0
+    return {'value': round(k / el, 1), 'unit': 'tries/s', 'cores': 1, 'kind': 'port',
+            'sample': '%d tries in %.1f s: OpenSSL EC_POINT_mul x2 (system libcrypto, as pyelliptic calls it), '
+                      'hashlib SHA-512, RIPEMD-160 via %s; 1 thread' % (k, el, which)}
+
+
 # ----------------------------------------------------------------------------------------
 # CPU baseline (rank 0, N=1): the reference's own BitmessagePOW built from its source
 # ----------------------------------------------------------------------------------------
@@ -367,7 +442,8 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--config', default='c2', choices=['c1', 'c2', 'c3', 'c4', 'c5', 'verify'])
+    ap.add_argument('--config', default='c2', choices=['c1', 'c2', 'c3', 'c4', 'c5', 'verify', 'addrgen'])
+    ap.add_argument('--null-bytes', type=int, default=3, help='addrgen: leading zero bytes of the ripe')
     ap.add_argument('--objects', type=int, default=None, help='override the object count (c2/c4/c5)')
     ap.add_argument('--c3-log2', type=int, default=36)
     ap.add_argument('--step-trials', type=int, default=0, help='per-launch trial budget per GPU (0 = lib default)')
@@ -387,6 +463,15 @@ def main():
     if args.step_trials:
         lib.bmpow_set_step_trials(args.step_trials)
 
+    if args.config == 'addrgen':
+        r = run_addr_bench(args, dist)
+        line = summarize_addr(args, dist, r, lib.bmpow_version().decode())
+        if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
+            line['cpu_baseline'] = cpu_addr_baseline(min(args.cpu_seconds, 10.0))
+        if dist.rank == 0:
+            print(json.dumps(line), flush=True)
+        dist.close()
+        return
     if args.config == 'verify':
         r = run_verify_bench(args, dist)
         line = summarize_verify(args, dist, r, lib.bmpow_version().decode())
