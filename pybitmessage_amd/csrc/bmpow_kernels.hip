@@ -40,8 +40,11 @@ __device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce) {
 #ifndef BM_MIN_WAVES
 #define BM_MIN_WAVES 1
 #endif
+#ifndef BM_MAX_WAVES
+#define BM_MAX_WAVES 8
+#endif
 #if BM_MIN_WAVES > 0
-#define BM_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(BM_MIN_WAVES, 8)))
+#define BM_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(BM_MIN_WAVES, BM_MAX_WAVES)))
 #else
 #define BM_WAVES_ATTR
 #endif
