@@ -118,6 +118,11 @@ class Dist(object):
         self.dist.all_reduce(t, op={'max': self.dist.ReduceOp.MAX, 'sum': self.dist.ReduceOp.SUM}[op])
         return float(t.item())
 
+    def store(self):
+        """The process group's TCP store (host-side key/value; used for work claiming)."""
+        from torch.distributed import distributed_c10d
+        return distributed_c10d._get_default_store()
+
     def close(self):
         if self.dist:
             self.dist.destroy_process_group()
@@ -134,29 +139,80 @@ def solve_batch(lib, h, budget=0):
         pending = _lib.check(lib, lib.bmpow_batch_step(h, budget), 'bmpow_batch_step')
 
 
+class Claimer(object):
+    """Hands out pieces of the global batch to ranks on demand: a shared counter in the
+    torch.distributed TCP store (host-side coordination only; no data moves).  With one rank it
+    is a local counter that hands out everything at once."""
+
+    def __init__(self, dist, n, chunk):
+        self.n, self.chunk = n, chunk
+        self.store = dist.store() if dist.world > 1 else None
+        self.key, self.local = None, 0
+
+    def start(self, tag):
+        self.key, self.local = 'bmpow_claim_%s' % tag, 0
+
+    def claim(self):
+        if self.store is not None:
+            lo = int(self.store.add(self.key, self.chunk)) - self.chunk
+        else:
+            lo, self.local = self.local, self.local + self.chunk
+        return None if lo >= self.n else (lo, min(lo + self.chunk, self.n))
+
+
+def solve_claimed(lib, h, claimer, tag, low_water):
+    """Solve the pieces of the global batch this rank claims: the whole table is resident and
+    parked; pieces are scheduled (bmpow_batch_set_pending) whenever fewer than low_water objects
+    are pending, so every rank keeps its GPU busy until the global batch runs out."""
+    from pybitmessage_amd import _lib
+    _lib.check(lib, lib.bmpow_batch_reset(h, None), 'bmpow_batch_reset')
+    _lib.check(lib, lib.bmpow_batch_set_pending(h, 0, claimer.n, 0), 'bmpow_batch_set_pending')
+    claimer.start(tag)
+    mine, pending, exhausted = [], 0, False
+    while True:
+        while not exhausted and pending < low_water:
+            r = claimer.claim()
+            if r is None:
+                exhausted = True
+                break
+            pending = _lib.check(lib, lib.bmpow_batch_set_pending(h, r[0], r[1] - r[0], 1), 'set_pending')
+            mine.append(r)
+        if pending == 0:
+            return mine
+        pending = _lib.check(lib, lib.bmpow_batch_step(h, 0), 'bmpow_batch_step')
+
+
 def run_batch_bench(args, dist):
+    """C2/C4/C5 over one global batch of objects-per-GPU x world objects.  Every rank holds the
+    whole table in HBM (128 B/object) and claims pieces of it on demand, so all GPUs finish
+    together (weak scaling without the max-over-ranks penalty of a fixed random split)."""
     import ctypes
 
     import numpy as np
 
     from pybitmessage_amd import _lib, proofofwork
-    objs, desc = make_objects(args.config, dist.rank, args.objects)
+    per_gpu = args.objects or {'c2': 1024, 'c4': 64, 'c5': 100000}[args.config]
+    objs, desc = make_objects(args.config, 0, per_gpu * dist.world)
     lib = _lib.get()
     n = len(objs)
     ihs = b''.join(ih for _, ih in objs)
     tg = np.array([t for t, _ in objs], dtype=np.uint64)
     p64 = ctypes.POINTER(ctypes.c_uint64)
+    chunk = n if dist.world == 1 else max(1, min(8, per_gpu // 8))
+    low_water = max(chunk, min(128, per_gpu // 4))
+    claimer = Claimer(dist, n, chunk)
     h = lib.bmpow_batch_create(n, ihs, tg.ctypes.data_as(p64), None)
     if not h:
         raise RuntimeError('bmpow_batch_create: %s' % lib.bmpow_last_error().decode())
     try:
-        for _ in range(args.warmup):
-            solve_batch(lib, h)
+        for w in range(args.warmup):
+            solve_claimed(lib, h, claimer, 'w%d' % w, low_water)
         dist.barrier()
         lib.bmpow_reset_stats()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
-            solve_batch(lib, h)
+        mine = []
+        for k in range(args.steps):
+            mine = solve_claimed(lib, h, claimer, 's%d' % k, low_water)
         dist.barrier()
         elapsed = time.perf_counter() - t0
         st = _lib.BmpowStats()
@@ -168,13 +224,16 @@ def run_batch_bench(args, dist):
                                 done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), None)
     finally:
         lib.bmpow_batch_destroy(h)
-    # every answer re-checked on the host: trial(nonce) <= target with hashlib
-    assert (done == _lib.DONE_FOUND).all()
-    for i in range(n):
+    # every answer of the last step re-checked on the host: trial(nonce) <= target with hashlib
+    idx = [i for lo, hi in mine for i in range(lo, hi)]
+    assert all(done[i] == _lib.DONE_FOUND for i in idx)
+    for i in idx:
         proofofwork._verify(int(tg[i]), objs[i][1], int(trial[i]), int(nonce[i]))
-    useful = float(nonce.astype(np.float64).sum()) * args.steps
-    return {'desc': desc, 'objects': n * args.steps, 'useful': useful, 'elapsed': elapsed, 'stats': st,
-            'nonces_sum': int(nonce.astype(object).sum())}
+    useful = float(sum(int(nonce[i]) for i in idx)) * args.steps
+    if dist.world > 1:
+        desc += ' (global batch of %d, pieces of %d claimed on demand)' % (n, chunk)
+    return {'desc': desc, 'objects': len(idx) * args.steps, 'useful': useful, 'elapsed': elapsed, 'stats': st,
+            'nonces_sum': int(sum(int(nonce[i]) for i in idx))}
 
 
 def run_c3_bench(args, dist):
@@ -247,7 +306,7 @@ def run_verify_bench(args, dist):
     import ctypes
 
     from pybitmessage_amd import _lib, targets, verify
-    n = args.objects or 200000
+    n = args.objects or 500000  # an inventory sync's worth of objects (--objects to change)
     objs = verify_objects(n, dist.rank)
     payload_bytes = sum(len(o) - 8 for o in objs)
     lib = _lib.get()
@@ -450,6 +509,7 @@ def main():
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--share-device', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--cpu-baseline-worker', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_baseline_worker:
@@ -457,7 +517,9 @@ def main():
         return
 
     dist = Dist()
-    os.environ['BMPOW_DEVICES'] = str(dist.local_rank)  # one process per GPU
+    # one process per GPU; --share-device puts every rank on GPU 0 (rehearsing the multi-rank
+    # path on a one-GPU box: the ranks then split one GPU, so the value is not a scaling number)
+    os.environ['BMPOW_DEVICES'] = '0' if args.share_device else str(dist.local_rank)
     from pybitmessage_amd import _lib
     lib = _lib.get()
     if args.step_trials:

@@ -49,6 +49,7 @@ extern "C" {
 #define BMPOW_PENDING 0
 #define BMPOW_DONE_FOUND 1
 #define BMPOW_DONE_EXHAUSTED 2 /* reached nonce 2^64-1 without a hit */
+#define BMPOW_PARKED 3         /* in the table but not scheduled (bmpow_batch_set_pending) */
 
 /* ---- lifecycle (replaces proofofwork.init / bmpow global, src/proofofwork.py:336-394) ---- */
 
@@ -120,6 +121,12 @@ BMPOW_API int bmpow_batch_results(const bmpow_batch *b, uint64_t *nonce_out, uin
 /* Restart every object at nonce `start` (NULL = 1) without re-uploading the object table
  * (used by bench.py to time repeated full solves with inputs already resident in HBM). */
 BMPOW_API int bmpow_batch_reset(bmpow_batch *b, const uint64_t *start);
+
+/* Park (pending = 0) or schedule (pending = 1) objects [first, first + count) of a session:
+ * parked objects stay resident but bmpow_batch_step skips them; finished objects are not
+ * affected.  Lets a caller feed a resident table in pieces (bench.py hands out pieces of one
+ * global batch to the ranks on demand).  Returns the pending count or < 0. */
+BMPOW_API int bmpow_batch_set_pending(bmpow_batch *b, size_t first, size_t count, int pending);
 
 BMPOW_API void bmpow_batch_destroy(bmpow_batch *b);
 

@@ -23,6 +23,7 @@ E_STATE = -5
 PENDING = 0
 DONE_FOUND = 1
 DONE_EXHAUSTED = 2
+PARKED = 3
 
 U64_MAX = (1 << 64) - 1
 
@@ -76,6 +77,7 @@ SIGNATURES = [
     ('bmpow_batch_step', ctypes.c_int, [_vp, _u64]),
     ('bmpow_batch_results', ctypes.c_int, [_vp, _p64, _p64, _pu8, _p64]),
     ('bmpow_batch_reset', ctypes.c_int, [_vp, _p64]),
+    ('bmpow_batch_set_pending', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]),
     ('bmpow_batch_destroy', None, [_vp]),
     ('bmpow_get_stats', ctypes.c_int, [ctypes.POINTER(BmpowStats)]),
     ('bmpow_reset_stats', None, []),

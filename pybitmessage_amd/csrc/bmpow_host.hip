@@ -986,6 +986,23 @@ int bmpow_batch_reset(bmpow_batch* b, const uint64_t* start) {
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
+int bmpow_batch_set_pending(bmpow_batch* b, size_t first, size_t count, int pending) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!b) return set_err(BMPOW_E_STATE, "null batch");
+  if (first > b->n || count > b->n - first) return set_err(BMPOW_E_ARG, "range outside the batch");
+  for (size_t i = first; i < first + count; ++i) {
+    if (pending && b->done[i] == BMPOW_PARKED) {
+      b->done[i] = BMPOW_PENDING;
+      b->pending++;
+    } else if (!pending && b->done[i] == BMPOW_PENDING) {
+      b->done[i] = BMPOW_PARKED;
+      b->pending--;
+    }
+  }
+  if (pending && first < b->first_pending) b->first_pending = first;
+  return (int)std::min<size_t>(b->pending, 0x7fffffff);
+}
+
 void bmpow_batch_destroy(bmpow_batch* b) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!b) return;

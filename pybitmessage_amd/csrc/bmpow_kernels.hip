@@ -37,18 +37,7 @@ __device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce) {
 // ---------------------------------------------------------------------------------------
 // Search kernel.
 // ---------------------------------------------------------------------------------------
-#ifndef BM_MIN_WAVES
-#define BM_MIN_WAVES 1
-#endif
-#ifndef BM_MAX_WAVES
-#define BM_MAX_WAVES 8
-#endif
-#if BM_MIN_WAVES > 0
-#define BM_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(BM_MIN_WAVES, BM_MAX_WAVES)))
-#else
-#define BM_WAVES_ATTR
-#endif
-__global__ __launch_bounds__(BM_BLOCK) BM_WAVES_ATTR void bm_search_kernel(const bm_obj* __restrict__ objs,
+__global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __restrict__ objs,
                                                              const bm_item* __restrict__ items,
                                                              uint32_t nitems,
                                                              unsigned long long* __restrict__ best,

@@ -37,6 +37,49 @@ def _worker(rank, world, port, outdir):
     d.close()
 
 
+def _claim_worker(rank, world, port, outdir):
+    os.environ.update({'RANK': str(rank), 'LOCAL_RANK': str(rank), 'WORLD_SIZE': str(world),
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
+    import time
+    d = bench.Dist()
+    c = bench.Claimer(d, 1000, 7)
+    got = []
+    for tag in ('a', 'b'):
+        c.start(tag)
+        mine = []
+        while True:
+            r = c.claim()
+            if r is None:
+                break
+            mine.append(r)
+            time.sleep(0.001 * (rank + 1))  # ranks of different speed
+        got.append(mine)
+    d.barrier()
+    with open(os.path.join(outdir, 'claims%d.json' % rank), 'w') as f:
+        json.dump(got, f)
+    d.close()
+
+
+def test_claims_partition_the_global_batch(tmp_path):
+    """Work claiming over the TCP store: every object of the global batch is claimed by
+    exactly one rank, per step (tag), and the faster rank claims more."""
+    port = _free_port()
+    mp.spawn(_claim_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    c0 = json.load(open(tmp_path / 'claims0.json'))
+    c1 = json.load(open(tmp_path / 'claims1.json'))
+    for step in range(2):
+        idx = sorted(i for lo, hi in c0[step] + c1[step] for i in range(lo, hi))
+        assert idx == list(range(1000))
+    assert sum(hi - lo for lo, hi in c0[0]) > sum(hi - lo for lo, hi in c1[0])
+
+
+def test_single_rank_claims_everything():
+    import types
+    c = bench.Claimer(types.SimpleNamespace(world=1), 50, 50)
+    c.start('x')
+    assert c.claim() == (0, 50) and c.claim() is None
+
+
 def test_two_rank_aggregation(tmp_path):
     port = _free_port()
     mp.spawn(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
