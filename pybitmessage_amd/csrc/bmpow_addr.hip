@@ -157,11 +157,12 @@ BM_DEV void ripe_of_points(uint32_t (&rh)[5], const ge& ps, const ge& pe) {
 
 }  // namespace
 
-// table[i*256 + v] = v * 2^(8i) * G (affine), v = 1..255.  One thread per entry.
+// table[i << W | v] = v * 2^(W i) * G (affine), v = 1 .. 2^W - 1 (W = ec::kWBits).  One thread
+// per entry; entries v = 0 are never read as points (the comb skips zero windows).
 __global__ __launch_bounds__(64) void ar_table_kernel(ge* __restrict__ table) {
-  const uint32_t t = blockIdx.x * 64 + threadIdx.x;
-  if (t >= 32 * 256) return;
-  const uint32_t i = t >> 8, v = t & 255;
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (t >= ec::kTableEntries) return;
+  const uint32_t i = (uint32_t)(t >> ec::kWBits), v = (uint32_t)t & ec::kWMask;
   if (v == 0) return;
   gej b;
   b.inf = false;
@@ -175,12 +176,12 @@ __global__ __launch_bounds__(64) void ar_table_kernel(ge* __restrict__ table) {
     b.y.d[j] = gy[j];
   }
   ec::fe_set(b.z, 1);
-  for (uint32_t d = 0; d < 8 * i; ++d) ec::gej_double(b, b);  // 2^(8i) * G
+  for (uint32_t d = 0; d < (uint32_t)ec::kWBits * i; ++d) ec::gej_double(b, b);  // 2^(W i) * G
   ge ba;
   ec::gej_to_ge(ba, b);
   gej acc;
   acc.inf = true;
-  for (int bit = 7; bit >= 0; --bit) {  // v * B, MSB first
+  for (int bit = ec::kWBits - 1; bit >= 0; --bit) {  // v * B, MSB first
     ec::gej_double(acc, acc);
     if ((v >> bit) & 1) ec::gej_add_ge(acc, acc, ba);
   }
@@ -251,7 +252,7 @@ __global__ void ar_midstate_kernel(const uint8_t* __restrict__ pass, uint64_t nf
 // Launch wrappers (C++ linkage, used by bmpow_host.hip).
 // ---------------------------------------------------------------------------------------
 hipError_t ar_launch_table(hipStream_t st, ge* table) {
-  hipLaunchKernelGGL(ar_table_kernel, dim3(32 * 256 / 64), dim3(64), 0, st, table);
+  hipLaunchKernelGGL(ar_table_kernel, dim3((uint32_t)(ec::kTableEntries / 64)), dim3(64), 0, st, table);
   return hipGetLastError();
 }
 

@@ -603,8 +603,8 @@ constexpr uint64_t kAddrMaxStep = 1ULL << 20;  // tries per shard per launch (~t
 int ensure_table(Shard& sh) {
   if (sh.d_table) return 0;
   HIPTRY(hipSetDevice(sh.dev));
-  HIPTRY(hipMalloc(&sh.d_table, 32 * 256 * sizeof(ec::ge)));
-  HIPTRY(hipMemsetAsync(sh.d_table, 0, 32 * 256 * sizeof(ec::ge), sh.stream));
+  HIPTRY(hipMalloc(&sh.d_table, ec::kTableEntries * sizeof(ec::ge)));
+  HIPTRY(hipMemsetAsync(sh.d_table, 0, ec::kTableEntries * sizeof(ec::ge), sh.stream));
   HIPTRY(ar_launch_table(sh.stream, sh.d_table));
   HIPTRY(hipStreamSynchronize(sh.stream));
   return 0;
@@ -863,13 +863,21 @@ int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t
   if (rc < 0) return rc;
   bmpow_batch* b = g_scratch;
   uint64_t left = max_trials;
-  const uint64_t step = g_step_trials * g_shards.size();
+  const uint64_t full = g_step_trials * g_shards.size();
+  // The first step is sized to the object's expected trial count, 2^64 / (target + 1): an easy
+  // object does not launch (and drain) a full grid.  Steps then double up to the default; they
+  // cover consecutive windows, so exactness is unaffected.
+  const long double expect = 18446744073709551616.0L / ((long double)target + 1.0L);
+  const uint64_t floor_step = std::min<uint64_t>(full, (uint64_t)(1u << 23) * g_shards.size());
+  uint64_t step = expect * 2 >= (long double)full ? full : std::max<uint64_t>(floor_step, (uint64_t)(expect * 2));
+  step = (step + BM_CHUNK - 1) / BM_CHUNK * BM_CHUNK;
   while (left > 0) {
     // This step's window for the single object is `want` nonces rounded up to whole chunks;
     // a hit in the round-up tail lies beyond the caller's budget and is reported as
     // NOT_FOUND (the caller resumes at start + max_trials and finds it again: exactness
     // only needs every nonce below a reported hit to have been hashed).
     const uint64_t want = std::min(left, step);
+    step = std::min(full, step * 2);
     const uint64_t chunks = (want + BM_CHUNK - 1) / BM_CHUNK;
     const uint64_t st = b->next[0];
     rc = batch_step_locked(b, chunks * BM_CHUNK, nullptr);

@@ -4,9 +4,9 @@
 // (src/highlevelcrypto.py:111-140, pointMult).  Here one lane computes k*G for its own k:
 //   * field elements mod p = 2^256 - 2^32 - 977 as 8 x 32-bit little-endian limbs, always fully
 //     reduced; products by v_mad_u64_u32 (operand scanning), reduction by 2^256 = 2^32 + 977;
-//   * k*G by a fixed-base comb: 32 byte windows, table[i][v] = v * 2^(8i) * G in affine
-//     coordinates (512 KB, built once per device by ar_table_kernel, L2 resident), so one
-//     scalar multiplication is 32 mixed Jacobian+affine additions and one inversion;
+//   * k*G by a fixed-base comb: 16 windows of 16 bits, table[i][v] = v * 2^(16i) * G in affine
+//     coordinates (64 MB, built once per device by ar_table_kernel), so one scalar
+//     multiplication is 16 mixed Jacobian+affine additions and one inversion;
 //   * inversion by Fermat (a^(p-2)) with the 255-squaring / 15-multiplication addition chain
 //     for the exponent's bit pattern [223 ones][0][22 ones][0000101101].
 #pragma once
@@ -284,19 +284,37 @@ BM_DEV void gej_to_ge(ge& r, const gej& p) {
   fe_mul(r.y, p.y, zi2);
 }
 
+// Comb window width: table[i << AR_WBITS | v] = v * 2^(AR_WBITS * i) * G, 256/AR_WBITS windows.
+// 16 bits: 16 mixed additions per k*G over a 64 MB table (HBM / Infinity-Cache resident);
+// 8 bits: 32 additions over 512 KB.
+#ifndef AR_WBITS
+#define AR_WBITS 16
+#endif
+constexpr int kWBits = AR_WBITS;
+constexpr int kWindows = 256 / kWBits;
+constexpr uint32_t kWMask = (1u << kWBits) - 1;
+constexpr size_t kTableEntries = (size_t)kWindows << kWBits;
+static_assert(64 % kWBits == 0, "windows must not straddle 64-bit words");
+
+BM_DEV uint32_t window(const uint64_t (&kw)[4], int i) {  // window i, least significant first
+  return (uint32_t)(kw[3 - ((i * kWBits) >> 6)] >> ((i * kWBits) & 63)) & kWMask;
+}
+
 // k*G for the 256-bit scalar given as 4 big-endian 64-bit words (k = w0*2^192 + ... + w3),
 // i.e. the first 32 bytes of a SHA-512 digest read as a big-endian integer (BN_bin2bn).
-// Returns false for k = 0 (the point at infinity).
+// The next window's table entry is loaded before the current addition, so the gather's
+// latency hides behind ~3,000 VALU instructions.  Returns false for k*G = infinity (k = 0).
 BM_DEV bool scalar_mult_base(ge& r, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
   gej acc;
   acc.inf = true;
+  ge q = table[window(kw, 0)];
 #pragma unroll 1
-  for (int i = 0; i < 32; ++i) {
-    const uint32_t v = (uint32_t)(kw[3 - (i >> 3)] >> (8 * (i & 7))) & 0xff;  // byte i, LSB first
-    if (v) {
-      const ge q = table[i * 256 + v];
-      gej_add_ge(acc, acc, q);
-    }
+  for (int i = 0; i < kWindows; ++i) {
+    const uint32_t v = window(kw, i);
+    ge qn;
+    if (i + 1 < kWindows) qn = table[((size_t)(i + 1) << kWBits) | window(kw, i + 1)];
+    if (v) gej_add_ge(acc, acc, q);
+    q = qn;
   }
   if (acc.inf) return false;
   gej_to_ge(r, acc);
