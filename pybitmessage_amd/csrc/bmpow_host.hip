@@ -25,6 +25,7 @@
 #include <ctime>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/bmpow.h"
@@ -510,17 +511,26 @@ int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs) {
     HIPTRY(hipSetDevice(sh.dev));
     const size_t m = pt.orig.size();
     std::vector<bv_obj> ho(m);
-    std::vector<uint8_t> pool(pt.blocks * 128);
     uint64_t blk = 0;
     for (size_t j = 0; j < m; ++j) {
-      const Span& sp = objs[pt.orig[j]];
       const uint32_t nb = nblk[pt.orig[j]];
-      pad_into(sp.p + 8, sp.len - 8, pool.data() + blk * 128, nb);
       ho[j].blk = (uint32_t)blk;
       ho[j].nblk = nb;
-      ho[j].nonce = load_be64(sp.p);
+      ho[j].nonce = load_be64(objs[pt.orig[j]].p);
       blk += nb;
     }
+    // padding is a memory-bound copy of every payload: spread it over host threads
+    std::vector<uint8_t> pool(pt.blocks * 128);
+    const size_t nth = std::max<size_t>(1, std::min<size_t>({16, std::thread::hardware_concurrency(), m / 4096 + 1}));
+    std::vector<std::thread> th;
+    for (size_t t = 0; t < nth; ++t)
+      th.emplace_back([&, t] {
+        for (size_t j = m * t / nth; j < m * (t + 1) / nth; ++j) {
+          const Span& sp = objs[pt.orig[j]];
+          pad_into(sp.p + 8, sp.len - 8, pool.data() + (uint64_t)ho[j].blk * 128, ho[j].nblk);
+        }
+      });
+    for (auto& x : th) x.join();
     HIPTRY(hipMalloc(&pt.d_obj, m * sizeof(bv_obj)));
     HIPTRY(hipMalloc(&pt.d_pool, std::max<size_t>(pool.size(), 16)));
     HIPTRY(hipMalloc(&pt.d_pow, m * sizeof(uint64_t)));

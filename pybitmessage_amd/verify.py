@@ -20,9 +20,11 @@ P64 = ctypes.POINTER(ctypes.c_uint64)
 
 
 def _pack(objects):
-    objs = [bytes(o) for o in objects]
+    """One concatenated buffer + byte offsets (the ABI's layout); bytes objects are not copied
+    before the join."""
+    objs = [o if type(o) is bytes else bytes(o) for o in objects]
     offsets = np.zeros(len(objs) + 1, dtype=np.uint64)
-    np.cumsum([len(o) for o in objs], out=offsets[1:])
+    np.cumsum(np.fromiter(map(len, objs), dtype=np.uint64, count=len(objs)), out=offsets[1:])
     return b''.join(objs), offsets, objs
 
 

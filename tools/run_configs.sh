@@ -18,10 +18,14 @@ run c3 200 --config c3 --c3-log2 38 --steps 1 --warmup 0 --no-cpu-baseline
 run c4 200 --config c4 --steps 1 --warmup 0 --no-cpu-baseline
 run c5 200 --config c5 --objects 4096 --steps 1 --warmup 0 --no-cpu-baseline
 run verify 200 --config verify --steps 10 --warmup 2
+run addrgen 200 --config addrgen --null-bytes 3 --steps 2 --warmup 1 --cpu-seconds 5
 echo "[$(date +%T)] rocprof c2" >&2
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof_c2" -o run -- \
   python3 bench.py --config c2 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/${TAG}_prof_c2.json" 2> "$OUT/${TAG}_prof_c2.err"
 echo "[$(date +%T)] rocprof verify" >&2
 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof_verify" -o run -- \
   python3 bench.py --config verify --steps 10 --warmup 1 --no-cpu-baseline > "$OUT/${TAG}_prof_verify.json" 2> "$OUT/${TAG}_prof_verify.err"
+echo "[$(date +%T)] rocprof addrgen" >&2
+timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/${TAG}_prof_addrgen" -o run -- \
+  python3 bench.py --config addrgen --null-bytes 3 --steps 1 --warmup 1 --no-cpu-baseline > "$OUT/${TAG}_prof_addrgen.json" 2> "$OUT/${TAG}_prof_addrgen.err"
 echo "[$(date +%T)] done" >&2
