@@ -158,6 +158,12 @@ BMPOW_API int bmpow_verify_batch(size_t n, const uint8_t *objs, const uint64_t *
 BMPOW_API int bmpow_pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, int64_t recv_time,
                                    uint64_t expires);
 
+/* The same check with the objects where they lie: objs[i] points at object i (lens[i] bytes),
+ * so a caller holding separate buffers (one per received object) needs no concatenation. */
+BMPOW_API int bmpow_verify_batch_ptrs(size_t n, const uint8_t *const *objs, const uint64_t *lens,
+                                      const uint64_t *ntpb, const uint64_t *extra, const int64_t *recv_time,
+                                      uint8_t *ok_out);
+
 /* Device-resident verification session: pad, sort and upload the objects once, then hash
  * them repeatedly (bench.py times bmpow_vbatch_run with the payloads resident in HBM). */
 typedef struct bmpow_vbatch bmpow_vbatch;

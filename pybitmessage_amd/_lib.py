@@ -86,6 +86,8 @@ SIGNATURES = [
     ('bmpow_pow_values', ctypes.c_int, [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64]),
     ('bmpow_verify_batch', ctypes.c_int,
      [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _p64, ctypes.POINTER(ctypes.c_int64), _pu8]),
+    ('bmpow_verify_batch_ptrs', ctypes.c_int,
+     [ctypes.c_size_t, ctypes.c_void_p, _p64, _p64, _p64, ctypes.POINTER(ctypes.c_int64), _pu8]),
     ('bmpow_pow_sufficient', ctypes.c_int, [_u64, _u64, _u64, _u64, ctypes.c_int64, _u64]),
     ('bmpow_vbatch_create', _vp, [ctypes.c_size_t, ctypes.c_char_p, _p64]),
     ('bmpow_vbatch_run', ctypes.c_int, [_vp, _p64]),

@@ -1073,31 +1073,28 @@ int bmpow_pow_values(size_t n, const uint8_t* objs, const uint64_t* offsets, uin
   return rc;
 }
 
-int bmpow_verify_batch(size_t n, const uint8_t* objs, const uint64_t* offsets, const uint64_t* ntpb,
-                       const uint64_t* extra, const int64_t* recv_time, uint8_t* ok_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  int rc = init_locked();
-  if (rc < 0) return rc;
-  if (n == 0) return 0;
-  if (!objs || !offsets || !ok_out) return set_err(BMPOW_E_ARG, "null pointer");
+// shared by both verify entry points (internal linkage despite the extern "C" block)
+static int verify_spans_locked(size_t n, const uint8_t* const* ptrs, const uint64_t* lens, const uint64_t* ntpb,
+                               const uint64_t* extra, const int64_t* recv_time, uint8_t* ok_out) {
   std::vector<Span> spans;
   std::vector<size_t> idx;
+  spans.reserve(n);
+  idx.reserve(n);
   for (size_t i = 0; i < n; ++i) {
-    if (offsets[i + 1] < offsets[i]) return set_err(BMPOW_E_ARG, "offsets are not ascending");
-    const uint64_t len = offsets[i + 1] - offsets[i];
     if ((ntpb && ntpb[i] >= (1ULL << 62)) || (extra && extra[i] >= (1ULL << 62)))
       return set_err(BMPOW_E_ARG, "nonceTrialsPerByte / payloadLengthExtraBytes above 2^62");
-    if (len < 16) {
+    if (lens[i] < 16) {
       ok_out[i] = 2;  // the reference's unpack('>Q', data[8:16]) raises struct.error
       continue;
     }
-    spans.push_back({objs + offsets[i], len});
+    if (!ptrs[i]) return set_err(BMPOW_E_ARG, "null object pointer");
+    spans.push_back({ptrs[i], lens[i]});
     idx.push_back(i);
   }
   std::vector<uint64_t> pow(spans.size());
   if (!spans.empty()) {
     bmpow_vbatch vb;
-    rc = vbatch_build(&vb, spans);
+    int rc = vbatch_build(&vb, spans);
     if (rc == 0) rc = vbatch_run_locked(&vb, pow.data());
     vbatch_free(&vb);
     if (rc < 0) return rc;
@@ -1110,6 +1107,33 @@ int bmpow_verify_batch(size_t n, const uint8_t* objs, const uint64_t* offsets, c
                                         load_be64(spans[j].p + 8));
   }
   return 0;
+}
+
+int bmpow_verify_batch(size_t n, const uint8_t* objs, const uint64_t* offsets, const uint64_t* ntpb,
+                       const uint64_t* extra, const int64_t* recv_time, uint8_t* ok_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (n == 0) return 0;
+  if (!objs || !offsets || !ok_out) return set_err(BMPOW_E_ARG, "null pointer");
+  std::vector<const uint8_t*> ptrs(n);
+  std::vector<uint64_t> lens(n);
+  for (size_t i = 0; i < n; ++i) {
+    if (offsets[i + 1] < offsets[i]) return set_err(BMPOW_E_ARG, "offsets are not ascending");
+    ptrs[i] = objs + offsets[i];
+    lens[i] = offsets[i + 1] - offsets[i];
+  }
+  return verify_spans_locked(n, ptrs.data(), lens.data(), ntpb, extra, recv_time, ok_out);
+}
+
+int bmpow_verify_batch_ptrs(size_t n, const uint8_t* const* objs, const uint64_t* lens, const uint64_t* ntpb,
+                            const uint64_t* extra, const int64_t* recv_time, uint8_t* ok_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (n == 0) return 0;
+  if (!objs || !lens || !ok_out) return set_err(BMPOW_E_ARG, "null pointer");
+  return verify_spans_locked(n, objs, lens, ntpb, extra, recv_time, ok_out);
 }
 
 int bmpow_pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, int64_t recv_time,

@@ -51,26 +51,55 @@ def pow_values(objects):
     return [int(v) for v in out]
 
 
+def _bytes_data_offset():
+    """Offset of a CPython bytes object's data from its id() (the object's address): the header
+    size, ``bytes.__basicsize__ - 1``.  Checked on a probe; None when the layout differs (then
+    the pointers come from a ctypes array instead)."""
+    off = bytes.__basicsize__ - 1
+    probe = b'bmpow-probe-0123456789'
+    try:
+        if ctypes.string_at(id(probe) + off, len(probe)) == probe:
+            return off
+    except Exception:  # noqa: BLE001
+        pass
+    return None
+
+
+_DATA_OFFSET = _bytes_data_offset()
+
+
+def _pointers(objs):
+    """Addresses of each object's bytes, without copying them (objs must stay alive)."""
+    if _DATA_OFFSET is not None:
+        return np.fromiter(map(id, objs), dtype=np.uint64, count=len(objs)) + np.uint64(_DATA_OFFSET)
+    arr = (ctypes.c_char_p * len(objs))(*objs)
+    return np.frombuffer(arr, dtype=np.uint64).copy()
+
+
 def isProofOfWorkSufficient_batch(objects, nonceTrialsPerByte=0, payloadLengthExtraBytes=0, recvTime=0):
     """``[protocol.isProofOfWorkSufficient(o, nonceTrialsPerByte, payloadLengthExtraBytes,
     recvTime) for o in objects]`` with one GPU launch.  Each difficulty argument and
     ``recvTime`` may be a scalar or one value per object (``recvTime`` 0 = now, as in the
     reference).  An object shorter than 16 bytes raises ``struct.error`` as the reference's
-    ``unpack('>Q', data[8:16])`` does."""
-    data, offsets, objs = _pack(objects)
+    ``unpack('>Q', data[8:16])`` does.  The objects are read where they lie
+    (``bmpow_verify_batch_ptrs``): no concatenation on the host."""
+    objs = [o if type(o) is bytes else bytes(o) for o in objects]
     n = len(objs)
     if n == 0:
         return []
+    ptrs = _pointers(objs)
+    lens = np.fromiter(map(len, objs), dtype=np.uint64, count=n)
     ntpb = _per_object(nonceTrialsPerByte, n, np.uint64)
     extra = _per_object(payloadLengthExtraBytes, n, np.uint64)
     recv = _per_object([int(r) for r in recvTime] if np.ndim(recvTime) else int(recvTime), n, np.int64)
     lib = _lib.get()
     ok = np.zeros(n, dtype=np.uint8)
-    _lib.check(lib, lib.bmpow_verify_batch(n, data, offsets.ctypes.data_as(P64), ntpb.ctypes.data_as(P64),
-                                           extra.ctypes.data_as(P64),
-                                           recv.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
-                                           ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
-               'bmpow_verify_batch')
+    _lib.check(lib, lib.bmpow_verify_batch_ptrs(n, ptrs.ctypes.data, lens.ctypes.data_as(P64),
+                                                ntpb.ctypes.data_as(P64), extra.ctypes.data_as(P64),
+                                                recv.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                                ok.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
+               'bmpow_verify_batch_ptrs')
+    del objs  # the pointers were valid for the call
     if (ok == 2).any():
         raise struct.error('unpack requires a buffer of 8 bytes')
     return [bool(v) for v in ok]

@@ -147,3 +147,26 @@ def test_gpu_verify_edge_cases(gpulib):
     obj = bytes(8) + pack('>Q', 1) + bytes(30)
     assert verify.isProofOfWorkSufficient_batch([obj], recvTime=0) == \
         [targets.isProofOfWorkSufficient(obj, 0, 0, 0)]
+
+
+@gpu
+def test_gpu_offsets_and_pointer_entry_points_agree(gpulib, kats):
+    """bmpow_verify_batch (one concatenated buffer + offsets) and bmpow_verify_batch_ptrs (the
+    objects where they lie) give the same verdicts, including the malformed-object code."""
+    from pybitmessage_amd import verify
+    objs = [regen(k, True) for k in kats['verdict_kats']] + [bytes(12), bytes(16)]
+    n = len(objs)
+    data, offsets, _ = verify._pack(objs)
+    ok1 = np.zeros(n, dtype=np.uint8)
+    recv = np.full(n, kats['recv'], dtype=np.int64)
+    _lib.check(gpulib, gpulib.bmpow_verify_batch(n, data, offsets.ctypes.data_as(verify.P64), None, None,
+                                                 recv.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                                 ok1.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), 'offsets')
+    ptrs = verify._pointers(objs)
+    lens = np.fromiter(map(len, objs), dtype=np.uint64, count=n)
+    ok2 = np.zeros(n, dtype=np.uint8)
+    _lib.check(gpulib, gpulib.bmpow_verify_batch_ptrs(n, ptrs.ctypes.data, lens.ctypes.data_as(verify.P64), None,
+                                                      None, recv.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                                                      ok2.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), 'ptrs')
+    assert ok1.tolist() == ok2.tolist()
+    assert ok1.tolist() == [1] * (n - 2) + [2, 0]
