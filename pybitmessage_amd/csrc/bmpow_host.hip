@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -520,23 +521,23 @@ int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs) {
       blk += nb;
     }
     // padding is a memory-bound copy of every payload: spread it over host threads
-    std::vector<uint8_t> pool(pt.blocks * 128);
+    std::unique_ptr<uint8_t[]> pool(new uint8_t[pt.blocks * 128]);  // pad_into writes every byte
     const size_t nth = std::max<size_t>(1, std::min<size_t>({16, std::thread::hardware_concurrency(), m / 4096 + 1}));
     std::vector<std::thread> th;
     for (size_t t = 0; t < nth; ++t)
       th.emplace_back([&, t] {
         for (size_t j = m * t / nth; j < m * (t + 1) / nth; ++j) {
           const Span& sp = objs[pt.orig[j]];
-          pad_into(sp.p + 8, sp.len - 8, pool.data() + (uint64_t)ho[j].blk * 128, ho[j].nblk);
+          pad_into(sp.p + 8, sp.len - 8, pool.get() + (uint64_t)ho[j].blk * 128, ho[j].nblk);
         }
       });
     for (auto& x : th) x.join();
     HIPTRY(hipMalloc(&pt.d_obj, m * sizeof(bv_obj)));
-    HIPTRY(hipMalloc(&pt.d_pool, std::max<size_t>(pool.size(), 16)));
+    HIPTRY(hipMalloc(&pt.d_pool, std::max<size_t>(pt.blocks * 128, 16)));
     HIPTRY(hipMalloc(&pt.d_pow, m * sizeof(uint64_t)));
     HIPTRY(hipHostMalloc(&pt.h_pow, m * sizeof(uint64_t), hipHostMallocDefault));
     HIPTRY(hipMemcpy(pt.d_obj, ho.data(), m * sizeof(bv_obj), hipMemcpyHostToDevice));
-    HIPTRY(hipMemcpy(pt.d_pool, pool.data(), pool.size(), hipMemcpyHostToDevice));
+    HIPTRY(hipMemcpy(pt.d_pool, pool.get(), pt.blocks * 128, hipMemcpyHostToDevice));
   }
   return 0;
 }
