@@ -222,3 +222,46 @@ def test_stats_count_trials(gpulib):
     st = _lib.BmpowStats()
     gpulib.bmpow_get_stats(ctypes.byref(st))
     assert st.launches >= 1 and st.trials >= 129430 and st.kernel_ms > 0
+
+
+def test_concurrent_callers_are_serialised_and_exact(gpulib, coracle):
+    """The reference calls run() from the worker thread and the API thread at once
+    (class_singleWorker.py:236, api.py:1304); every entry point is thread safe and exact."""
+    from concurrent.futures import ThreadPoolExecutor
+    rng = random.Random(77)
+    jobs = [(U64 // rng.choice([50, 3000, 70000]), rng.randbytes(64)) for _ in range(24)]
+    with ThreadPoolExecutor(6) as ex:
+        got = list(ex.map(lambda j: proofofwork.run(*j), jobs))
+        batches = list(ex.map(proofofwork.run_batch, [jobs[i::3] for i in range(3)]))
+    assert got == [list(coracle.search(ih, t)) for t, ih in jobs]
+    for i in range(3):
+        assert batches[i] == got[i::3]
+
+
+def test_batch_park_and_schedule(gpulib, coracle):
+    """bmpow_batch_set_pending: parked objects are skipped, scheduled ones solve exactly, in
+    any order of scheduling (bench.py's cross-rank claiming)."""
+    rng = random.Random(5)
+    n = 12
+    objs = [(U64 // rng.choice([100, 5000]), rng.randbytes(64)) for _ in range(n)]
+    tg = np.array([t for t, _ in objs], dtype=np.uint64)
+    h = gpulib.bmpow_batch_create(n, b''.join(ih for _, ih in objs), tg.ctypes.data_as(P64), None)
+    assert h
+    try:
+        assert gpulib.bmpow_batch_set_pending(h, 0, n, 0) == 0
+        assert gpulib.bmpow_batch_step(h, 0) == 0  # nothing scheduled: nothing to do
+        done = np.zeros(n, dtype=np.uint8)
+        nonce = np.zeros(n, dtype=np.uint64)
+        trial = np.zeros(n, dtype=np.uint64)
+        for lo, hi in [(8, 12), (0, 3), (3, 8)]:  # out of order
+            gpulib.bmpow_batch_set_pending(h, lo, hi - lo, 1)
+            while gpulib.bmpow_batch_step(h, 0) > 0:
+                pass
+            gpulib.bmpow_batch_results(h, nonce.ctypes.data_as(P64), trial.ctypes.data_as(P64),
+                                       done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), None)
+            assert (done[lo:hi] == _lib.DONE_FOUND).all()
+        for i, (t, ih) in enumerate(objs):
+            assert (int(trial[i]), int(nonce[i])) == coracle.search(ih, t)
+        assert gpulib.bmpow_batch_set_pending(h, n, 1, 1) < 0  # range outside the batch
+    finally:
+        gpulib.bmpow_batch_destroy(h)
