@@ -264,7 +264,11 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
   const size_t S = g_shards.size();
   if (budget == 0) budget = g_step_trials * S;
   budget = std::min<uint64_t>(budget, (uint64_t)S << 36);  // grid.x stays far below 2^31
-  uint64_t total_chunks = std::max<uint64_t>(budget / BM_CHUNK, S);
+  // workgroup size in nonces: short rounds for small steps (below ~6 full rounds of the chip
+  // per shard), full chunks otherwise
+  const uint32_t iters = budget < ((uint64_t)1 << 26) * S ? BM_ITERS_SMALL : BM_ITERS;
+  const uint64_t chunk = (uint64_t)BM_BLOCK * iters;
+  uint64_t total_chunks = std::max<uint64_t>(budget / chunk, S);
 
   // 1. windows: pending objects in index order, k chunks each
   struct Win { uint32_t obj; uint64_t start, count, chunks, chunk0; };
@@ -274,10 +278,10 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
   for (size_t i = b->first_pending; i < b->n && chunk_acc < total_chunks; ++i) {
     if (b->done[i] != BMPOW_PENDING) continue;
     const uint64_t st = b->next[i];
-    uint64_t want = k * BM_CHUNK;
+    uint64_t want = k * chunk;
     const uint64_t room = kU64Max - st;  // nonces remaining after st
     if (room < want - 1) want = room + 1;   // st + want - 1 <= 2^64-1
-    const uint64_t ch = (want + BM_CHUNK - 1) / BM_CHUNK;
+    const uint64_t ch = (want + chunk - 1) / chunk;
     wins.push_back({(uint32_t)i, st, want, ch, chunk_acc});
     chunk_acc += ch;
   }
@@ -305,9 +309,9 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
         int rc = ensure_items(sh, sh.nitems + 1);
         if (rc < 0) return rc;
         bm_item& it = sh.h_items[sh.nitems];
-        const uint64_t off = (c - w.chunk0) * BM_CHUNK;
+        const uint64_t off = (c - w.chunk0) * chunk;
         it.start = w.start + off;
-        it.count = std::min<uint64_t>(w.count - off, (seg_end - c) * BM_CHUNK);
+        it.count = std::min<uint64_t>(w.count - off, (seg_end - c) * chunk);
         it.obj = w.obj;
         it.chunk_base = (uint32_t)(c - cut[s]);
         it.pad = 0;
@@ -326,8 +330,8 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     HIPTRY(hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream));
     HIPTRY(hipMemsetAsync(sh.d_trials, 0, sizeof(unsigned long long), sh.stream));
     HIPTRY(hipEventRecord(sh.ev0, sh.stream));
-    HIPTRY(bm_launch_search(sh.stream, sh.nchunks, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best,
-                            sh.d_trials));
+    HIPTRY(bm_launch_search(sh.stream, sh.nchunks, iters, b->dev[s].d_obj, sh.d_items, sh.nitems,
+                            b->dev[s].d_best, sh.d_trials));
     HIPTRY(hipEventRecord(sh.ev1, sh.stream));
     HIPTRY(bm_launch_resolve(sh.stream, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best, sh.d_res));
     HIPTRY(hipMemcpyAsync(sh.h_res, sh.d_res, sh.nitems * sizeof(bm_result), hipMemcpyDeviceToHost, sh.stream));

@@ -5,10 +5,14 @@
 
 #include "secp256k1_dev.h"
 
-// One workgroup = BM_BLOCK lanes x BM_ITERS nonces = one CHUNK of a work item.
+// One workgroup = BM_BLOCK lanes x iters nonces = one CHUNK of a work item.  Full steps use
+// BM_ITERS iterations per workgroup; small steps (a single easy object) use BM_ITERS_SMALL so a
+// "round" of resident workgroups is short and the answer is reached sooner.  BM_CHUNK (the full
+// chunk) is a multiple of every chunk size, so windows rounded to it fit either.
 #ifndef BM_ITERS
 #define BM_ITERS 32
 #endif
+#define BM_ITERS_SMALL 4
 #define BM_BLOCK 256
 #define BM_CHUNK ((uint64_t)BM_BLOCK * BM_ITERS)
 
@@ -45,8 +49,9 @@ struct bv_obj {
 
 hipError_t bv_launch_pow(hipStream_t st, const bv_obj* objs, uint32_t n, const uint4* pool, uint64_t* pow_out);
 
-hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, const bm_obj* objs, const bm_item* items,
-                            uint32_t nitems, unsigned long long* best, unsigned long long* trials_done);
+hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
+                            const bm_item* items, uint32_t nitems, unsigned long long* best,
+                            unsigned long long* trials_done);
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                              const unsigned long long* best, bm_result* res);
 hipError_t bm_launch_trials(hipStream_t st, const bm_obj* obj, const uint64_t* nonces, uint64_t n,

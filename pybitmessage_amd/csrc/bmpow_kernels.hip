@@ -41,8 +41,10 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __res
                                                              const bm_item* __restrict__ items,
                                                              uint32_t nitems,
                                                              unsigned long long* __restrict__ best,
-                                                             unsigned long long* __restrict__ trials_done) {
+                                                             unsigned long long* __restrict__ trials_done,
+                                                             uint32_t iters) {
   const uint32_t b = blockIdx.x;
+  const uint64_t chunk = (uint64_t)BM_BLOCK * iters;  // nonces per workgroup in this launch
   // largest item index with chunk_base <= b (items sorted by chunk_base, uniform search)
   uint32_t lo = 0, hi = nitems;
   while (hi - lo > 1) {
@@ -50,9 +52,9 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __res
     if (items[mid].chunk_base <= b) lo = mid; else hi = mid;
   }
   const bm_item it = items[lo];
-  const uint64_t off = (uint64_t)(b - it.chunk_base) * BM_CHUNK;
+  const uint64_t off = (uint64_t)(b - it.chunk_base) * chunk;
   if (off >= it.count) return;
-  const uint64_t cnt = (it.count - off < BM_CHUNK) ? (it.count - off) : BM_CHUNK;
+  const uint64_t cnt = (it.count - off < chunk) ? (it.count - off) : chunk;
   const uint64_t first = it.start + off;
   unsigned long long* bestp = best + it.obj;
   if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < first) return;
@@ -64,7 +66,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __res
   const uint64_t target = o->target;
 
   uint32_t done = 0;
-  for (uint32_t i = 0; i < BM_ITERS; ++i) {
+  for (uint32_t i = 0; i < iters; ++i) {
     const uint64_t base = (uint64_t)i * BM_BLOCK;
     if (base >= cnt) break;
     // Early exit, one iteration of granularity at no stall: the running minimum is read
@@ -109,10 +111,11 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_trials_kernel(const bm_obj* __res
 // ---------------------------------------------------------------------------------------
 // Launch wrappers (C++ linkage, used by bmpow_host.hip).
 // ---------------------------------------------------------------------------------------
-hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, const bm_obj* objs, const bm_item* items,
-                            uint32_t nitems, unsigned long long* best, unsigned long long* trials_done) {
+hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
+                            const bm_item* items, uint32_t nitems, unsigned long long* best,
+                            unsigned long long* trials_done) {
   hipLaunchKernelGGL(bm_search_kernel, dim3(nchunks), dim3(BM_BLOCK), 0, st, objs, items, nitems, best,
-                     trials_done);
+                     trials_done, iters);
   return hipGetLastError();
 }
 
