@@ -116,34 +116,43 @@ BM_DEV bool prefix_ok(const uint32_t (&rh)[5], uint32_t null_bytes) {
 
 // The keys of one try.  mode 0 (deterministic): signing from m = 2k, encryption from 2k+1.
 // mode 1 (random): fixed signing key prm->pub_s; encryption key from m = k of a random seed.
+// Both public keys leave the comb in Jacobian coordinates and share one inversion (mode 1 feeds
+// the given signing key in with Z = 1, so both modes run the same code).
 BM_DEV bool try_keys(const ar_params* __restrict__ prm, const ge* __restrict__ table, uint64_t k,
                      uint64_t (&hs)[8], uint64_t (&he)[8], ge& ps, ge& pe) {
   const uint32_t first = prm->mode == 0 ? 0 : 1;  // mode 1: the signing key is given
+  gej js, je;
   if (first) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) hs[i] = 0;
-    ps = prm->pub_s;
+    js.x = prm->pub_s.x;
+    js.y = prm->pub_s.y;
+    ec::fe_set(js.z, 1);
+    js.inf = false;
   }
   bool ok = true;
 #pragma unroll 1
-  for (uint32_t which = first; which < 2; ++which) {  // one hash + one scalar-mult body for both keys
+  for (uint32_t which = first; which < 2; ++which) {  // one hash + one comb body for both keys
     const uint64_t m = prm->mode == 0 ? 2 * k + which : k;
     uint64_t h[8];
     key_hash(h, prm, m);
     const uint64_t kw[4] = {h[0], h[1], h[2], h[3]};
-    ge r;
-    ok = ok && ec::scalar_mult_base(r, table, kw);
+    gej r;
+    ec::scalar_mult_base_jac(r, table, kw);
+    ok = ok && !r.inf;
     if (which == 0) {
-      ps = r;
+      js = r;
 #pragma unroll
       for (int i = 0; i < 8; ++i) hs[i] = h[i];
     } else {
-      pe = r;
+      je = r;
 #pragma unroll
       for (int i = 0; i < 8; ++i) he[i] = h[i];
     }
   }
-  return ok;
+  if (!ok) return false;
+  ec::gej_pair_to_ge(ps, pe, js, je);
+  return true;
 }
 
 BM_DEV void ripe_of_points(uint32_t (&rh)[5], const ge& ps, const ge& pe) {
@@ -189,22 +198,30 @@ __global__ __launch_bounds__(64) void ar_table_kernel(ge* __restrict__ table) {
 }
 
 // Search: lane g tries k = start + g (g < count).  best: running minimum k with a hit.
-// With out != nullptr the launch instead reports everything about the single try k = start
-// (keys, public keys, ripe) -- the resolve step, sharing this kernel's code.
-__global__ __launch_bounds__(64) void ar_search_kernel(const ar_params* __restrict__ prm, const ge* __restrict__ table,
+// kResolve: the launch instead reports everything about the single try k = start (keys, public
+// keys, ripe) -- the resolve step, sharing this kernel's code; a separate instantiation so the
+// search never keeps the private-key digests live.
+// 3 waves/SIMD (168 VGPRs, a few dwords spilled) beat 2 waves at 173 VGPRs: 206 vs 193 M tries/s
+// end to end at 3 null bytes (r01p).
+#ifndef AR_WAVES
+#define AR_WAVES 3
+#endif
+#define AR_OCC __attribute__((amdgpu_waves_per_eu(AR_WAVES)))
+template <bool kResolve>
+__global__ __launch_bounds__(64) AR_OCC void ar_search_kernel(const ar_params* __restrict__ prm, const ge* __restrict__ table,
                                                        uint64_t start, uint32_t count,
                                                        unsigned long long* __restrict__ best,
                                                        ar_result* __restrict__ out) {
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
   if (g >= count) return;
   const uint64_t k = start + g;
-  if (!out && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) return;
+  if (!kResolve && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) return;
   uint64_t hs[8], he[8];
   ge ps, pe;
   const bool ok = try_keys(prm, table, k, hs, he, ps, pe);
   uint32_t rh[5] = {0, 0, 0, 0, 0};
   if (ok) ripe_of_points(rh, ps, pe);
-  if (out) {
+  if (kResolve) {
     out->k = k;
     out->ok = ok ? 1u : 0u;
     for (int i = 0; i < 4; ++i) {
@@ -259,13 +276,13 @@ hipError_t ar_launch_table(hipStream_t st, ge* table) {
 hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, const ge* table, uint64_t start, uint32_t count,
                             unsigned long long* best) {
   if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(ar_search_kernel, dim3((count + 63) / 64), dim3(64), 0, st, prm, table, start, count, best,
+  hipLaunchKernelGGL(ar_search_kernel<false>, dim3((count + 63) / 64), dim3(64), 0, st, prm, table, start, count, best,
                      (ar_result*)nullptr);
   return hipGetLastError();
 }
 
 hipError_t ar_launch_resolve(hipStream_t st, const ar_params* prm, const ge* table, uint64_t k, ar_result* out) {
-  hipLaunchKernelGGL(ar_search_kernel, dim3(1), dim3(64), 0, st, prm, table, k, 1u, (unsigned long long*)nullptr,
+  hipLaunchKernelGGL(ar_search_kernel<true>, dim3(1), dim3(64), 0, st, prm, table, k, 1u, (unsigned long long*)nullptr,
                      out);
   return hipGetLastError();
 }

@@ -6,7 +6,8 @@
 //     reduced; products by v_mad_u64_u32 (operand scanning), reduction by 2^256 = 2^32 + 977;
 //   * k*G by a fixed-base comb: 16 windows of 16 bits, table[i][v] = v * 2^(16i) * G in affine
 //     coordinates (64 MB, built once per device by ar_table_kernel), so one scalar
-//     multiplication is 16 mixed Jacobian+affine additions and one inversion;
+//     multiplication is 16 mixed Jacobian+affine additions and one inversion (shared by the two
+//     keys of an address try, gej_pair_to_ge);
 //   * inversion by Fermat (a^(p-2)) with the 255-squaring / 15-multiplication addition chain
 //     for the exponent's bit pattern [223 ones][0][22 ones][0000101101].
 #pragma once
@@ -107,21 +108,8 @@ BM_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
 // r = 2a, 3a, 8a as additions (cheap, exact)
 BM_DEV void fe_dbl(fe& r, const fe& a) { fe_add(r, a, a); }
 
-BM_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
-  uint32_t p[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) p[i] = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      c += (uint64_t)a.d[i] * b.d[j] + p[i + j];  // <= (2^32-1)^2 + 2(2^32-1) < 2^64
-      p[i + j] = (uint32_t)c;
-      c >>= 32;
-    }
-    p[i + 8] = (uint32_t)c;
-  }
+// r = p mod p_field for a 512-bit product p (16 limbs): fold the high half by 2^256 = 2^32 + 977.
+BM_DEV void fe_reduce512(fe& r, const uint32_t (&p)[16]) {
   // fold the high half: L + H * (2^32 + 977)
   uint32_t t[8];
   uint64_t c = 0;
@@ -160,7 +148,57 @@ BM_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
   fe_cond_sub_p(r, t, (uint32_t)e);
 }
 
-BM_DEV void fe_sqr(fe& r, const fe& a) { fe_mul(r, a, a); }
+
+BM_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
+  uint32_t p[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) p[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      c += (uint64_t)a.d[i] * b.d[j] + p[i + j];  // <= (2^32-1)^2 + 2(2^32-1) < 2^64
+      p[i + j] = (uint32_t)c;
+      c >>= 32;
+    }
+    p[i + 8] = (uint32_t)c;
+  }
+  fe_reduce512(r, p);
+}
+
+// r = a^2: the 28 cross products once, doubled by a 1-bit funnel shift, plus the 8 squares
+// (36 v_mad_u64_u32 instead of 64) -- the inversion is 255 of these per point.
+BM_DEV void fe_sqr(fe& r, const fe& a) {
+  uint32_t p[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) p[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = i + 1; j < 8; ++j) {
+      c += (uint64_t)a.d[i] * a.d[j] + p[i + j];
+      p[i + j] = (uint32_t)c;
+      c >>= 32;
+    }
+    p[i + 8] = (uint32_t)c;
+  }
+  // cross sum < 2^511: doubling cannot carry out of 16 limbs
+#pragma unroll
+  for (int i = 15; i > 0; --i) p[i] = (p[i] << 1) | (p[i - 1] >> 31);
+  p[0] <<= 1;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (uint64_t)a.d[i] * a.d[i] + p[2 * i];
+    p[2 * i] = (uint32_t)c;
+    c = (c >> 32) + p[2 * i + 1];
+    p[2 * i + 1] = (uint32_t)c;
+    c >>= 32;
+  }
+  fe_reduce512(r, p);
+}
 
 // a^(p-2) = a^-1 (a != 0).  The exponent is [223 ones][0][22 ones][0000101101]; the 255-
 // squaring / 15-multiplication addition chain (runs of 2^n - 1 ones: 1, 2, 3, 6, 9, 11, 22, 44,
@@ -174,7 +212,7 @@ BM_DEV void fe_inv(fe& r, const fe& a) {
 #pragma unroll 1
   for (int s = 0; s < 15; ++s) {
 #pragma unroll 1
-    for (int i = 0; i < N[s]; ++i) fe_mul(t, t, t);
+    for (int i = 0; i < N[s]; ++i) fe_sqr(t, t);
     const int m = M[s];
     fe f;
 #pragma unroll
@@ -301,11 +339,11 @@ BM_DEV uint32_t window(const uint64_t (&kw)[4], int i) {  // window i, least sig
 }
 
 // k*G for the 256-bit scalar given as 4 big-endian 64-bit words (k = w0*2^192 + ... + w3),
-// i.e. the first 32 bytes of a SHA-512 digest read as a big-endian integer (BN_bin2bn).
-// The next window's table entry is loaded before the current addition, so the gather's
-// latency hides behind ~3,000 VALU instructions.  Returns false for k*G = infinity (k = 0).
-BM_DEV bool scalar_mult_base(ge& r, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
-  gej acc;
+// i.e. the first 32 bytes of a SHA-512 digest read as a big-endian integer (BN_bin2bn), left in
+// Jacobian coordinates (acc.inf for k*G = infinity, i.e. k = 0 mod n).  The next window's table
+// entry is loaded before the current addition, so the gather's latency hides behind ~3,000 VALU
+// instructions.
+BM_DEV void scalar_mult_base_jac(gej& acc, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
   acc.inf = true;
   ge q = table[window(kw, 0)];
 #pragma unroll 1
@@ -316,9 +354,34 @@ BM_DEV bool scalar_mult_base(ge& r, const ge* __restrict__ table, const uint64_t
     if (v) gej_add_ge(acc, acc, q);
     q = qn;
   }
+}
+
+// k*G in affine coordinates; returns false for k*G = infinity.
+BM_DEV bool scalar_mult_base(ge& r, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
+  gej acc;
+  scalar_mult_base_jac(acc, table, kw);
   if (acc.inf) return false;
   gej_to_ge(r, acc);
   return true;
+}
+
+// Two Jacobian points (neither at infinity) to affine with ONE inversion (Montgomery's trick):
+// i = (Za Zb)^-1, Za^-1 = i Zb, Zb^-1 = i Za.  The inversion is ~270 multiplications against
+// ~180 for a whole comb, so sharing it between the two keys of a try saves ~30 % of the try.
+BM_DEV void gej_pair_to_ge(ge& ra, ge& rb, const gej& a, const gej& b) {
+  fe zab, i, zia, zib, t;
+  fe_mul(zab, a.z, b.z);
+  fe_inv(i, zab);
+  fe_mul(zia, i, b.z);
+  fe_mul(zib, i, a.z);
+  fe_sqr(t, zia);
+  fe_mul(ra.x, a.x, t);
+  fe_mul(t, t, zia);
+  fe_mul(ra.y, a.y, t);
+  fe_sqr(t, zib);
+  fe_mul(rb.x, b.x, t);
+  fe_mul(t, t, zib);
+  fe_mul(rb.y, b.y, t);
 }
 
 // 4 big-endian 64-bit words of a field element (the 32-byte big-endian serialization)
