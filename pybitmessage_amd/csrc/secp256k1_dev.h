@@ -3,7 +3,8 @@
 // The reference turns a private key into a public key with OpenSSL EC_POINT_mul on secp256k1
 // (src/highlevelcrypto.py:111-140, pointMult).  Here one lane computes k*G for its own k:
 //   * field elements mod p = 2^256 - 2^32 - 977 as 8 x 32-bit little-endian limbs, always fully
-//     reduced; products by v_mad_u64_u32 (operand scanning), reduction by 2^256 = 2^32 + 977;
+//     reduced; products by v_mad_u64_u32 with its carry-out (product scanning, 2 instructions per
+//     32x32 product), reduction by 2^256 = 2^32 + 977;
 //   * k*G by a fixed-base comb: 16 windows of 16 bits, table[i][v] = v * 2^(16i) * G in affine
 //     coordinates (64 MB, built once per device by ar_table_kernel), so one scalar
 //     multiplication is 16 mixed Jacobian+affine additions and one inversion (shared by the two
@@ -48,154 +49,165 @@ BM_DEV bool fe_is_zero(const fe& a) {
   return o == 0;
 }
 
-// r = t mod p for t < 2^256 + small carry c (c in {0,1} after the callers' folds): returns
+// ---- carry primitives ----
+// Limb chains use __builtin_addc/__builtin_subc (v_add_co/v_addc_co with the carry in VCC); the
+// products use v_mad_u64_u32 directly for its carry-out (VOP3b sdst), which no builtin exposes:
+// a 64-bit column accumulator plus a 32-bit top word absorb every product at 2 instructions
+// (mad + addc), against ~4 (mad + 64-bit add + 2 moves to build zero-extended pairs) for the
+// uint64_t operand-scanning form.
+
+// (acc, top) += a * b
+BM_DEV void mac(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
+  uint64_t cc, unused;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
+  asm("v_addc_co_u32_e64 %0, %1, %0, 0, %2" : "+v"(top), "=s"(unused) : "s"(cc));
+}
+
+// acc += a * b; top = the carry out (first product of a column)
+BM_DEV void mac_first(uint64_t& acc, uint32_t& top, uint32_t a, uint32_t b) {
+  uint64_t cc, unused;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(cc) : "v"(a), "v"(b));
+  asm("v_addc_co_u32_e64 %0, %1, 0, 0, %2" : "=v"(top), "=s"(unused) : "s"(cc));
+}
+
+// acc += a (a 32-bit add into the 64-bit accumulator, as a * 1)
+BM_DEV void add_nc(uint64_t& acc, uint32_t a) {
+  uint64_t unused;
+  asm("v_mad_u64_u32 %0, %1, %2, 1, %0" : "+v"(acc), "=s"(unused) : "v"(a));
+}
+
+// acc += a * 977 (977 = 2^256 mod p - 2^32, from an SGPR)
+BM_DEV void mad977_nc(uint64_t& acc, uint32_t a) {
+  uint64_t unused;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(acc), "=s"(unused) : "v"(a), "s"(C0));
+}
+
+// a * b as 64 bits
+BM_DEV uint64_t mul_wide(uint32_t a, uint32_t b) {
+  uint64_t r, unused;
+  asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(r), "=s"(unused) : "v"(a), "v"(b));
+  return r;
+}
+
+// r = t mod p for t < 2^256 + carry * 2^256 (carry in {0,1}, t < p when it is set): returns
 // t - p when t >= p.  t >= p  <=>  t + (2^256 - p) carries out of 256 bits.
 BM_DEV void fe_cond_sub_p(fe& r, const uint32_t (&t)[8], uint32_t carry) {
-  uint32_t u[8];
-  uint64_t c = (uint64_t)t[0] + C0;
-  u[0] = (uint32_t)c;
-  c = (c >> 32) + (uint64_t)t[1] + 1;
-  u[1] = (uint32_t)c;
-  c >>= 32;
+  uint32_t u[8], c;
+  u[0] = __builtin_addc(t[0], C0, 0u, &c);
+  u[1] = __builtin_addc(t[1], 1u, c, &c);
 #pragma unroll
-  for (int i = 2; i < 8; ++i) {
-    c += t[i];
-    u[i] = (uint32_t)c;
-    c >>= 32;
-  }
+  for (int i = 2; i < 8; ++i) u[i] = __builtin_addc(t[i], 0u, c, &c);
   const bool ge_p = (c | carry) != 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) r.d[i] = ge_p ? u[i] : t[i];
 }
 
 BM_DEV void fe_add(fe& r, const fe& a, const fe& b) {
-  uint32_t t[8];
-  uint64_t c = 0;
+  uint32_t t[8], c = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    c += (uint64_t)a.d[i] + b.d[i];
-    t[i] = (uint32_t)c;
-    c >>= 32;
-  }
-  fe_cond_sub_p(r, t, (uint32_t)c);
+  for (int i = 0; i < 8; ++i) t[i] = __builtin_addc(a.d[i], b.d[i], c, &c);
+  fe_cond_sub_p(r, t, c);
 }
 
 BM_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
-  uint32_t t[8];
-  uint32_t bw = 0;
+  uint32_t t[8], bw = 0;
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint64_t v = (uint64_t)a.d[i] - b.d[i] - bw;
-    t[i] = (uint32_t)v;
-    bw = (uint32_t)(v >> 32) & 1;
-  }
+  for (int i = 0; i < 8; ++i) t[i] = __builtin_subc(a.d[i], b.d[i], bw, &bw);
   // on borrow add p back: t + p = t - (2^32 + 977) mod 2^256
   const uint32_t m = 0u - bw;
-  uint64_t v = (uint64_t)t[0] - (C0 & m);
-  r.d[0] = (uint32_t)v;
-  uint32_t b2 = (uint32_t)(v >> 32) & 1;
-  v = (uint64_t)t[1] - (1u & m) - b2;
-  r.d[1] = (uint32_t)v;
-  b2 = (uint32_t)(v >> 32) & 1;
+  uint32_t b2;
+  r.d[0] = __builtin_subc(t[0], C0 & m, 0u, &b2);
+  r.d[1] = __builtin_subc(t[1], 1u & m, b2, &b2);
 #pragma unroll
-  for (int i = 2; i < 8; ++i) {
-    v = (uint64_t)t[i] - b2;
-    r.d[i] = (uint32_t)v;
-    b2 = (uint32_t)(v >> 32) & 1;
-  }
+  for (int i = 2; i < 8; ++i) r.d[i] = __builtin_subc(t[i], 0u, b2, &b2);
 }
 
-// r = 2a, 3a, 8a as additions (cheap, exact)
+// r = 2a as an addition (cheap, exact)
 BM_DEV void fe_dbl(fe& r, const fe& a) { fe_add(r, a, a); }
 
-// r = p mod p_field for a 512-bit product p (16 limbs): fold the high half by 2^256 = 2^32 + 977.
+// r = p mod p_field for a 512-bit product p (16 limbs): t = L + H * 977 + H * 2^32 column by
+// column (each column < 2^43, no carry out of the accumulator), then the overflow c < 2^33 above
+// 2^256 folded once more the same way, a last 0/1 fold and the conditional subtraction.
 BM_DEV void fe_reduce512(fe& r, const uint32_t (&p)[16]) {
-  // fold the high half: L + H * (2^32 + 977)
   uint32_t t[8];
-  uint64_t c = 0;
+  uint64_t acc = p[0];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    c += (uint64_t)p[i] + (uint64_t)p[8 + i] * C0 + (i ? p[7 + i] : 0u);
-    t[i] = (uint32_t)c;
-    c >>= 32;
+    if (i) add_nc(acc, p[i]);
+    mad977_nc(acc, p[8 + i]);
+    if (i) add_nc(acc, p[7 + i]);
+    t[i] = (uint32_t)acc;
+    acc >>= 32;
   }
-  c += p[15];  // the H * 2^32 term's top limb; now value = t + c * 2^256, c < 2^34
-  // fold c * (2^32 + 977)
-  uint64_t d = (uint64_t)t[0] + c * C0;
-  t[0] = (uint32_t)d;
-  d = (d >> 32) + (uint64_t)t[1] + c;
-  t[1] = (uint32_t)d;
-  d >>= 32;
+  add_nc(acc, p[15]);  // value = t + acc * 2^256, acc = ah * 2^32 + al < 2^33
+  const uint32_t al = (uint32_t)acc, ah = (uint32_t)(acc >> 32);
+  // + acc * (2^32 + 977): al*977 into limb 0, al + ah*977 into limb 1, ah into limb 2
+  uint64_t lo = t[0];
+  mad977_nc(lo, al);
+  t[0] = (uint32_t)lo;
+  const uint32_t x = (uint32_t)(lo >> 32) + ah * C0;  // < 2^11
+  uint32_t c, c2;
+  t[1] = __builtin_addc(t[1], al, 0u, &c);
+  t[1] = __builtin_addc(t[1], x, 0u, &c2);
+  t[2] = __builtin_addc(t[2], ah, c, &c);
+  t[2] = __builtin_addc(t[2], 0u, c2, &c2);
+  c |= c2;  // at most one of them is set
 #pragma unroll
-  for (int i = 2; i < 8; ++i) {
-    d += t[i];
-    t[i] = (uint32_t)d;
-    d >>= 32;
-  }
-  // d in {0,1}: one more fold of 2^256 (t is tiny when it happens)
-  const uint32_t m = 0u - (uint32_t)d;
-  uint64_t e = (uint64_t)t[0] + (C0 & m);
-  t[0] = (uint32_t)e;
-  e = (e >> 32) + (uint64_t)t[1] + (1u & m);
-  t[1] = (uint32_t)e;
-  e >>= 32;
+  for (int i = 3; i < 8; ++i) t[i] = __builtin_addc(t[i], 0u, c, &c);
+  // c in {0,1}: one more fold of 2^256 (t is tiny when it happens)
+  const uint32_t m = 0u - c;
+  t[0] = __builtin_addc(t[0], C0 & m, 0u, &c);
+  t[1] = __builtin_addc(t[1], 1u & m, c, &c);
 #pragma unroll
-  for (int i = 2; i < 8; ++i) {
-    e += t[i];
-    t[i] = (uint32_t)e;
-    e >>= 32;
-  }
-  fe_cond_sub_p(r, t, (uint32_t)e);
+  for (int i = 2; i < 8; ++i) t[i] = __builtin_addc(t[i], 0u, c, &c);
+  fe_cond_sub_p(r, t, c);
 }
 
-
+// 512-bit product by columns (product scanning): column k sums a_i b_j over i + j = k.
 BM_DEV void fe_mul(fe& r, const fe& a, const fe& b) {
   uint32_t p[16];
+  uint64_t acc = 0;
+  uint32_t top = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) p[i] = 0;
+  for (int k = 0; k < 15; ++k) {
+    const int i0 = k < 8 ? 0 : k - 7, i1 = k < 8 ? k : 7;
+    mac_first(acc, top, a.d[i0], b.d[k - i0]);
 #pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      c += (uint64_t)a.d[i] * b.d[j] + p[i + j];  // <= (2^32-1)^2 + 2(2^32-1) < 2^64
-      p[i + j] = (uint32_t)c;
-      c >>= 32;
-    }
-    p[i + 8] = (uint32_t)c;
+    for (int i = i0 + 1; i <= i1; ++i) mac(acc, top, a.d[i], b.d[k - i]);
+    p[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)top << 32);
   }
+  p[15] = (uint32_t)acc;
   fe_reduce512(r, p);
 }
 
-// r = a^2: the 28 cross products once, doubled by a 1-bit funnel shift, plus the 8 squares
-// (36 v_mad_u64_u32 instead of 64) -- the inversion is 255 of these per point.
+// r = a^2: the 28 cross products once (product scanning), doubled by a 1-bit funnel shift, plus
+// the 8 squares -- the inversion is 255 of these per point.
 BM_DEV void fe_sqr(fe& r, const fe& a) {
   uint32_t p[16];
+  p[0] = 0;
+  uint64_t acc = 0;
+  uint32_t top = 0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) p[i] = 0;
+  for (int k = 1; k < 14; ++k) {
+    const int i0 = k < 8 ? 0 : k - 7, i1 = (k - 1) / 2;  // i < j = k - i
+    mac_first(acc, top, a.d[i0], a.d[k - i0]);
 #pragma unroll
-  for (int i = 0; i < 7; ++i) {
-    uint64_t c = 0;
-#pragma unroll
-    for (int j = i + 1; j < 8; ++j) {
-      c += (uint64_t)a.d[i] * a.d[j] + p[i + j];
-      p[i + j] = (uint32_t)c;
-      c >>= 32;
-    }
-    p[i + 8] = (uint32_t)c;
+    for (int i = i0 + 1; i <= i1; ++i) mac(acc, top, a.d[i], a.d[k - i]);
+    p[k] = (uint32_t)acc;
+    acc = (acc >> 32) | ((uint64_t)top << 32);
   }
-  // cross sum < 2^511: doubling cannot carry out of 16 limbs
+  p[14] = (uint32_t)acc;  // cross sum < 2^511: nothing above limb 14 but its carry bit
+  p[15] = (uint32_t)(acc >> 32);
 #pragma unroll
-  for (int i = 15; i > 0; --i) p[i] = (p[i] << 1) | (p[i - 1] >> 31);
-  p[0] <<= 1;
-  uint64_t c = 0;
+  for (int i = 15; i > 0; --i) p[i] = __builtin_amdgcn_alignbit(p[i], p[i - 1], 31);
+  p[0] = 0;  // p[0] was 0 before the doubling too
+  uint32_t c = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    c += (uint64_t)a.d[i] * a.d[i] + p[2 * i];
-    p[2 * i] = (uint32_t)c;
-    c = (c >> 32) + p[2 * i + 1];
-    p[2 * i + 1] = (uint32_t)c;
-    c >>= 32;
+    const uint64_t sq = mul_wide(a.d[i], a.d[i]);
+    p[2 * i] = __builtin_addc(p[2 * i], (uint32_t)sq, c, &c);
+    p[2 * i + 1] = __builtin_addc(p[2 * i + 1], (uint32_t)(sq >> 32), c, &c);
   }
   fe_reduce512(r, p);
 }

@@ -87,7 +87,7 @@ def test_random_batch_vs_c_oracle(gpulib, coracle):
 
 
 @pytest.mark.parametrize('layout,step', [([0], 1 << 28), ([0], 8192 * 3), ([0, 0], 1 << 20),
-                                         ([0, 0, 0], 8192 * 5)])
+                                         ([0, 0, 0], 8192 * 5), ([0, 0], 3001), ([0], (1 << 26) + 777)])
 def test_shard_layouts_and_step_sizes(gpulib, shards, coracle, golden, layout, step):
     """Several shards on one GPU exercise the multi-device nonce-sharding path (each shard
     is its own stream + object table); tiny steps force windows to split across shards and

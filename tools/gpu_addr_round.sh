@@ -1,6 +1,6 @@
 set -euo pipefail
 export TMPDIR=/tmp
-O=gpurun_out/r01r
+O=gpurun_out/${RUN_TAG:-r01r}
 mkdir -p $O
 timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest.log 2>&1
 tail -1 $O/pytest.log

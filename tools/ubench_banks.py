@@ -46,20 +46,16 @@ def mixed(second, group):
 
 PATS = []
 PATS.append(('bitop3 banks 012, 4 waves/SIMD', chains3('v_bitop3_b32', 0, 1, 2, tail=' bitop3:0x96'), 1, 0))
-PATS.append(('bitop3 banks 012, 1 wave/SIMD', chains3('v_bitop3_b32', 0, 1, 2, tail=' bitop3:0x96'), 1, 1))
-PATS.append(('bitop3 banks 012, 2 waves/SIMD', chains3('v_bitop3_b32', 0, 1, 2, tail=' bitop3:0x96'), 1, 2))
-PATS.append(('xor, 1 wave/SIMD', ['v_xor_b32 v%d, v%d, v%d' % (8 + 12 * c, 8 + 12 * c, 9 + 12 * c) for c in range(8)], 1, 1))
-PATS.append(('alignbit, 1 wave/SIMD', mixed('xor', 8)[:8], 1, 1))
-for grp in (1, 2, 4, 8):
-    PATS.append(('alignbit/bitop3 alternating in groups of %d' % grp, mixed('bitop3', grp), 1, 0))
-    PATS.append(('alignbit/xor alternating in groups of %d' % grp, mixed('xor', grp), 1, 0))
-for bar in (0, 1, 4):
-    PATS.append(('SYNC%d alignbit/bitop3 groups of 1, 1024-thread blocks, barrier every %d' % (bar, bar), mixed('bitop3', 1), 1, 0))
-    PATS.append(('SYNC%d alignbit/bitop3 groups of 8, 1024-thread blocks, barrier every %d' % (bar, bar), mixed('bitop3', 8), 1, 0))
-PATS.append(('alignbit/bitop3 groups of 1, 1 wave/SIMD', mixed('bitop3', 1), 1, 1))
-PATS.append(('alignbit/xor groups of 1, 1 wave/SIMD', mixed('xor', 1), 1, 1))
+PATS.append(('alignbit banks 01', [l.rsplit(',', 1)[0] + ', 7' for l in chains3('v_alignbit_b32', 0, 1, 2)], 1, 0))
+PATS.append(('mad_u64_u32 (per instr)', ['v_mad_u64_u32 v[%d:%d], s[44:45], v%d, v%d, v[%d:%d]' % (8 + 12 * c, 9 + 12 * c, 12 + 12 * c, 13 + 12 * c, 8 + 12 * c, 9 + 12 * c) for c in range(8)], 1, 0))
+PATS.append(('mul_lo_u32', ['v_mul_lo_u32 v%d, v%d, v%d' % (8 + 12 * c, 8 + 12 * c, 13 + 12 * c) for c in range(8)], 1, 0))
+PATS.append(('mul_hi_u32', ['v_mul_hi_u32 v%d, v%d, v%d' % (8 + 12 * c, 8 + 12 * c, 13 + 12 * c) for c in range(8)], 1, 0))
+PATS.append(('fma_f64', ['v_fma_f64 v[%d:%d], v[%d:%d], v[%d:%d], v[%d:%d]' % (8 + 12 * c, 9 + 12 * c, 8 + 12 * c, 9 + 12 * c, 14 + 12 * c, 15 + 12 * c, 16 + 12 * c, 17 + 12 * c) for c in range(8)], 1, 0))
+PATS.append(('add_co_u32 e32 (vcc)', ['v_add_co_u32_e32 v%d, vcc, v%d, v%d' % (8 + 12 * c, 8 + 12 * c, 13 + 12 * c) for c in range(8)], 1, 0))
+PATS.append(('addc_co_u32 e32 (vcc in/out)', ['v_addc_co_u32_e32 v%d, vcc, v%d, v%d, vcc' % (8 + 12 * c, 8 + 12 * c, 13 + 12 * c) for c in range(8)], 1, 0))
+PATS.append(('add_co_u32 e64 (sgpr carry)', ['v_add_co_u32_e64 v%d, s[%d:%d], v%d, v%d' % (8 + 12 * c, 46 + 2 * (c % 4), 47 + 2 * (c % 4), 8 + 12 * c, 13 + 12 * c) for c in range(8)], 1, 0))
 
-CLOB = ', '.join('"v%d"' % i for i in range(112)) + ', "s40"'
+CLOB = ', '.join('"v%d"' % i for i in range(112)) + ', "s40", "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "vcc"'
 
 
 def body(lines, reps):
