@@ -9,10 +9,13 @@
 //     coordinates (64 MB, built once per device by ar_table_kernel), so one scalar
 //     multiplication is 16 mixed Jacobian+affine additions and one inversion (shared by the two
 //     keys of an address try, gej_pair_to_ge);
-//   * inversion by Fermat (a^(p-2)) with the 255-squaring / 15-multiplication addition chain
-//     for the exponent's bit pattern [223 ones][0][22 ones][0000101101].
+//   * inversion by Bernstein-Yang divsteps (modinv_dev.h: 600 divsteps on 32-bit words + 20
+//     updates of 9 x 30-bit limbs); Fermat (a^(p-2), 255 squarings + 15 products) is kept
+//     behind -DAR_INV_FERMAT for A/B runs.
 #pragma once
 #include <stdint.h>
+
+#include "modinv_dev.h"
 
 #ifndef BM_DEV
 #define BM_DEV __device__ __forceinline__
@@ -212,6 +215,10 @@ BM_DEV void fe_sqr(fe& r, const fe& a) {
   fe_reduce512(r, p);
 }
 
+// a^-1 mod p (a != 0; a = 0 gives 0).
+#ifndef AR_INV_FERMAT
+BM_DEV void fe_inv(fe& r, const fe& a) { mi::inv_mod_p(r.d, a.d); }
+#else
 // a^(p-2) = a^-1 (a != 0).  The exponent is [223 ones][0][22 ones][0000101101]; the 255-
 // squaring / 15-multiplication addition chain (runs of 2^n - 1 ones: 1, 2, 3, 6, 9, 11, 22, 44,
 // 88, 176, 220, 223) runs as a rolled loop of (squarings, multiplier) steps so the kernel holds
@@ -249,6 +256,7 @@ BM_DEV void fe_inv(fe& r, const fe& a) {
   }
   r = t;
 }
+#endif
 
 // ---- group law (y^2 = x^3 + 7, a = 0) ----
 
