@@ -394,6 +394,10 @@ def run_addr_bench(args, dist):
     lib = _lib.get()
     pp = ADDR_PASSPHRASE + b' rank %d' % dist.rank
     nb = args.null_bytes
+    lib.bmpow_addr_set_comb(args.addr_comb)
+    t0 = time.perf_counter()
+    addressgen.search_deterministic(b'comb table build', 1)  # builds the comb table(s) once per device
+    table_s = time.perf_counter() - t0
     for _ in range(args.warmup):
         f = addressgen.search_deterministic(pp, nb)
     dist.barrier()
@@ -406,8 +410,11 @@ def run_addr_bench(args, dist):
     st = _lib.BmpowStats()
     lib.bmpow_get_stats(ctypes.byref(st))
     assert f.ripe[:nb] == b'\x00' * nb
-    return {'desc': 'addrgen: deterministic address search, %d null bytes, passphrase %r, found k=%d' % (nb, pp, f.k),
-            'tries': float(f.k + 1) * args.steps, 'elapsed': elapsed, 'stats': st, 'k': f.k}
+    comb = lib.bmpow_addr_last_comb()
+    return {'desc': 'addrgen: deterministic address search, %d null bytes, passphrase %r, found k=%d, '
+                    '%d-bit comb' % (nb, pp, f.k, comb),
+            'tries': float(f.k + 1) * args.steps, 'elapsed': elapsed, 'stats': st, 'k': f.k,
+            'comb_bits': comb, 'table_build_s': table_s}
 
 
 def summarize_addr(args, dist, r, lib_version):
@@ -422,6 +429,8 @@ def summarize_addr(args, dist, r, lib_version):
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32', 'data': 'synthetic',
         'config': {'workload': r['desc'], 'parallelism': 'dp%d' % dist.world, 'lib': lib_version},
         'launched_tries_per_s': round(launched / el_max, 1),
+        'comb_bits': r['comb_bits'],
+        'table_build_s': round(r['table_build_s'], 3),  # one-time per device, before the timed region
     }
     if st.addr_kernel_ms > 0:
         line['kernel'] = {'name': 'ar_search_kernel', 'tries_per_s': round(st.addr_tries / (st.addr_kernel_ms * 1e-3), 1),
@@ -513,6 +522,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--config', default='c2', choices=['c1', 'c2', 'c3', 'c4', 'c5', 'verify', 'addrgen'])
     ap.add_argument('--null-bytes', type=int, default=3, help='addrgen: leading zero bytes of the ripe')
+    ap.add_argument('--addr-comb', type=int, default=24, choices=[0, 16, 24],
+                    help='addrgen: comb window bits (0 = the library\'s automatic choice)')
     ap.add_argument('--objects', type=int, default=None, help='override the object count (c2/c4/c5)')
     ap.add_argument('--c3-log2', type=int, default=36)
     ap.add_argument('--step-trials', type=int, default=0, help='per-launch trial budget per GPU (0 = lib default)')

@@ -205,6 +205,14 @@ BMPOW_API int bmpow_address_search(const uint8_t *passphrase, size_t len, uint64
 BMPOW_API int bmpow_address_search_random(const uint8_t priv_signing[32], const uint8_t *seed, size_t seed_len,
                                           uint64_t start, uint64_t max_tries, int null_bytes, bmpow_address *out);
 
+/* Fixed-base comb used by the address search: 16-bit windows (64 MB table, 16 additions per k*G)
+ * or 24-bit windows (10.7 GB table per device, 11 additions, ~25 % more tries/s, ~0.4 s to build
+ * once).  wbits = 0 (default): automatic -- the 24-bit comb when it is already built or a search
+ * is expected to need >= 2^32 tries; 16 or 24 force one.  Returns the previous setting or < 0. */
+BMPOW_API int bmpow_addr_set_comb(int wbits);
+/* Window width (16 or 24) the last address search ran with; 0 before the first. */
+BMPOW_API int bmpow_addr_last_comb(void);
+
 /* ---- instrumentation (bench.py's roofline leg) ---- */
 typedef struct bmpow_stats {
     uint64_t launches;        /* search-kernel launches (summed over shards) */

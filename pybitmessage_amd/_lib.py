@@ -97,6 +97,8 @@ SIGNATURES = [
      [ctypes.c_char_p, ctypes.c_size_t, _u64, _u64, ctypes.c_int, ctypes.POINTER(BmpowAddress)]),
     ('bmpow_address_search_random', ctypes.c_int,
      [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, _u64, _u64, ctypes.c_int, ctypes.POINTER(BmpowAddress)]),
+    ('bmpow_addr_set_comb', ctypes.c_int, [ctypes.c_int]),
+    ('bmpow_addr_last_comb', ctypes.c_int, []),
     ('BitmessagePOW', ctypes.c_ulonglong, [ctypes.c_char_p, ctypes.c_ulonglong]),
 ]
 

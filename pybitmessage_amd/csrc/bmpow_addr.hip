@@ -118,6 +118,7 @@ BM_DEV bool prefix_ok(const uint32_t (&rh)[5], uint32_t null_bytes) {
 // mode 1 (random): fixed signing key prm->pub_s; encryption key from m = k of a random seed.
 // Both public keys leave the comb in Jacobian coordinates and share one inversion (mode 1 feeds
 // the given signing key in with Z = 1, so both modes run the same code).
+template <int W>
 BM_DEV bool try_keys(const ar_params* __restrict__ prm, const ge* __restrict__ table, uint64_t k,
                      uint64_t (&hs)[8], uint64_t (&he)[8], ge& ps, ge& pe) {
   const uint32_t first = prm->mode == 0 ? 0 : 1;  // mode 1: the signing key is given
@@ -138,7 +139,7 @@ BM_DEV bool try_keys(const ar_params* __restrict__ prm, const ge* __restrict__ t
     key_hash(h, prm, m);
     const uint64_t kw[4] = {h[0], h[1], h[2], h[3]};
     gej r;
-    ec::scalar_mult_base_jac(r, table, kw);
+    ec::scalar_mult_base_jac<W>(r, table, kw);
     ok = ok && !r.inf;
     if (which == 0) {
       js = r;
@@ -166,13 +167,13 @@ BM_DEV void ripe_of_points(uint32_t (&rh)[5], const ge& ps, const ge& pe) {
 
 }  // namespace
 
-// table[i << W | v] = v * 2^(W i) * G (affine), v = 1 .. 2^W - 1 (W = ec::kWBits).  One thread
-// per entry; entries v = 0 are never read as points (the comb skips zero windows).
-__global__ __launch_bounds__(64) void ar_table_kernel(ge* __restrict__ table) {
-  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
-  if (t >= ec::kTableEntries) return;
-  const uint32_t i = (uint32_t)(t >> ec::kWBits), v = (uint32_t)t & ec::kWMask;
-  if (v == 0) return;
+// The comb table in two launches.  ar_base_kernel: bases[i] = 2^(W i) * G (affine), one thread per
+// window.  ar_table_kernel: table[i << W | v] = v * bases[i] by double-and-add over v's W bits,
+// one thread per entry (entries v = 0 are never read as points: the comb skips zero windows).
+template <int W>
+__global__ __launch_bounds__(64) void ar_base_kernel(ge* __restrict__ bases) {
+  const uint32_t i = blockIdx.x * 64 + threadIdx.x;
+  if (i >= (uint32_t)ec::comb<W>::kWindows) return;
   gej b;
   b.inf = false;
   // G
@@ -185,12 +186,20 @@ __global__ __launch_bounds__(64) void ar_table_kernel(ge* __restrict__ table) {
     b.y.d[j] = gy[j];
   }
   ec::fe_set(b.z, 1);
-  for (uint32_t d = 0; d < (uint32_t)ec::kWBits * i; ++d) ec::gej_double(b, b);  // 2^(W i) * G
-  ge ba;
-  ec::gej_to_ge(ba, b);
+  for (uint32_t d = 0; d < (uint32_t)W * i; ++d) ec::gej_double(b, b);  // 2^(W i) * G
+  ec::gej_to_ge(bases[i], b);
+}
+
+template <int W>
+__global__ __launch_bounds__(64) void ar_table_kernel(const ge* __restrict__ bases, ge* __restrict__ table) {
+  const size_t t = (size_t)blockIdx.x * 64 + threadIdx.x;
+  if (t >= ec::comb<W>::kEntries) return;
+  const uint32_t i = (uint32_t)(t >> W), v = (uint32_t)t & ec::comb<W>::kMask;
+  if (v == 0) return;
+  const ge ba = bases[i];
   gej acc;
   acc.inf = true;
-  for (int bit = ec::kWBits - 1; bit >= 0; --bit) {  // v * B, MSB first
+  for (int bit = 31 - __builtin_clz(v); bit >= 0; --bit) {  // v * B, MSB first
     ec::gej_double(acc, acc);
     if ((v >> bit) & 1) ec::gej_add_ge(acc, acc, ba);
   }
@@ -207,7 +216,7 @@ __global__ __launch_bounds__(64) void ar_table_kernel(ge* __restrict__ table) {
 #define AR_WAVES 3
 #endif
 #define AR_OCC __attribute__((amdgpu_waves_per_eu(AR_WAVES)))
-template <bool kResolve>
+template <bool kResolve, int W>
 __global__ __launch_bounds__(64) AR_OCC void ar_search_kernel(const ar_params* __restrict__ prm, const ge* __restrict__ table,
                                                        uint64_t start, uint32_t count,
                                                        unsigned long long* __restrict__ best,
@@ -218,7 +227,7 @@ __global__ __launch_bounds__(64) AR_OCC void ar_search_kernel(const ar_params* _
   if (!kResolve && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) return;
   uint64_t hs[8], he[8];
   ge ps, pe;
-  const bool ok = try_keys(prm, table, k, hs, he, ps, pe);
+  const bool ok = try_keys<W>(prm, table, k, hs, he, ps, pe);
   uint32_t rh[5] = {0, 0, 0, 0, 0};
   if (ok) ripe_of_points(rh, ps, pe);
   if (kResolve) {
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(64) void ar_pubkey_kernel(const uint64_t* __restric
   if (g >= n) return;
   const uint64_t kw[4] = {privs[4 * g], privs[4 * g + 1], privs[4 * g + 2], privs[4 * g + 3]};
   ge r;
-  ok[g] = ec::scalar_mult_base(r, table, kw) ? 1u : 0u;
+  ok[g] = ec::scalar_mult_base<ec::kCombSmall>(r, table, kw) ? 1u : 0u;
   pubs[g] = r;
 }
 
@@ -268,22 +277,48 @@ __global__ void ar_midstate_kernel(const uint8_t* __restrict__ pass, uint64_t nf
 // ---------------------------------------------------------------------------------------
 // Launch wrappers (C++ linkage, used by bmpow_host.hip).
 // ---------------------------------------------------------------------------------------
-hipError_t ar_launch_table(hipStream_t st, ge* table) {
-  hipLaunchKernelGGL(ar_table_kernel, dim3((uint32_t)(ec::kTableEntries / 64)), dim3(64), 0, st, table);
+// table: ec::comb<W>::kEntries entries followed by ec::comb<W>::kWindows scratch entries (the bases)
+template <int W>
+hipError_t launch_table(hipStream_t st, ge* table) {
+  using C = ec::comb<W>;
+  ge* bases = table + C::kEntries;
+  hipLaunchKernelGGL(ar_base_kernel<W>, dim3(1), dim3(64), 0, st, bases);
+  hipLaunchKernelGGL(ar_table_kernel<W>, dim3((uint32_t)((C::kEntries + 63) / 64)), dim3(64), 0, st,
+                     (const ge*)bases, table);
   return hipGetLastError();
 }
 
-hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, const ge* table, uint64_t start, uint32_t count,
-                            unsigned long long* best) {
+size_t ar_table_entries(int wbits) {
+  return wbits == ec::kCombLarge ? ec::comb<ec::kCombLarge>::kEntries + ec::comb<ec::kCombLarge>::kWindows
+                                 : ec::comb<ec::kCombSmall>::kEntries + ec::comb<ec::kCombSmall>::kWindows;
+}
+
+hipError_t ar_launch_table(hipStream_t st, ge* table, int wbits) {
+  return wbits == ec::kCombLarge ? launch_table<ec::kCombLarge>(st, table) : launch_table<ec::kCombSmall>(st, table);
+}
+
+hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, const ge* table, int wbits, uint64_t start,
+                            uint32_t count, unsigned long long* best) {
   if (count == 0) return hipSuccess;
-  hipLaunchKernelGGL(ar_search_kernel<false>, dim3((count + 63) / 64), dim3(64), 0, st, prm, table, start, count, best,
-                     (ar_result*)nullptr);
+  if (wbits == ec::kCombLarge)
+    hipLaunchKernelGGL((ar_search_kernel<false, ec::kCombLarge>), dim3((count + 63) / 64), dim3(64), 0, st, prm, table,
+                       start, count, best, (ar_result*)nullptr);
+  else
+    hipLaunchKernelGGL((ar_search_kernel<false, ec::kCombSmall>), dim3((count + 63) / 64), dim3(64), 0, st, prm, table,
+                       start, count, best, (ar_result*)nullptr);
   return hipGetLastError();
 }
 
-hipError_t ar_launch_resolve(hipStream_t st, const ar_params* prm, const ge* table, uint64_t k, ar_result* out) {
-  hipLaunchKernelGGL(ar_search_kernel<true>, dim3(1), dim3(64), 0, st, prm, table, k, 1u, (unsigned long long*)nullptr,
-                     out);
+// the resolve step runs with the search's comb (so the tests see that comb's public keys); the
+// pointMult probe (ar_launch_pubkeys) always uses the small one
+hipError_t ar_launch_resolve(hipStream_t st, const ar_params* prm, const ge* table, int wbits, uint64_t k,
+                             ar_result* out) {
+  if (wbits == ec::kCombLarge)
+    hipLaunchKernelGGL((ar_search_kernel<true, ec::kCombLarge>), dim3(1), dim3(64), 0, st, prm, table, k, 1u,
+                       (unsigned long long*)nullptr, out);
+  else
+    hipLaunchKernelGGL((ar_search_kernel<true, ec::kCombSmall>), dim3(1), dim3(64), 0, st, prm, table, k, 1u,
+                       (unsigned long long*)nullptr, out);
   return hipGetLastError();
 }
 

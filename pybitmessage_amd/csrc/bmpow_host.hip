@@ -71,8 +71,10 @@ struct Shard {
   std::vector<uint32_t> item_obj;
   // stats
   double kernel_ms = 0.0;
-  // address search: the fixed-base comb table (v * 2^(8i) * G), built on first use
-  ec::ge* d_table = nullptr;
+  // address search: the fixed-base comb tables (v * 2^(W i) * G) for W = 16 ([0]) and 24 ([1]),
+  // built on first use and shared by the shards of one device (owns_table marks the freeing one)
+  ec::ge* d_table[2] = {nullptr, nullptr};
+  bool owns_table[2] = {false, false};
 };
 
 std::vector<Shard> g_shards;
@@ -106,7 +108,8 @@ void free_shard(Shard& s) {
   if (s.h_items) (void)hipHostFree(s.h_items);
   if (s.h_res) (void)hipHostFree(s.h_res);
   if (s.h_trials) (void)hipHostFree(s.h_trials);
-  if (s.d_table) (void)hipFree(s.d_table);
+  for (int c = 0; c < 2; ++c)
+    if (s.d_table[c] && s.owns_table[c]) (void)hipFree(s.d_table[c]);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
   if (s.stream) (void)hipStreamDestroy(s.stream);
@@ -613,16 +616,59 @@ int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, in
 // ---------------------------------------------------------------------------------------
 namespace {
 
-constexpr uint64_t kAddrMaxStep = 1ULL << 20;  // tries per shard per launch (~tens of ms)
+constexpr uint64_t kAddrMaxStep = 1ULL << 22;  // tries per shard per launch (~10 ms)
 
-int ensure_table(Shard& sh) {
-  if (sh.d_table) return 0;
+// Shards are only ever freed all together (reset / re-init), so a borrowed table never outlives
+// its owner.  The allocation holds ec::kWindows extra entries: ar_launch_table's base points.
+// c = 0: the 16-bit comb (64 MB), c = 1: the 24-bit comb (10.7 GB).
+constexpr int kCombBits[2] = {ec::kCombSmall, ec::kCombLarge};
+
+int ensure_table(Shard& sh, int c = 0) {
+  if (sh.d_table[c]) return 0;
+  for (const Shard& o : g_shards)
+    if (&o != &sh && o.dev == sh.dev && o.d_table[c] && o.owns_table[c]) {
+      sh.d_table[c] = o.d_table[c];
+      return 0;
+    }
   HIPTRY(hipSetDevice(sh.dev));
-  HIPTRY(hipMalloc(&sh.d_table, ec::kTableEntries * sizeof(ec::ge)));
-  HIPTRY(hipMemsetAsync(sh.d_table, 0, ec::kTableEntries * sizeof(ec::ge), sh.stream));
-  HIPTRY(ar_launch_table(sh.stream, sh.d_table));
+  const size_t bytes = ar_table_entries(kCombBits[c]) * sizeof(ec::ge);
+  ec::ge* t = nullptr;
+  const hipError_t e = hipMalloc(&t, bytes);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();  // an out-of-memory here is reported, not sticky
+    return set_err(BMPOW_E_HIP, std::string("comb table allocation: ") + hipGetErrorString(e));
+  }
+  sh.d_table[c] = t;
+  sh.owns_table[c] = true;
+  HIPTRY(hipMemsetAsync(t, 0, bytes, sh.stream));
+  HIPTRY(ar_launch_table(sh.stream, t, kCombBits[c]));
   HIPTRY(hipStreamSynchronize(sh.stream));
   return 0;
+}
+
+// Comb choice for one search: the 24-bit comb when forced (bmpow_addr_set_comb(24)), or in auto
+// mode when it is already built on every shard or the search is expected to take >= 2^32 tries
+// (4+ null bytes: seconds of work, against ~0.4 s to build the table once per device; judged from
+// null_bytes alone, since callers cut long searches into bounded calls); else the 16-bit one.  An
+// auto-mode allocation failure falls back to the small comb.
+int g_addr_comb = 0;       // 0 auto, 16, 24
+int g_addr_last_comb = 0;  // width used by the last search
+
+int addr_pick_comb(int null_bytes) {
+  if (g_addr_comb == ec::kCombSmall) return 0;
+  bool built = true;
+  for (const Shard& sh : g_shards) built = built && sh.d_table[1] != nullptr;
+  const uint64_t expected = null_bytes >= 8 ? kU64Max : (1ULL << (8 * null_bytes));
+  const bool want = g_addr_comb == ec::kCombLarge || built || expected >= (1ULL << 32);
+  if (!want) return 0;
+  for (Shard& sh : g_shards) {
+    const int rc = ensure_table(sh, 1);
+    if (rc < 0) {
+      if (g_addr_comb == ec::kCombLarge) return rc;
+      return 0;
+    }
+  }
+  return 1;
 }
 
 void be_words_from_bytes(const uint8_t* b, uint64_t (&w)[4]) {
@@ -688,7 +734,7 @@ int addr_search_locked(uint32_t mode, const uint8_t* seed, size_t len, const uin
   as.assign(S, AddrShard());
   for (size_t s = 0; s < S; ++s) {
     Shard& sh = g_shards[s];
-    int rc = ensure_table(sh);
+    int rc = ensure_table(sh, 0);
     if (rc < 0) return rc;
     AddrShard& a = as[s];
     HIPTRY(hipMalloc(&a.d_prm, sizeof(ar_params)));
@@ -703,7 +749,7 @@ int addr_search_locked(uint32_t mode, const uint8_t* seed, size_t len, const uin
     HIPTRY(ar_launch_midstate(sh.stream, a.d_seed, nfull, (uint64_t*)a.d_prm));  // mid[] is at offset 0
     if (mode == 1) {
       HIPTRY(hipMemcpyAsync(a.d_priv, pw, sizeof pw, hipMemcpyHostToDevice, sh.stream));
-      HIPTRY(ar_launch_pubkeys(sh.stream, a.d_priv, 1, sh.d_table, &a.d_prm->pub_s, a.d_ok));
+      HIPTRY(ar_launch_pubkeys(sh.stream, a.d_priv, 1, sh.d_table[0], &a.d_prm->pub_s, a.d_ok));
     }
   }
   for (auto& sh : g_shards) {
@@ -717,6 +763,9 @@ int addr_search_locked(uint32_t mode, const uint8_t* seed, size_t len, const uin
     if (!ok) return set_err(BMPOW_E_ARG, "signing private key is zero");
   }
   const uint64_t end = (kU64Max - start < max_tries) ? kU64Max : start + max_tries;
+  const int comb = addr_pick_comb(null_bytes);
+  if (comb < 0) return comb;
+  g_addr_last_comb = kCombBits[comb];
   uint64_t step = 4096;
   for (int b = 0; b < null_bytes && step < kAddrMaxStep; ++b) step = std::min<uint64_t>(step * 256, kAddrMaxStep);
   step = std::max<uint64_t>(step / 4, 4096);
@@ -731,7 +780,8 @@ int addr_search_locked(uint32_t mode, const uint8_t* seed, size_t len, const uin
       Shard& sh = g_shards[s];
       HIPTRY(hipSetDevice(sh.dev));
       HIPTRY(hipEventRecord(sh.ev0, sh.stream));
-      HIPTRY(ar_launch_search(sh.stream, as[s].d_prm, sh.d_table, lo[s], (uint32_t)cnt[s], as[s].d_best));
+      HIPTRY(ar_launch_search(sh.stream, as[s].d_prm, sh.d_table[comb], kCombBits[comb], lo[s], (uint32_t)cnt[s],
+                              as[s].d_best));
       HIPTRY(hipEventRecord(sh.ev1, sh.stream));
     }
     uint64_t best = kU64Max;
@@ -757,7 +807,8 @@ int addr_search_locked(uint32_t mode, const uint8_t* seed, size_t len, const uin
     if (best != kU64Max) {
       Shard& sh = g_shards[best_s];
       HIPTRY(hipSetDevice(sh.dev));
-      HIPTRY(ar_launch_resolve(sh.stream, as[best_s].d_prm, sh.d_table, best, as[best_s].d_res));
+      HIPTRY(ar_launch_resolve(sh.stream, as[best_s].d_prm, sh.d_table[comb], kCombBits[comb], best,
+                               as[best_s].d_res));
       ar_result r;
       HIPTRY(hipMemcpyAsync(&r, as[best_s].d_res, sizeof r, hipMemcpyDeviceToHost, sh.stream));
       HIPTRY(hipStreamSynchronize(sh.stream));
@@ -1155,7 +1206,7 @@ int bmpow_pubkeys(size_t n, const uint8_t* privkeys, uint8_t* pubkeys_out) {
   if (!privkeys || !pubkeys_out) return set_err(BMPOW_E_ARG, "null pointer");
   if (n > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many keys");
   Shard& sh = g_shards[0];
-  rc = ensure_table(sh);
+  rc = ensure_table(sh, 0);
   if (rc < 0) return rc;
   std::vector<uint64_t> w(4 * n);
   for (size_t i = 0; i < n; ++i) {
@@ -1173,7 +1224,7 @@ int bmpow_pubkeys(size_t n, const uint8_t* privkeys, uint8_t* pubkeys_out) {
   if (e == hipSuccess) e = hipMalloc(&d_p, n * sizeof(ec::ge));
   if (e == hipSuccess) e = hipMalloc(&d_ok, n * sizeof(uint32_t));
   if (e == hipSuccess) e = hipMemcpyAsync(d_w, w.data(), w.size() * sizeof(uint64_t), hipMemcpyHostToDevice, sh.stream);
-  if (e == hipSuccess) e = ar_launch_pubkeys(sh.stream, d_w, (uint32_t)n, sh.d_table, d_p, d_ok);
+  if (e == hipSuccess) e = ar_launch_pubkeys(sh.stream, d_w, (uint32_t)n, sh.d_table[0], d_p, d_ok);
   if (e == hipSuccess) e = hipMemcpyAsync(pubs.data(), d_p, n * sizeof(ec::ge), hipMemcpyDeviceToHost, sh.stream);
   if (e == hipSuccess) e = hipMemcpyAsync(ok.data(), d_ok, n * sizeof(uint32_t), hipMemcpyDeviceToHost, sh.stream);
   if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
@@ -1208,6 +1259,20 @@ int bmpow_address_search_random(const uint8_t priv_signing[32], const uint8_t* s
   rc = addr_search_locked(1, seed, seed_len, priv_signing, start, max_tries, null_bytes, out, as);
   addr_free(as);
   return rc;
+}
+
+int bmpow_addr_set_comb(int wbits) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (wbits != 0 && wbits != ec::kCombSmall && wbits != ec::kCombLarge)
+    return set_err(BMPOW_E_ARG, "comb width must be 0 (auto), 16 or 24");
+  const int prev = g_addr_comb;
+  g_addr_comb = wbits;
+  return prev;
+}
+
+int bmpow_addr_last_comb(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  return g_addr_last_comb;
 }
 
 int bmpow_get_stats(bmpow_stats* out) {

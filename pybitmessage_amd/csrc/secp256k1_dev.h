@@ -5,10 +5,10 @@
 //   * field elements mod p = 2^256 - 2^32 - 977 as 8 x 32-bit little-endian limbs, always fully
 //     reduced; products by v_mad_u64_u32 with its carry-out (product scanning, 2 instructions per
 //     32x32 product), reduction by 2^256 = 2^32 + 977;
-//   * k*G by a fixed-base comb: 16 windows of 16 bits, table[i][v] = v * 2^(16i) * G in affine
-//     coordinates (64 MB, built once per device by ar_table_kernel), so one scalar
-//     multiplication is 16 mixed Jacobian+affine additions and one inversion (shared by the two
-//     keys of an address try, gej_pair_to_ge);
+//   * k*G by a fixed-base comb: windows of W = 16 or 24 bits, table[i][v] = v * 2^(W i) * G in
+//     affine coordinates (64 MB or 10.7 GB, built once per device by ar_table_kernel), so one
+//     scalar multiplication is 16 or 11 mixed Jacobian+affine additions and one inversion (shared
+//     by the two keys of an address try, gej_pair_to_ge);
 //   * inversion by Bernstein-Yang divsteps (modinv_dev.h: 600 divsteps on 32-bit words + 20
 //     updates of 9 x 30-bit limbs); Fermat (a^(p-2), 255 squarings + 15 products) is kept
 //     behind -DAR_INV_FERMAT for A/B runs.
@@ -342,44 +342,66 @@ BM_DEV void gej_to_ge(ge& r, const gej& p) {
   fe_mul(r.y, p.y, zi2);
 }
 
-// Comb window width: table[i << AR_WBITS | v] = v * 2^(AR_WBITS * i) * G, 256/AR_WBITS windows.
-// 16 bits: 16 mixed additions per k*G over a 64 MB table (HBM / Infinity-Cache resident);
-// 8 bits: 32 additions over 512 KB.
-#ifndef AR_WBITS
-#define AR_WBITS 16
+// Fixed-base combs: table[i << W | v] = v * 2^(W i) * G (affine), ceil(256 / W) windows, the last
+// one ragged (256 - W (windows - 1) bits, only 2^that entries stored).  Two widths are built:
+//   W = 16: 16 mixed additions per k*G over a 64 MB table (built in ~15 ms);
+//   W = 24: 11 additions over a 10.7 GB table (HBM-resident, ~0.4 s to build once per device),
+// chosen per search by the host (bmpow_host.hip addr_comb_for) so short searches never pay for the
+// big table and long ones run 25 % faster.
+constexpr int kCombSmall = 16;
+#ifndef AR_WBITS_LARGE
+#define AR_WBITS_LARGE 24
 #endif
-constexpr int kWBits = AR_WBITS;
-constexpr int kWindows = 256 / kWBits;
-constexpr uint32_t kWMask = (1u << kWBits) - 1;
-constexpr size_t kTableEntries = (size_t)kWindows << kWBits;
-static_assert(64 % kWBits == 0, "windows must not straddle 64-bit words");
+constexpr int kCombLarge = AR_WBITS_LARGE;
 
-BM_DEV uint32_t window(const uint64_t (&kw)[4], int i) {  // window i, least significant first
-  return (uint32_t)(kw[3 - ((i * kWBits) >> 6)] >> ((i * kWBits) & 63)) & kWMask;
+template <int W>
+struct comb {
+  static_assert(W >= 8 && W <= 26, "comb window width");
+  static constexpr int kWindows = (256 + W - 1) / W;
+  static constexpr int kLastBits = 256 - W * (kWindows - 1);
+  static constexpr uint32_t kMask = (1u << W) - 1;
+  static constexpr size_t kEntries = ((size_t)(kWindows - 1) << W) + ((size_t)1 << kLastBits);
+};
+
+// s (256 bits, s[0] least significant) >>= W
+template <int W>
+BM_DEV void shr256_window(uint64_t (&s)[4]) {
+  s[0] = (s[0] >> W) | (s[1] << (64 - W));
+  s[1] = (s[1] >> W) | (s[2] << (64 - W));
+  s[2] = (s[2] >> W) | (s[3] << (64 - W));
+  s[3] >>= W;
 }
 
 // k*G for the 256-bit scalar given as 4 big-endian 64-bit words (k = w0*2^192 + ... + w3),
 // i.e. the first 32 bytes of a SHA-512 digest read as a big-endian integer (BN_bin2bn), left in
-// Jacobian coordinates (acc.inf for k*G = infinity, i.e. k = 0 mod n).  The next window's table
-// entry is loaded before the current addition, so the gather's latency hides behind ~3,000 VALU
-// instructions.
+// Jacobian coordinates (acc.inf for k*G = infinity, i.e. k = 0 mod n).  Windows are peeled off
+// the low end of a 256-bit shift register (no runtime-indexed register arrays), and the next
+// window's table entry is loaded before the current addition, so the gather's latency hides
+// behind ~2,500 VALU instructions.
+template <int W>
 BM_DEV void scalar_mult_base_jac(gej& acc, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
+  using C = comb<W>;
+  uint64_t s[4] = {kw[3], kw[2], kw[1], kw[0]};
   acc.inf = true;
-  ge q = table[window(kw, 0)];
+  uint32_t v = (uint32_t)s[0] & C::kMask;
+  ge q = table[v];
 #pragma unroll 1
-  for (int i = 0; i < kWindows; ++i) {
-    const uint32_t v = window(kw, i);
+  for (int i = 0; i < C::kWindows; ++i) {
+    shr256_window<W>(s);
+    const uint32_t vn = (uint32_t)s[0] & C::kMask;
     ge qn;
-    if (i + 1 < kWindows) qn = table[((size_t)(i + 1) << kWBits) | window(kw, i + 1)];
+    if (i + 1 < C::kWindows) qn = table[((size_t)(i + 1) << W) | vn];
     if (v) gej_add_ge(acc, acc, q);
     q = qn;
+    v = vn;
   }
 }
 
 // k*G in affine coordinates; returns false for k*G = infinity.
+template <int W>
 BM_DEV bool scalar_mult_base(ge& r, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
   gej acc;
-  scalar_mult_base_jac(acc, table, kw);
+  scalar_mult_base_jac<W>(acc, table, kw);
   if (acc.inf) return false;
   gej_to_ge(r, acc);
   return true;

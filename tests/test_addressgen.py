@@ -149,6 +149,57 @@ def test_gpu_search_budget_and_shards(gpulib, shards):
     assert addressgen.search_deterministic(b'two null bytes', 2).k == 5640
 
 
+@pytest.fixture
+def comb24(gpulib):
+    """Force the 24-bit comb (10.7 GB table) for the test, restore automatic choice after."""
+    lib = _lib.get()
+    lib.bmpow_addr_set_comb(24)
+    yield lib
+    lib.bmpow_addr_set_comb(0)
+
+
+@gpu
+def test_gpu_large_comb_every_try_and_search(comb24, kats):
+    """The 24-bit comb (ragged last window of 16 bits) gives the reference's values for every
+    per-try fixture and the reference's first k for every search fixture."""
+    for t in kats['try_kats']:
+        f = addressgen.search_deterministic(bytes.fromhex(t['passphrase']), 0, t['k'], 1)
+        assert comb24.bmpow_addr_last_comb() == 24
+        assert (f.pub_signing.hex(), f.pub_encryption.hex()) == (t['pub_signing'], t['pub_encryption'])
+        assert f.ripe.hex() == t['ripe'], (t['passphrase'][:16], t['k'])
+    runs = {}
+    for s in kats['search_kats']:
+        runs.setdefault((s['passphrase'], s['null_bytes']), []).append(s)
+    for (pp, nb), ss in runs.items():
+        got = addressgen.deterministic_addresses(bytes.fromhex(pp), len(ss), 4, 1, nb)
+        for g, s in zip(got, ss):
+            assert (g['k'], g['ripe'].hex(), g['address']) == (s['k'], s['ripe'], s['addr4']), s['label']
+    g = addressgen.deterministic_addresses(SAMPLE_SEED, 1, 3)[0]
+    assert g['address'] == SAMPLE_DET_ADDR3 and g['ripe'].hex() == SAMPLE_DET_RIPE
+
+
+@gpu
+def test_gpu_comb_policy(gpulib, shards):
+    """Automatic choice: the 16-bit comb for short searches, the 24-bit one once built (and on
+    every shard); an explicit width is validated."""
+    lib = _lib.get()
+    assert lib.bmpow_addr_set_comb(0) in (0, 16, 24)
+    shards([0, 0])  # fresh shards: no table built yet
+    assert addressgen.search_deterministic(SAMPLE_SEED, 1).k == 21
+    assert lib.bmpow_addr_last_comb() == 16
+    lib.bmpow_addr_set_comb(24)
+    assert addressgen.search_deterministic(SAMPLE_SEED, 1).k == 21
+    assert lib.bmpow_addr_last_comb() == 24
+    lib.bmpow_addr_set_comb(0)
+    assert addressgen.search_deterministic(b'two null bytes', 2).k == 5640
+    assert lib.bmpow_addr_last_comb() == 24  # already built: used
+    assert lib.bmpow_addr_set_comb(20) < 0
+    assert lib.bmpow_addr_set_comb(16) == 0
+    assert addressgen.search_deterministic(b'two null bytes', 2).k == 5640
+    assert lib.bmpow_addr_last_comb() == 16
+    lib.bmpow_addr_set_comb(0)
+
+
 @gpu
 def test_gpu_random_address_property(gpulib):
     import os
