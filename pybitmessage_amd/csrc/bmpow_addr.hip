@@ -165,6 +165,118 @@ BM_DEV void ripe_of_points(uint32_t (&rh)[5], const ge& ps, const ge& pe) {
   ripe_of(rh, xs, ys, xe, ye);
 }
 
+
+#ifndef AR_SINGLE
+// ---- paired tries (the search path): two tries per lane behind ONE inversion ----
+// Lane tries k0 and k0 + 1: four keys (mode 0: 2k0, 2k0+1, 2k0+2, 2k0+3; mode 1: the fixed signing
+// key, k0, the fixed signing key, k0 + 1), four combs left in Jacobian coordinates, then
+// Montgomery's trick over both tries: ZA = Z0 Z1, ZB = Z2 Z3, inv = (ZA ZB)^-1, iA = inv ZB,
+// iB = inv ZA, and per try Zs^-1 = iT Ze, Ze^-1 = iT Zs -- 9 products + 1 inversion for two
+// tries against 6 products + 2 inversions.  X, Y of keys 0..2 wait in LDS (lane-major, so the
+// accesses are bank-conflict free); key 3 stays in registers.
+constexpr int kPairLanes = 64;
+
+BM_DEV void fe_sel(fe& r, bool c, const fe& a, const fe& b) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r.d[j] = c ? a.d[j] : b.d[j];
+}
+
+BM_DEV void stash_put(uint32_t* st, int slot, uint32_t lane, const fe& x, const fe& y) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    st[(slot * 16 + j) * kPairLanes + lane] = x.d[j];
+    st[(slot * 16 + 8 + j) * kPairLanes + lane] = y.d[j];
+  }
+}
+
+BM_DEV void stash_get(const uint32_t* st, int slot, uint32_t lane, fe& x, fe& y) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    x.d[j] = st[(slot * 16 + j) * kPairLanes + lane];
+    y.d[j] = st[(slot * 16 + 8 + j) * kPairLanes + lane];
+  }
+}
+
+// Jacobian (X, Y) with known Z^-1 -> affine
+BM_DEV void to_affine(ge& r, const fe& x, const fe& y, const fe& zi) {
+  fe t;
+  ec::fe_sqr(t, zi);
+  ec::fe_mul(r.x, x, t);
+  ec::fe_mul(t, t, zi);
+  ec::fe_mul(r.y, y, t);
+}
+
+// ripes of tries k0 (rh[0]) and k0 + 1 (rh[1]); ok[t] false when a key of try t is 0 mod n
+template <int W>
+BM_DEV void try_pair(const ar_params* __restrict__ prm, const ge* __restrict__ table, uint64_t k0, uint32_t* st,
+                     uint32_t lane, uint32_t (&rh0)[5], uint32_t (&rh1)[5], bool& ok0, bool& ok1) {
+  const bool fixed_sign = prm->mode != 0;
+  fe z0, z1, z2;
+  ok0 = ok1 = true;
+  gej r;  // after the loop: key 3 (no copy of it is kept live across the loop)
+#pragma unroll 1
+  for (int q = 0; q < 4; ++q) {  // one hash + one comb body for the four keys
+    if (fixed_sign && (q & 1) == 0) {
+      r.x = prm->pub_s.x;
+      r.y = prm->pub_s.y;
+      ec::fe_set(r.z, 1);
+      r.inf = false;
+    } else {
+      const uint64_t m = fixed_sign ? k0 + (q >> 1) : 2 * k0 + q;
+      uint64_t h[8];
+      key_hash(h, prm, m);
+      const uint64_t kw[4] = {h[0], h[1], h[2], h[3]};
+      ec::scalar_mult_base_jac<W>(r, table, kw);
+    }
+    if (r.inf) {  // k = 0 mod n: keep the shared product invertible, drop the try
+      ec::fe_set(r.z, 1);
+      if (q < 2) ok0 = false;
+      else ok1 = false;
+    }
+    if (q < 3) stash_put(st, q, lane, r.x, r.y);
+    fe_sel(z0, q == 0, r.z, z0);
+    fe_sel(z1, q == 1, r.z, z1);
+    fe_sel(z2, q == 2, r.z, z2);
+  }
+  const fe& x3 = r.x;
+  const fe& y3 = r.y;
+  const fe& z3 = r.z;
+  fe za, zb, inv, ia, ib;
+  ec::fe_mul(za, z0, z1);
+  ec::fe_mul(zb, z2, z3);
+  ec::fe_mul(inv, za, zb);
+  ec::fe_inv(inv, inv);
+  ec::fe_mul(ia, inv, zb);
+  ec::fe_mul(ib, inv, za);
+#pragma unroll 1
+  for (int t = 1; t >= 0; --t) {  // one affine + hash body for both tries (try B first: key 3 is live)
+    fe it, zs, ze, zis, zie, xs, ys, xe, ye;
+    fe_sel(it, t == 1, ib, ia);
+    fe_sel(zs, t == 1, z2, z0);
+    fe_sel(ze, t == 1, z3, z1);
+    ec::fe_mul(zis, it, ze);
+    ec::fe_mul(zie, it, zs);
+    stash_get(st, 2 * t, lane, xs, ys);
+    if (t == 1) {
+      xe = x3;
+      ye = y3;
+    } else {
+      stash_get(st, 1, lane, xe, ye);
+    }
+    ge ps, pe;
+    to_affine(ps, xs, ys, zis);
+    to_affine(pe, xe, ye, zie);
+    uint32_t rh[5];
+    ripe_of_points(rh, ps, pe);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+      rh1[i] = t == 1 ? rh[i] : rh1[i];
+      rh0[i] = t == 0 ? rh[i] : rh0[i];
+    }
+  }
+}
+#endif  // AR_SINGLE
+
 }  // namespace
 
 // The comb table in two launches.  ar_base_kernel: bases[i] = 2^(W i) * G (affine), one thread per
@@ -206,7 +318,8 @@ __global__ __launch_bounds__(64) void ar_table_kernel(const ge* __restrict__ bas
   ec::gej_to_ge(table[t], acc);
 }
 
-// Search: lane g tries k = start + g (g < count).  best: running minimum k with a hit.
+// Search: lanes try k in [start, start + count), two consecutive tries per lane (try_pair; one per
+// lane when built with -DAR_SINGLE, the A/B baseline).  best: running minimum k with a hit.
 // kResolve: the launch instead reports everything about the single try k = start (keys, public
 // keys, ripe) -- the resolve step, sharing this kernel's code; a separate instantiation so the
 // search never keeps the private-key digests live.
@@ -222,6 +335,20 @@ __global__ __launch_bounds__(64) AR_OCC void ar_search_kernel(const ar_params* _
                                                        unsigned long long* __restrict__ best,
                                                        ar_result* __restrict__ out) {
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+#ifndef AR_SINGLE
+  if (!kResolve) {  // lane g: tries start + 2g and start + 2g + 1 (the second only below start + count)
+    __shared__ uint32_t stash[3 * 16 * kPairLanes];
+    if (2ull * g >= count) return;
+    const uint64_t k0 = start + 2ull * g;
+    if (__hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k0) return;
+    uint32_t rh0[5] = {0, 0, 0, 0, 0}, rh1[5] = {0, 0, 0, 0, 0};
+    bool ok0, ok1;
+    try_pair<W>(prm, table, k0, stash, threadIdx.x, rh0, rh1, ok0, ok1);
+    if (ok0 && prefix_ok(rh0, prm->null_bytes)) atomicMin(best, (unsigned long long)k0);
+    else if (ok1 && 2ull * g + 1 < count && prefix_ok(rh1, prm->null_bytes)) atomicMin(best, (unsigned long long)(k0 + 1));
+    return;
+  }
+#endif
   if (g >= count) return;
   const uint64_t k = start + g;
   if (!kResolve && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k) return;
@@ -300,11 +427,16 @@ hipError_t ar_launch_table(hipStream_t st, ge* table, int wbits) {
 hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, const ge* table, int wbits, uint64_t start,
                             uint32_t count, unsigned long long* best) {
   if (count == 0) return hipSuccess;
+#ifndef AR_SINGLE
+  const uint32_t lanes = (uint32_t)(((uint64_t)count + 1) / 2);  // two tries per lane
+#else
+  const uint32_t lanes = count;
+#endif
   if (wbits == ec::kCombLarge)
-    hipLaunchKernelGGL((ar_search_kernel<false, ec::kCombLarge>), dim3((count + 63) / 64), dim3(64), 0, st, prm, table,
+    hipLaunchKernelGGL((ar_search_kernel<false, ec::kCombLarge>), dim3((lanes + 63) / 64), dim3(64), 0, st, prm, table,
                        start, count, best, (ar_result*)nullptr);
   else
-    hipLaunchKernelGGL((ar_search_kernel<false, ec::kCombSmall>), dim3((count + 63) / 64), dim3(64), 0, st, prm, table,
+    hipLaunchKernelGGL((ar_search_kernel<false, ec::kCombSmall>), dim3((lanes + 63) / 64), dim3(64), 0, st, prm, table,
                        start, count, best, (ar_result*)nullptr);
   return hipGetLastError();
 }
