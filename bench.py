@@ -45,11 +45,11 @@ PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
 BASELINE_MD_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
 #: issued instructions per trial of bm_search_kernel (tools/isa_census.py on the gfx950 ISA) and
 #: their measured issue rates, lane-ops/clk/CU (tools/ubench_valu.hip, profiles/r01_ubench_valu.json).
-#: v_alignbit_b32, v_lshl_add_u64 and v_bitop3_b32 have no full-rate encoding, so the trial's
-#: instruction mix, not PEAK_TOPS, is the ceiling this kernel can reach.
-ISA_MIX = {'v_alignbit_b32': (3041, 63.2), 'v_bitop3_b32': (1722, 76.6), 'v_lshl_add_u64': (1434, 63.1),
-           'v_lshrrev_b32': (229, 117.8), 'other': (50, 117.8)}
-#: CU-clocks per trial = sum(count / rate); x 256 CUs -> trials per clock of the chip
+#: v_alignbit_b32, v_lshl_add_u64, v_lshrrev_b64 and v_bitop3_b32 have no full-rate encoding, so the
+#: trial's instruction mix, not PEAK_TOPS, is the ceiling this kernel can reach.  (SHR64 is one
+#: v_lshrrev_b64 since r01's last kernel revision; it was v_alignbit_b32 + v_lshrrev_b32 before.)
+ISA_MIX = {'v_alignbit_b32': (2812, 63.2), 'v_bitop3_b32': (1738, 76.6), 'v_lshl_add_u64': (1435, 63.1),
+           'v_lshrrev_b64': (237, 63.6), 'other': (59, 117.8)}
 ISSUE_CLK_PER_TRIAL_PER_CU = sum(c / r for c, r in ISA_MIX.values())
 
 

@@ -1,0 +1,68 @@
+// bmpow_trials.hip -- the small trial kernels beside the search (gfx950): bm_resolve_kernel
+// (winning trial values after a step) and bm_trials_kernel (trial values of arbitrary nonces, the
+// parity probe).  A translation unit of their own, so scheduler and flag experiments on the search
+// kernel (tools/cmp_variants.sh) never touch them -- the iterative-ILP scheduler, for one, crashes
+// the register allocator on trial_ool (ROCm 7.2 clang) once SHR64 is an inline-asm v_lshrrev_b64.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "bmpow_kernels.h"
+#include "sha512_dev.h"
+
+using namespace bm;
+
+// Out-of-line trial for the small kernels (resolve, trials): one compiled copy of the ~6,500-
+// instruction body instead of one inlined per kernel (the search kernel keeps its own inline
+// copy, with the per-object words hoisted out of its nonce loop).
+__device__ __noinline__ uint64_t trial_ool(uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3, uint64_t w4,
+                                           uint64_t w5, uint64_t w6, uint64_t w7, uint64_t nonce) {
+  const uint64_t ihw[8] = {w0, w1, w2, w3, w4, w5, w6, w7};
+  return trial_of(ihw, nonce);
+}
+
+__device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce) {
+  return trial_ool(o->w[0], o->w[1], o->w[2], o->w[3], o->w[4], o->w[5], o->w[6], o->w[7], nonce);
+}
+
+// For each launched item whose object has a hit, recompute the trial value at the winning
+// nonce (one thread per item).  res[k] = {nonce, trial} or {UINT64_MAX, 0}.
+__global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
+                                  uint32_t nitems, const unsigned long long* __restrict__ best,
+                                  bm_result* __restrict__ res) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= nitems) return;
+  const uint32_t obj = items[k].obj;
+  const uint64_t n = best[obj];
+  bm_result r;
+  r.nonce = n;
+  r.trial = 0;
+  if (n != ~0ULL) r.trial = trial_obj(objs + obj, n);
+  res[k] = r;
+}
+
+// Trial values for an arbitrary list of nonces of one object (parity probe / verification).
+__global__ __launch_bounds__(BM_BLOCK) void bm_trials_kernel(const bm_obj* __restrict__ obj,
+                                                             const uint64_t* __restrict__ nonces,
+                                                             uint64_t n, uint64_t* __restrict__ out) {
+  const uint64_t k = (uint64_t)blockIdx.x * BM_BLOCK + threadIdx.x;
+  if (k >= n) return;
+  out[k] = trial_obj(obj, nonces[k]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Launch wrappers (C++ linkage, used by bmpow_host.hip).
+// ---------------------------------------------------------------------------------------
+hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
+                             const unsigned long long* best, bm_result* res) {
+  const uint32_t bs = 64;
+  hipLaunchKernelGGL(bm_resolve_kernel, dim3((nitems + bs - 1) / bs), dim3(bs), 0, st, objs, items, nitems,
+                     best, res);
+  return hipGetLastError();
+}
+
+hipError_t bm_launch_trials(hipStream_t st, const bm_obj* obj, const uint64_t* nonces, uint64_t n,
+                            uint64_t* out) {
+  const uint64_t nb = (n + BM_BLOCK - 1) / BM_BLOCK;
+  hipLaunchKernelGGL(bm_trials_kernel, dim3((uint32_t)nb), dim3(BM_BLOCK), 0, st, obj, nonces, n, out);
+  return hipGetLastError();
+}

@@ -68,11 +68,20 @@ BM_DEV uint64_t rotr(uint64_t x) {
   }
 }
 
+// SHR64 (sigma0/sigma1's third term) as ONE v_lshrrev_b64: the same half rate as v_alignbit_b32
+// (63.6 vs 63.2 lane-ops/clk/CU, tools/ubench_valu.hip), replacing the alignbit + v_lshrrev_b32
+// pair LLVM selects for x >> N.  Inline asm because the backend always splits the 64-bit shift.
 template <int N>
 BM_DEV uint64_t shr(uint64_t x) {
   static_assert(N > 0 && N < 32, "shift");
+#ifndef BM_SHR_SPLIT
+  uint64_t r;
+  asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(N), "v"(x));
+  return r;
+#else
   const uint32_t l = lo32(x), h = hi32(x);
   return mk64(__builtin_amdgcn_alignbit(h, l, N), h >> N);
+#endif
 }
 
 // ---- 3-input bitwise functions as one v_bitop3_b32 per 32-bit half ----
