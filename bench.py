@@ -51,8 +51,8 @@ BASELINE_MD_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
 #: v_bitop3_b32 at 81.0: its effective rate between half-rate VOP3 ops, from the alternating
 #: alignbit/bitop3 stream of tools/ubench_banks (71.0 lane-ops/clk/CU per instruction,
 #: profiles/r01_ubench_coissue.json: 2 / 71.0 - 1 / 63.2 = 1 / 81.0); alone it co-issues at ~122.
-ISA_MIX = {'v_alignbit_b32': (2812, 63.2), 'v_bitop3_b32': (1738, 81.0), 'v_lshl_add_u64': (1435, 63.1),
-           'v_lshrrev_b64': (237, 63.6), 'other': (59, 117.8)}
+ISA_MIX = {'v_alignbit_b32': (2788, 63.2), 'v_bitop3_b32': (1716, 81.0), 'v_lshl_add_u64': (1420, 63.1),
+           'v_lshrrev_b64': (226, 63.6), 'other': (46, 117.8)}
 ISSUE_CLK_PER_TRIAL_PER_CU = sum(c / r for c, r in ISA_MIX.values())
 
 

@@ -71,17 +71,20 @@ BM_DEV uint64_t rotr(uint64_t x) {
 // SHR64 (sigma0/sigma1's third term) as ONE v_lshrrev_b64: the same half rate as v_alignbit_b32
 // (63.6 vs 63.2 lane-ops/clk/CU, tools/ubench_valu.hip), replacing the alignbit + v_lshrrev_b32
 // pair LLVM selects for x >> N.  Inline asm because the backend always splits the 64-bit shift.
-template <int N>
+// kSplit: the builtin form, for the sigma terms of per-object (wave-uniform) words, which LICM must
+// be able to hoist out of the nonce loop -- it never hoists the asm.
+template <int N, bool kSplit = false>
 BM_DEV uint64_t shr(uint64_t x) {
   static_assert(N > 0 && N < 32, "shift");
 #ifndef BM_SHR_SPLIT
-  uint64_t r;
-  asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(N), "v"(x));
-  return r;
-#else
+  if constexpr (!kSplit) {
+    uint64_t r;
+    asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(N), "v"(x));
+    return r;
+  }
+#endif
   const uint32_t l = lo32(x), h = hi32(x);
   return mk64(__builtin_amdgcn_alignbit(h, l, N), h >> N);
-#endif
 }
 
 // ---- 3-input bitwise functions as one v_bitop3_b32 per 32-bit half ----
@@ -108,23 +111,30 @@ BM_DEV uint64_t opaque(uint64_t x) {
   return x;
 }
 
-template <uint8_t LUT>
+// kHoist: a per-object (wave-uniform) value LICM hoists out of the nonce loop -- no opaque barrier,
+// which would pin a register copy of it inside the loop.
+template <uint8_t LUT, bool kHoist = false>
 BM_DEV uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
-  return opaque(mk64(bitop3<LUT>(lo32(a), lo32(b), lo32(c)), bitop3<LUT>(hi32(a), hi32(b), hi32(c))));
+  const uint64_t r = mk64(bitop3<LUT>(lo32(a), lo32(b), lo32(c)), bitop3<LUT>(hi32(a), hi32(b), hi32(c)));
+  if constexpr (kHoist) return r;
+  return opaque(r);
 }
 
-BM_DEV uint64_t xor3(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0x96>(a, b, c); }
+template <bool kHoist = false>
+BM_DEV uint64_t xor3(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0x96, kHoist>(a, b, c); }
 
 // FIPS 180-4 4.1.3 functions.
 BM_DEV uint64_t Sig0(uint64_t a) { return xor3(rotr<28>(a), rotr<34>(a), rotr<39>(a)); }
 BM_DEV uint64_t Sig1(uint64_t e) { return xor3(rotr<14>(e), rotr<18>(e), rotr<41>(e)); }
+template <bool kSplit = false>
 BM_DEV uint64_t sig0(uint64_t w) {
   if (__builtin_constant_p(w)) return (w >> 1 | w << 63) ^ (w >> 8 | w << 56) ^ (w >> 7);
-  return xor3(rotr<1>(w), rotr<8>(w), shr<7>(w));
+  return xor3<kSplit>(rotr<1>(w), rotr<8>(w), shr<7, kSplit>(w));
 }
+template <bool kSplit = false>
 BM_DEV uint64_t sig1(uint64_t w) {
   if (__builtin_constant_p(w)) return (w >> 19 | w << 45) ^ (w >> 61 | w << 3) ^ (w >> 6);
-  return xor3(rotr<19>(w), rotr<61>(w), shr<6>(w));
+  return xor3<kSplit>(rotr<19>(w), rotr<61>(w), shr<6, kSplit>(w));
 }
 BM_DEV uint64_t Ch(uint64_t e, uint64_t f, uint64_t g) { return bitop3_64<0xCA>(e, f, g); }
 BM_DEV uint64_t Maj(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0xE8>(a, b, c); }
@@ -151,26 +161,31 @@ constexpr uint64_t PAD = 0x8000000000000000ULL;
 // index below is a compile-time constant after template expansion, so s[] and w[] live in
 // VGPR/SGPR pairs (verified: no scratch in the ISA).
 // ---------------------------------------------------------------------------------------
-template <int T>
+// kTrial1: block 1 of the trial, whose W1..W8 are the object's (wave-uniform) initialHash words: the
+// sigma0 of W1..W8 (T = 16..23) and the sigma1 of the uniform W17, W19, W21 (T = 19, 21, 23) take the
+// hoistable builtin form.
+template <int T, bool kTrial1 = false>
 BM_DEV void round_step(uint64_t (&s)[8], uint64_t (&w)[16]) {
   constexpr int A = (8 - (T & 7)) & 7;
   constexpr int B = (A + 1) & 7, C = (A + 2) & 7, D = (A + 3) & 7;
   constexpr int E = (A + 4) & 7, F = (A + 5) & 7, G = (A + 6) & 7, H = (A + 7) & 7;
   if constexpr (T >= 16) {
+    constexpr bool kU0 = kTrial1 && T <= 23;
+    constexpr bool kU1 = kTrial1 && (T == 19 || T == 21 || T == 23);
     // grouped so the terms that do not depend on the nonce (per-object or compile-time)
     // are summed first and hoisted out of the nonce loop by LICM
-    w[T & 15] = (w[(T - 7) & 15] + sig0(w[(T - 15) & 15]) + w[(T - 16) & 15]) + sig1(w[(T - 2) & 15]);
+    w[T & 15] = (w[(T - 7) & 15] + sig0<kU0>(w[(T - 15) & 15]) + w[(T - 16) & 15]) + sig1<kU1>(w[(T - 2) & 15]);
   }
   const uint64_t t1 = s[H] + Sig1(s[E]) + Ch(s[E], s[F], s[G]) + (K(T) + w[T & 15]);
   s[D] += t1;
   s[H] = t1 + Sig0(s[A]) + Maj(s[A], s[B], s[C]);
 }
 
-template <int T, int END>
+template <int T, int END, bool kTrial1 = false>
 BM_DEV void rounds(uint64_t (&s)[8], uint64_t (&w)[16]) {
   if constexpr (T < END) {
-    round_step<T>(s, w);
-    rounds<T + 1, END>(s, w);
+    round_step<T, kTrial1>(s, w);
+    rounds<T + 1, END, kTrial1>(s, w);
   }
 }
 
@@ -187,7 +202,7 @@ BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
   w[15] = 72 * 8;
   // state after the folded round 0 (round 1 has A = 7: a=s7 b=s0 c=s1 d=s2 e=s3 f=s4 g=s5 h=s6)
   uint64_t s[8] = {IV(0), IV(1), IV(2), nonce + E1C, IV(4), IV(5), IV(6), nonce + A1C};
-  rounds<1, 80>(s, w);
+  rounds<1, 80, true>(s, w);
   // after 80 rounds A = 0: s[i] holds a..h in order
   uint64_t w2[16];
 #pragma unroll
