@@ -330,11 +330,14 @@ def run_verify_bench(args, dist):
     lib.bmpow_get_stats(ctypes.byref(st))
     # end to end, the way a caller uses it: host buffers in, verdicts out (padding and sorting on
     # the host, PCIe upload, kernel, IEEE-double verdicts) -- reported beside, never as `value`
-    t1 = time.perf_counter()
-    ok = verify.isProofOfWorkSufficient_batch(objs, recvTime=1700000000)
-    e2e = time.perf_counter() - t1
-    assert len(ok) == n
-    return {'e2e_objects_per_s': n / e2e, 'e2e_s': e2e,
+    # (first call: allocates the library's staging and device buffers; later floods reuse them)
+    e2e = []
+    for _ in range(3):
+        t1 = time.perf_counter()
+        ok = verify.isProofOfWorkSufficient_batch(objs, recvTime=1700000000)
+        e2e.append(time.perf_counter() - t1)
+        assert len(ok) == n
+    return {'e2e_objects_per_s': n / min(e2e[1:]), 'e2e_s': min(e2e[1:]), 'e2e_first_s': e2e[0],
             'desc': 'verify: %d received objects (50%% acks, 25%% pubkeys, 25%% msgs 0.5-16 KB), POW of each '
                     '(protocol.isProofOfWorkSufficient hashing) resident in HBM' % n,
             'objects': n * args.steps, 'elapsed': elapsed, 'stats': st, 'payload_bytes': payload_bytes * args.steps}
@@ -353,8 +356,10 @@ def summarize_verify(args, dist, r, lib_version):
         'config': {'workload': r['desc'], 'parallelism': 'object-sharded dp%d' % dist.world, 'lib': lib_version},
         'payload_GBps': round(nbytes / el_max / 1e9, 3),
         'e2e_host_buffers': {'objects_per_s': round(r['e2e_objects_per_s'], 1), 'seconds': round(r['e2e_s'], 3),
-                             'what': 'bmpow_verify_batch from host buffers: pad + sort + PCIe upload + kernel + '
-                                     'verdicts (rank 0)'},
+                             'first_call_seconds': round(r['e2e_first_s'], 3),
+                             'what': 'bmpow_verify_batch_ptrs from host buffers: sort + pad into pinned staging '
+                                     'overlapped with the PCIe upload + kernel + verdicts (rank 0; best of 2 '
+                                     'calls after the first, which allocates the reused buffers)'},
     }
     if st.verify_kernel_ms > 0:
         # algorithmic ops: 4,144 per 128-B payload block (SURVEY 8(d) per-block count) + 8,288 for

@@ -75,6 +75,17 @@ struct Shard {
   // built on first use and shared by the shards of one device (owns_table marks the freeing one)
   ec::ge* d_table[2] = {nullptr, nullptr};
   bool owns_table[2] = {false, false};
+  // one-shot verification (bmpow_verify_batch*, bmpow_pow_values): buffers kept across calls
+  // (grow-only), so a flood pays neither allocation nor first-touch page faults; two pinned
+  // staging chunks let the padding of chunk c+1 overlap the DMA of chunk c
+  uint8_t* h_vstage[2] = {nullptr, nullptr};
+  hipEvent_t ev_vstage[2] = {nullptr, nullptr};
+  uint4* d_vpool = nullptr;
+  size_t d_vpool_cap = 0;
+  bv_obj* d_vobj = nullptr;
+  uint64_t* d_vpow = nullptr;
+  uint64_t* h_vpow = nullptr;  // pinned
+  size_t vobj_cap = 0;
 };
 
 std::vector<Shard> g_shards;
@@ -110,6 +121,14 @@ void free_shard(Shard& s) {
   if (s.h_trials) (void)hipHostFree(s.h_trials);
   for (int c = 0; c < 2; ++c)
     if (s.d_table[c] && s.owns_table[c]) (void)hipFree(s.d_table[c]);
+  for (int c = 0; c < 2; ++c) {
+    if (s.h_vstage[c]) (void)hipHostFree(s.h_vstage[c]);
+    if (s.ev_vstage[c]) (void)hipEventDestroy(s.ev_vstage[c]);
+  }
+  if (s.d_vpool) (void)hipFree(s.d_vpool);
+  if (s.d_vobj) (void)hipFree(s.d_vobj);
+  if (s.d_vpow) (void)hipFree(s.d_vpow);
+  if (s.h_vpow) (void)hipHostFree(s.h_vpow);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
   if (s.stream) (void)hipStreamDestroy(s.stream);
@@ -438,6 +457,7 @@ struct bmpow_vbatch {
     uint4* d_pool = nullptr;
     uint64_t* d_pow = nullptr;
     uint64_t* h_pow = nullptr;  // pinned
+    bool borrowed = false;      // buffers belong to the shard (one-shot path)
   };
   std::vector<Part> parts;
   uint64_t blocks = 0;
@@ -473,6 +493,7 @@ void pad_into(const uint8_t* msg, uint64_t m, uint8_t* dst, uint64_t nblk) {
 
 void vbatch_free(bmpow_vbatch* vb) {
   for (auto& pt : vb->parts) {
+    if (pt.borrowed) continue;
     if (pt.shard < g_shards.size()) (void)hipSetDevice(g_shards[pt.shard].dev);
     if (pt.d_obj) (void)hipFree(pt.d_obj);
     if (pt.d_pool) (void)hipFree(pt.d_pool);
@@ -482,7 +503,115 @@ void vbatch_free(bmpow_vbatch* vb) {
   vb->parts.clear();
 }
 
-int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs) {
+// Pad objects [j0, j1) of a part (sorted order) into dst (their blocks from blk0 on), over up to 16
+// host threads: a memory-bound copy of every payload.
+void pad_range(const std::vector<Span>& objs, const bmpow_vbatch::Part& pt, const std::vector<bv_obj>& ho,
+               size_t j0, size_t j1, uint64_t blk0, uint8_t* dst) {
+  if (j1 <= j0) return;
+  const size_t m = j1 - j0;
+  const uint64_t bytes = (uint64_t)(ho[j1 - 1].blk + ho[j1 - 1].nblk - ho[j0].blk) * 128;
+  // a thread per ~2 MB (and per >= 64 objects), at most 16
+  const size_t nth = std::max<size_t>(
+      1, std::min<size_t>({16, std::thread::hardware_concurrency(), bytes / (2u << 20) + 1, m / 64 + 1}));
+  auto work = [&](size_t t) {
+    for (size_t j = j0 + m * t / nth; j < j0 + m * (t + 1) / nth; ++j) {
+      const Span& sp = objs[pt.orig[j]];
+      pad_into(sp.p + 8, sp.len - 8, dst + (uint64_t)(ho[j].blk - blk0) * 128, ho[j].nblk);
+    }
+  };
+  if (nth == 1) return work(0);
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nth; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+}
+
+template <typename T>
+int grow_device(T*& p, size_t& cap, size_t need) {
+  if (need <= cap && p) return 0;
+  if (p) (void)hipFree(p);
+  p = nullptr;
+  cap = 0;
+  HIPTRY(hipMalloc(&p, need));
+  cap = need;
+  return 0;
+}
+
+constexpr uint64_t kVStageBytes = 64ull << 20;  // pinned staging chunk (x2 per shard)
+
+// One-shot path: the part's pool goes up through the shard's two pinned staging chunks, padding of
+// chunk c+1 overlapping the DMA of chunk c; device buffers are the shard's, reused across calls.
+int vbatch_upload_transient(bmpow_vbatch::Part& pt, const std::vector<Span>& objs, const std::vector<bv_obj>& ho,
+                            const std::vector<uint32_t>& nblk) {
+  Shard& sh = g_shards[pt.shard];
+  const size_t m = pt.orig.size();
+  if (m > sh.vobj_cap || !sh.d_vobj) {
+    if (sh.d_vobj) (void)hipFree(sh.d_vobj);
+    if (sh.d_vpow) (void)hipFree(sh.d_vpow);
+    if (sh.h_vpow) (void)hipHostFree(sh.h_vpow);
+    sh.d_vobj = nullptr;
+    sh.d_vpow = nullptr;
+    sh.h_vpow = nullptr;
+    sh.vobj_cap = 0;
+    const size_t cap = std::max<size_t>(m, 4096);
+    HIPTRY(hipMalloc(&sh.d_vobj, cap * sizeof(bv_obj)));
+    HIPTRY(hipMalloc(&sh.d_vpow, cap * sizeof(uint64_t)));
+    HIPTRY(hipHostMalloc(&sh.h_vpow, cap * sizeof(uint64_t), hipHostMallocDefault));
+    sh.vobj_cap = cap;
+  }
+  {
+    size_t cap = sh.d_vpool_cap;
+    int rc = grow_device(sh.d_vpool, cap, std::max<size_t>(pt.blocks * 128, 16));
+    sh.d_vpool_cap = cap;
+    if (rc < 0) return rc;
+  }
+  for (int c = 0; c < 2; ++c) {
+    if (!sh.h_vstage[c]) HIPTRY(hipHostMalloc(&sh.h_vstage[c], kVStageBytes, hipHostMallocDefault));
+    if (!sh.ev_vstage[c]) HIPTRY(hipEventCreateWithFlags(&sh.ev_vstage[c], hipEventDisableTiming));
+  }
+  pt.d_obj = sh.d_vobj;
+  pt.d_pool = sh.d_vpool;
+  pt.d_pow = sh.d_vpow;
+  pt.h_pow = sh.h_vpow;
+  pt.borrowed = true;
+  HIPTRY(hipMemcpy(pt.d_obj, ho.data(), m * sizeof(bv_obj), hipMemcpyHostToDevice));
+  // chunks of whole objects; an object larger than a chunk is padded in pageable memory on its own
+  size_t j = 0;
+  int c = 0;
+  bool used[2] = {false, false};
+  std::unique_ptr<uint8_t[]> big;
+  while (j < m) {
+    const uint64_t blk0 = ho[j].blk;
+    size_t j1 = j;
+    uint64_t bytes = 0;
+    while (j1 < m && (j1 == j || bytes + (uint64_t)nblk[pt.orig[j1]] * 128 <= kVStageBytes)) {
+      bytes += (uint64_t)nblk[pt.orig[j1]] * 128;
+      ++j1;
+    }
+    uint8_t* dst;
+    if (bytes > kVStageBytes) {
+      big.reset(new uint8_t[bytes]);
+      dst = big.get();
+    } else {
+      if (used[c]) HIPTRY(hipEventSynchronize(sh.ev_vstage[c]));  // its previous DMA is done
+      dst = sh.h_vstage[c];
+    }
+    pad_range(objs, pt, ho, j, j1, blk0, dst);
+    HIPTRY(hipMemcpyAsync((uint8_t*)pt.d_pool + blk0 * 128, dst, bytes, hipMemcpyHostToDevice, sh.stream));
+    if (dst == big.get()) {
+      HIPTRY(hipStreamSynchronize(sh.stream));
+      big.reset();
+    } else {
+      HIPTRY(hipEventRecord(sh.ev_vstage[c], sh.stream));
+      used[c] = true;
+      c ^= 1;
+    }
+    j = j1;
+  }
+  return 0;
+}
+
+int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs, bool transient = false) {
   const size_t n = objs.size();
   if (n > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many objects");
   vb->n = n;
@@ -527,18 +656,14 @@ int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs) {
       ho[j].nonce = load_be64(objs[pt.orig[j]].p);
       blk += nb;
     }
+    if (transient) {
+      const int rc = vbatch_upload_transient(pt, objs, ho, nblk);
+      if (rc < 0) return rc;
+      continue;
+    }
     // padding is a memory-bound copy of every payload: spread it over host threads
     std::unique_ptr<uint8_t[]> pool(new uint8_t[pt.blocks * 128]);  // pad_into writes every byte
-    const size_t nth = std::max<size_t>(1, std::min<size_t>({16, std::thread::hardware_concurrency(), m / 4096 + 1}));
-    std::vector<std::thread> th;
-    for (size_t t = 0; t < nth; ++t)
-      th.emplace_back([&, t] {
-        for (size_t j = m * t / nth; j < m * (t + 1) / nth; ++j) {
-          const Span& sp = objs[pt.orig[j]];
-          pad_into(sp.p + 8, sp.len - 8, pool.get() + (uint64_t)ho[j].blk * 128, ho[j].nblk);
-        }
-      });
-    for (auto& x : th) x.join();
+    pad_range(objs, pt, ho, 0, m, 0, pool.get());
     HIPTRY(hipMalloc(&pt.d_obj, m * sizeof(bv_obj)));
     HIPTRY(hipMalloc(&pt.d_pool, std::max<size_t>(pt.blocks * 128, 16)));
     HIPTRY(hipMalloc(&pt.d_pow, m * sizeof(uint64_t)));
@@ -1123,7 +1248,7 @@ int bmpow_pow_values(size_t n, const uint8_t* objs, const uint64_t* offsets, uin
   rc = spans_from(n, objs, offsets, spans);
   if (rc < 0) return rc;
   bmpow_vbatch vb;
-  rc = vbatch_build(&vb, spans);
+  rc = vbatch_build(&vb, spans, true);
   if (rc == 0) rc = vbatch_run_locked(&vb, pow_out);
   vbatch_free(&vb);
   return rc;
@@ -1150,7 +1275,7 @@ static int verify_spans_locked(size_t n, const uint8_t* const* ptrs, const uint6
   std::vector<uint64_t> pow(spans.size());
   if (!spans.empty()) {
     bmpow_vbatch vb;
-    int rc = vbatch_build(&vb, spans);
+    int rc = vbatch_build(&vb, spans, true);
     if (rc == 0) rc = vbatch_run_locked(&vb, pow.data());
     vbatch_free(&vb);
     if (rc < 0) return rc;

@@ -29,7 +29,9 @@ def _pack(objects):
 
 
 def _per_object(value, n, dtype):
-    arr = np.asarray(value if np.ndim(value) else [value] * n, dtype=dtype)
+    if not np.ndim(value):
+        return np.full(n, value, dtype=dtype)
+    arr = np.asarray(value, dtype=dtype)
     if arr.shape != (n,):
         raise ValueError('expected a scalar or %d values' % n)
     return np.ascontiguousarray(arr)
@@ -83,7 +85,9 @@ def isProofOfWorkSufficient_batch(objects, nonceTrialsPerByte=0, payloadLengthEx
     reference).  An object shorter than 16 bytes raises ``struct.error`` as the reference's
     ``unpack('>Q', data[8:16])`` does.  The objects are read where they lie
     (``bmpow_verify_batch_ptrs``): no concatenation on the host."""
-    objs = [o if type(o) is bytes else bytes(o) for o in objects]
+    objs = objects if type(objects) is list else list(objects)
+    if set(map(type, objs)) - {bytes}:  # bytearray / memoryview: one bytes copy each
+        objs = [o if type(o) is bytes else bytes(o) for o in objs]
     n = len(objs)
     if n == 0:
         return []
@@ -102,7 +106,7 @@ def isProofOfWorkSufficient_batch(objects, nonceTrialsPerByte=0, payloadLengthEx
     del objs  # the pointers were valid for the call
     if (ok == 2).any():
         raise struct.error('unpack requires a buffer of 8 bytes')
-    return [bool(v) for v in ok]
+    return ok.astype(bool).tolist()
 
 
 class VerifyBatch(object):
