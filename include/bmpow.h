@@ -192,6 +192,13 @@ typedef struct bmpow_address {
  * 65 zero bytes.  Returns 0 or < 0. */
 BMPOW_API int bmpow_pubkeys(size_t n, const uint8_t *privkeys, uint8_t *pubkeys_out);
 
+/* Field-arithmetic probe for the tests (no reference counterpart): out[i] = op(a[i], b[i]) mod
+ * p = 2^256 - 2^32 - 977 on the device, operands as 8 little-endian 32-bit limbs each (any value
+ * below 2^256, reduced or not).  op: 0 a+b, 1 a-b, 2 a*b, 3 a^2, 4 canonical form of a, 5 a^-1
+ * (0 for a = 0 mod p), 6 (a = 0 mod p) in limb 0.  Results of 0..3 are weakly reduced (< 2^256,
+ * congruent), of 4..5 canonical (< p).  Returns 0 or < 0. */
+BMPOW_API int bmpow_fe_probe(int op, size_t n, const uint32_t *a, const uint32_t *b, uint32_t *out);
+
 /* Deterministic addresses (createDeterministicAddresses / getDeterministicAddress / chans):
  * privSigning = SHA512(passphrase || varint(2k))[:32], privEncryption = SHA512(passphrase ||
  * varint(2k+1))[:32], k in [start, start + max_tries).  Returns BMPOW_FOUND (out filled) with

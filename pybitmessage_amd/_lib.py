@@ -93,6 +93,7 @@ SIGNATURES = [
     ('bmpow_vbatch_run', ctypes.c_int, [_vp, _p64]),
     ('bmpow_vbatch_destroy', None, [_vp]),
     ('bmpow_pubkeys', ctypes.c_int, [ctypes.c_size_t, ctypes.c_char_p, ctypes.c_char_p]),
+    ('bmpow_fe_probe', ctypes.c_int, [ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     ('bmpow_address_search', ctypes.c_int,
      [ctypes.c_char_p, ctypes.c_size_t, _u64, _u64, ctypes.c_int, ctypes.POINTER(BmpowAddress)]),
     ('bmpow_address_search_random', ctypes.c_int,

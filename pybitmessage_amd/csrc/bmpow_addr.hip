@@ -197,13 +197,15 @@ BM_DEV void stash_get(const uint32_t* st, int slot, uint32_t lane, fe& x, fe& y)
   }
 }
 
-// Jacobian (X, Y) with known Z^-1 -> affine
+// Jacobian (X, Y) with known Z^-1 -> affine (canonical)
 BM_DEV void to_affine(ge& r, const fe& x, const fe& y, const fe& zi) {
   fe t;
   ec::fe_sqr(t, zi);
   ec::fe_mul(r.x, x, t);
   ec::fe_mul(t, t, zi);
   ec::fe_mul(r.y, y, t);
+  ec::fe_normalize(r.x, r.x);
+  ec::fe_normalize(r.y, r.y);
 }
 
 // ripes of tries k0 (rh[0]) and k0 + 1 (rh[1]); ok[t] false when a key of try t is 0 mod n
@@ -384,6 +386,29 @@ __global__ __launch_bounds__(64) void ar_pubkey_kernel(const uint64_t* __restric
   pubs[g] = r;
 }
 
+// Field-arithmetic probe (tests only): out[i] = op(a[i], b[i]) on arbitrary 256-bit inputs, so the
+// weak-reduction bounds are checked at the edges (values >= p, near 2^256) that random keys never
+// reach.  op: 0 add, 1 sub, 2 mul, 3 sqr, 4 normalize, 5 inv, 6 is_zero (out limb 0 = 0/1).
+__global__ __launch_bounds__(64) void ar_fe_probe_kernel(int op, const fe* __restrict__ a, const fe* __restrict__ b,
+                                                         fe* __restrict__ out, uint32_t n) {
+  const uint32_t g = blockIdx.x * 64 + threadIdx.x;
+  if (g >= n) return;
+  const fe x = a[g], y = b[g];
+  fe r;
+  ec::fe_set(r, 0);
+  switch (op) {
+    case 0: ec::fe_add(r, x, y); break;
+    case 1: ec::fe_sub(r, x, y); break;
+    case 2: ec::fe_mul(r, x, y); break;
+    case 3: ec::fe_sqr(r, x); break;
+    case 4: ec::fe_normalize(r, x); break;
+    case 5: ec::fe_inv(r, x); break;
+    case 6: ec::fe_set(r, ec::fe_is_zero(x) ? 1u : 0u); break;
+    default: break;
+  }
+  out[g] = r;
+}
+
 // Midstate of the passphrase's first nfull 128-byte blocks (one thread).
 __global__ void ar_midstate_kernel(const uint8_t* __restrict__ pass, uint64_t nfull, uint64_t* __restrict__ mid) {
   if (blockIdx.x != 0 || threadIdx.x != 0) return;
@@ -458,6 +483,12 @@ hipError_t ar_launch_pubkeys(hipStream_t st, const uint64_t* privs, uint32_t n, 
                              uint32_t* ok) {
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(ar_pubkey_kernel, dim3((n + 63) / 64), dim3(64), 0, st, privs, n, table, pubs, ok);
+  return hipGetLastError();
+}
+
+hipError_t ar_launch_fe_probe(hipStream_t st, int op, const ec::fe* a, const ec::fe* b, ec::fe* out, uint32_t n) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(ar_fe_probe_kernel, dim3((n + 63) / 64), dim3(64), 0, st, op, a, b, out, n);
   return hipGetLastError();
 }
 

@@ -1364,6 +1364,33 @@ int bmpow_pubkeys(size_t n, const uint8_t* privkeys, uint8_t* pubkeys_out) {
   return 0;
 }
 
+int bmpow_fe_probe(int op, size_t n, const uint32_t* a, const uint32_t* b, uint32_t* out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (n == 0) return 0;
+  if (!a || !b || !out) return set_err(BMPOW_E_ARG, "null pointer");
+  if (op < 0 || op > 6) return set_err(BMPOW_E_ARG, "fe probe op must be 0..6");
+  if (n > (1u << 24)) return set_err(BMPOW_E_ARG, "too many operands");
+  Shard& sh = g_shards[0];
+  const size_t bytes = n * sizeof(ec::fe);
+  ec::fe *d_a = nullptr, *d_b = nullptr, *d_o = nullptr;
+  HIPTRY(hipSetDevice(sh.dev));
+  hipError_t e = hipMalloc(&d_a, bytes);
+  if (e == hipSuccess) e = hipMalloc(&d_b, bytes);
+  if (e == hipSuccess) e = hipMalloc(&d_o, bytes);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_a, a, bytes, hipMemcpyHostToDevice, sh.stream);
+  if (e == hipSuccess) e = hipMemcpyAsync(d_b, b, bytes, hipMemcpyHostToDevice, sh.stream);
+  if (e == hipSuccess) e = ar_launch_fe_probe(sh.stream, op, d_a, d_b, d_o, (uint32_t)n);
+  if (e == hipSuccess) e = hipMemcpyAsync(out, d_o, bytes, hipMemcpyDeviceToHost, sh.stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
+  (void)hipFree(d_a);
+  (void)hipFree(d_b);
+  (void)hipFree(d_o);
+  if (e != hipSuccess) return set_err(BMPOW_E_HIP, std::string("bmpow_fe_probe: ") + hipGetErrorString(e));
+  return 0;
+}
+
 int bmpow_address_search(const uint8_t* passphrase, size_t len, uint64_t start, uint64_t max_tries, int null_bytes,
                          bmpow_address* out) {
   std::lock_guard<std::mutex> lk(g_mu);

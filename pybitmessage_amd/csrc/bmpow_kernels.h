@@ -85,4 +85,5 @@ hipError_t ar_launch_resolve(hipStream_t st, const ar_params* prm, const ec::ge*
                              ar_result* out);
 hipError_t ar_launch_pubkeys(hipStream_t st, const uint64_t* privs, uint32_t n, const ec::ge* table, ec::ge* pubs,
                              uint32_t* ok);
+hipError_t ar_launch_fe_probe(hipStream_t st, int op, const ec::fe* a, const ec::fe* b, ec::fe* out, uint32_t n);
 hipError_t ar_launch_midstate(hipStream_t st, const uint8_t* pass, uint64_t nfull, uint64_t* mid);

@@ -2,9 +2,12 @@
 //
 // The reference turns a private key into a public key with OpenSSL EC_POINT_mul on secp256k1
 // (src/highlevelcrypto.py:111-140, pointMult).  Here one lane computes k*G for its own k:
-//   * field elements mod p = 2^256 - 2^32 - 977 as 8 x 32-bit little-endian limbs, always fully
-//     reduced; products by v_mad_u64_u32 with its carry-out (product scanning, 2 instructions per
-//     32x32 product), reduction by 2^256 = 2^32 + 977;
+//   * field elements mod p = 2^256 - 2^32 - 977 as 8 x 32-bit little-endian limbs, WEAKLY reduced:
+//     every fe is some value < 2^256 congruent to the element (so 0 and p both stand for zero);
+//     products by v_mad_u64_u32 with its carry-out (product scanning, 2 instructions per 32x32
+//     product), reduction by 2^256 = 2^32 + 977.  Only affine points (ge: table entries, keys
+//     that get serialized) are canonical (< p): fe_normalize runs once per affine coordinate,
+//     instead of a conditional subtraction at the end of every operation;
 //   * k*G by a fixed-base comb: windows of W = 16 or 24 bits, table[i][v] = v * 2^(W i) * G in
 //     affine coordinates (64 MB or 10.7 GB, built once per device by ar_table_kernel), so one
 //     scalar multiplication is 16 or 11 mixed Jacobian+affine additions and one inversion (shared
@@ -45,11 +48,14 @@ BM_DEV void fe_set(fe& r, uint32_t v) {
   for (int i = 1; i < 8; ++i) r.d[i] = 0;
 }
 
+// a = 0 mod p for a weakly reduced a, i.e. a == 0 or a == p
 BM_DEV bool fe_is_zero(const fe& a) {
-  uint32_t o = 0;
+  uint32_t o = 0, n = (a.d[0] ^ 0xFFFFFC2Fu) | (a.d[1] ^ 0xFFFFFFFEu);
 #pragma unroll
   for (int i = 0; i < 8; ++i) o |= a.d[i];
-  return o == 0;
+#pragma unroll
+  for (int i = 2; i < 8; ++i) n |= ~a.d[i];
+  return o == 0 || n == 0;
 }
 
 // ---- carry primitives ----
@@ -105,32 +111,54 @@ BM_DEV void fe_cond_sub_p(fe& r, const uint32_t (&t)[8], uint32_t carry) {
   for (int i = 0; i < 8; ++i) r.d[i] = ge_p ? u[i] : t[i];
 }
 
+// r = t - p when t >= p (t < 2^256): the canonical form of a weakly reduced element
+BM_DEV void fe_normalize(fe& r, const fe& a) { fe_cond_sub_p(r, a.d, 0u); }
+
+// r = a + b for a, b < 2^256: the carry out of 256 bits folds back as 2^256 = 2^32 + 977.  A
+// second carry needs a + b >= 2^257 - (2^32 + 977); the sum left is then < 2^32 + 977, so the
+// second fold ends in limb 1.
 BM_DEV void fe_add(fe& r, const fe& a, const fe& b) {
   uint32_t t[8], c = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) t[i] = __builtin_addc(a.d[i], b.d[i], c, &c);
-  fe_cond_sub_p(r, t, c);
+  uint32_t m = 0u - c;
+  t[0] = __builtin_addc(t[0], C0 & m, 0u, &c);
+  t[1] = __builtin_addc(t[1], 1u & m, c, &c);
+#pragma unroll
+  for (int i = 2; i < 8; ++i) t[i] = __builtin_addc(t[i], 0u, c, &c);
+  m = 0u - c;
+  r.d[0] = __builtin_addc(t[0], C0 & m, 0u, &c);
+  r.d[1] = t[1] + (1u & m) + c;
+#pragma unroll
+  for (int i = 2; i < 8; ++i) r.d[i] = t[i];
 }
 
+// r = a - b for a, b < 2^256: a borrow out of 256 bits adds p back as - (2^32 + 977) mod 2^256.
+// A second borrow needs the difference t = a - b + 2^256 below 2^32 + 977 (b >= p + a, so b is
+// unreduced); t + 2^256 - (2^32 + 977) is then >= 2^256 - 2^32 - 976, and subtracting
+// 2^32 + 977 once more (= adding 2p in all) stays in limbs 0..1 without a borrow.
 BM_DEV void fe_sub(fe& r, const fe& a, const fe& b) {
   uint32_t t[8], bw = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) t[i] = __builtin_subc(a.d[i], b.d[i], bw, &bw);
-  // on borrow add p back: t + p = t - (2^32 + 977) mod 2^256
-  const uint32_t m = 0u - bw;
-  uint32_t b2;
-  r.d[0] = __builtin_subc(t[0], C0 & m, 0u, &b2);
-  r.d[1] = __builtin_subc(t[1], 1u & m, b2, &b2);
+  uint32_t m = 0u - bw;
+  t[0] = __builtin_subc(t[0], C0 & m, 0u, &bw);
+  t[1] = __builtin_subc(t[1], 1u & m, bw, &bw);
 #pragma unroll
-  for (int i = 2; i < 8; ++i) r.d[i] = __builtin_subc(t[i], 0u, b2, &b2);
+  for (int i = 2; i < 8; ++i) t[i] = __builtin_subc(t[i], 0u, bw, &bw);
+  m = 0u - bw;
+  r.d[0] = __builtin_subc(t[0], C0 & m, 0u, &bw);
+  r.d[1] = t[1] - (1u & m) - bw;  // limb 1 >= 2^32 - 2 here: no borrow into limb 2
+#pragma unroll
+  for (int i = 2; i < 8; ++i) r.d[i] = t[i];
 }
 
 // r = 2a as an addition (cheap, exact)
 BM_DEV void fe_dbl(fe& r, const fe& a) { fe_add(r, a, a); }
 
-// r = p mod p_field for a 512-bit product p (16 limbs): t = L + H * 977 + H * 2^32 column by
-// column (each column < 2^43, no carry out of the accumulator), then the overflow c < 2^33 above
-// 2^256 folded once more the same way, a last 0/1 fold and the conditional subtraction.
+// r = p mod p_field (weakly) for a 512-bit product p (16 limbs): t = L + H * 977 + H * 2^32
+// column by column (each column < 2^43, no carry out of the accumulator), then the overflow
+// c < 2^33 above 2^256 folded once more the same way and a last 0/1 fold.
 BM_DEV void fe_reduce512(fe& r, const uint32_t (&p)[16]) {
   uint32_t t[8];
   uint64_t acc = p[0];
@@ -157,13 +185,15 @@ BM_DEV void fe_reduce512(fe& r, const uint32_t (&p)[16]) {
   c |= c2;  // at most one of them is set
 #pragma unroll
   for (int i = 3; i < 8; ++i) t[i] = __builtin_addc(t[i], 0u, c, &c);
-  // c in {0,1}: one more fold of 2^256 (t is tiny when it happens)
+  // c in {0,1}: one more fold of 2^256.  The value was < 2^256 + 2^66 (t < 2^256 plus
+  // acc (2^32 + 977)), so when c is set t < 2^66: limb 2 < 4 absorbs the last carry, and the
+  // result is weakly reduced (< 2^256) either way -- no conditional subtraction.
   const uint32_t m = 0u - c;
-  t[0] = __builtin_addc(t[0], C0 & m, 0u, &c);
-  t[1] = __builtin_addc(t[1], 1u & m, c, &c);
+  r.d[0] = __builtin_addc(t[0], C0 & m, 0u, &c);
+  r.d[1] = __builtin_addc(t[1], 1u & m, c, &c);
+  r.d[2] = t[2] + c;
 #pragma unroll
-  for (int i = 2; i < 8; ++i) t[i] = __builtin_addc(t[i], 0u, c, &c);
-  fe_cond_sub_p(r, t, c);
+  for (int i = 3; i < 8; ++i) r.d[i] = t[i];
 }
 
 // 512-bit product by columns (product scanning): column k sums a_i b_j over i + j = k.
@@ -217,7 +247,11 @@ BM_DEV void fe_sqr(fe& r, const fe& a) {
 
 // a^-1 mod p (a != 0; a = 0 gives 0).
 #ifndef AR_INV_FERMAT
-BM_DEV void fe_inv(fe& r, const fe& a) { mi::inv_mod_p(r.d, a.d); }
+BM_DEV void fe_inv(fe& r, const fe& a) {  // inv_mod_p wants 0 <= a < p
+  fe n;
+  fe_normalize(n, a);
+  mi::inv_mod_p(r.d, n.d);
+}
 #else
 // a^(p-2) = a^-1 (a != 0).  The exponent is [223 ones][0][22 ones][0000101101]; the 255-
 // squaring / 15-multiplication addition chain (runs of 2^n - 1 ones: 1, 2, 3, 6, 9, 11, 22, 44,
@@ -291,46 +325,69 @@ BM_DEV void gej_double(gej& r, const gej& p) {
   r.inf = false;
 }
 
-// r = p + q with q affine (8M + 3S); handles p = inf, p = q, p = -q.
-BM_DEV void gej_add_ge(gej& r, const gej& p, const ge& q) {
+// r = p + q with q affine (8M + 3S); handles p = inf and p = -q, and p = q by doubling when
+// kDouble -- otherwise it returns false there with r unspecified (the comb's hot loop: its caller
+// redoes the multiplication with the doubling path, so gej_double's registers never weigh on the
+// loop that runs; keeping it inline there pushed the accumulator out to scratch).
+template <bool kDouble>
+BM_DEV bool gej_add_ge_t(gej& r, const gej& p, const ge& q) {
+  // Every path leaves its result in these locals and r is written once at the end: stores to r
+  // from several branches became one store through a phi'd address, which kept the comb's
+  // accumulator in scratch memory instead of registers.
+  fe rx, ry, rz;
+  bool rinf = false, ok = true;
   if (p.inf) {
-    r.x = q.x;
-    r.y = q.y;
-    fe_set(r.z, 1);
-    r.inf = false;
-    return;
-  }
-  fe z1z1, u2, s2, h, rr, hh, hhh, v, t;
-  fe_sqr(z1z1, p.z);
-  fe_mul(u2, q.x, z1z1);
-  fe_mul(s2, q.y, p.z);
-  fe_mul(s2, s2, z1z1);
-  fe_sub(h, u2, p.x);
-  fe_sub(rr, s2, p.y);
-  if (fe_is_zero(h)) {
-    if (fe_is_zero(rr)) {
-      gej_double(r, p);
+    rx = q.x;
+    ry = q.y;
+    fe_set(rz, 1);
+  } else {
+    fe z1z1, u2, s2, h, rr;
+    fe_sqr(z1z1, p.z);
+    fe_mul(u2, q.x, z1z1);
+    fe_mul(s2, q.y, p.z);
+    fe_mul(s2, s2, z1z1);
+    fe_sub(h, u2, p.x);
+    fe_sub(rr, s2, p.y);
+    if (fe_is_zero(h)) {
+      rx = p.x;
+      ry = p.y;
+      rz = p.z;
+      if (!fe_is_zero(rr)) {
+        rinf = true;  // p = -q
+      } else if (kDouble) {
+        gej d;
+        gej_double(d, p);
+        rx = d.x;
+        ry = d.y;
+        rz = d.z;
+        rinf = d.inf;
+      } else {
+        ok = false;  // p = q: the caller takes the doubling pass
+      }
     } else {
-      r.inf = true;
+      fe hh, hhh, v, t;
+      fe_sqr(hh, h);
+      fe_mul(hhh, h, hh);
+      fe_mul(v, p.x, hh);
+      fe_mul(rz, p.z, h);
+      fe_mul(t, p.y, hhh);
+      fe_sqr(rx, rr);
+      fe_sub(rx, rx, hhh);
+      fe_sub(rx, rx, v);
+      fe_sub(rx, rx, v);
+      fe_sub(v, v, rx);
+      fe_mul(v, rr, v);
+      fe_sub(ry, v, t);
     }
-    return;
   }
-  fe_sqr(hh, h);
-  fe_mul(hhh, h, hh);
-  fe_mul(v, p.x, hh);
-  fe_mul(r.z, p.z, h);
-  fe_mul(t, p.y, hhh);  // Y1 * HHH, before r.y overwrites p.y
-  fe x3;
-  fe_sqr(x3, rr);
-  fe_sub(x3, x3, hhh);
-  fe_sub(x3, x3, v);
-  fe_sub(x3, x3, v);
-  fe_sub(v, v, x3);
-  fe_mul(v, rr, v);
-  fe_sub(r.y, v, t);
-  r.x = x3;
-  r.inf = false;
+  r.x = rx;
+  r.y = ry;
+  r.z = rz;
+  r.inf = rinf;
+  return ok;
 }
+
+BM_DEV void gej_add_ge(gej& r, const gej& p, const ge& q) { gej_add_ge_t<true>(r, p, q); }
 
 // Jacobian -> affine (p not at infinity)
 BM_DEV void gej_to_ge(ge& r, const gej& p) {
@@ -340,6 +397,8 @@ BM_DEV void gej_to_ge(ge& r, const gej& p) {
   fe_mul(r.x, p.x, zi2);
   fe_mul(zi2, zi2, zi);
   fe_mul(r.y, p.y, zi2);
+  fe_normalize(r.x, r.x);
+  fe_normalize(r.y, r.y);
 }
 
 // Fixed-base combs: table[i << W | v] = v * 2^(W i) * G (affine), ceil(256 / W) windows, the last
@@ -378,11 +437,12 @@ BM_DEV void shr256_window(uint64_t (&s)[4]) {
 // the low end of a 256-bit shift register (no runtime-indexed register arrays), and the next
 // window's table entry is loaded before the current addition, so the gather's latency hides
 // behind ~2,500 VALU instructions.
-template <int W>
-BM_DEV void scalar_mult_base_jac(gej& acc, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
+template <int W, bool kDouble>
+BM_DEV bool comb_pass(gej& acc, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
   using C = comb<W>;
   uint64_t s[4] = {kw[3], kw[2], kw[1], kw[0]};
   acc.inf = true;
+  bool ok = true;
   uint32_t v = (uint32_t)s[0] & C::kMask;
   ge q = table[v];
 #pragma unroll 1
@@ -391,10 +451,18 @@ BM_DEV void scalar_mult_base_jac(gej& acc, const ge* __restrict__ table, const u
     const uint32_t vn = (uint32_t)s[0] & C::kMask;
     ge qn;
     if (i + 1 < C::kWindows) qn = table[((size_t)(i + 1) << W) | vn];
-    if (v) gej_add_ge(acc, acc, q);
+    if (v) ok = gej_add_ge_t<kDouble>(acc, acc, q) && ok;
     q = qn;
     v = vn;
   }
+  return ok;
+}
+
+template <int W>
+BM_DEV void scalar_mult_base_jac(gej& acc, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
+  // an addition of a point to itself (never seen with random scalars) sends the lane through
+  // the pass with the doubling path
+  if (!comb_pass<W, false>(acc, table, kw)) comb_pass<W, true>(acc, table, kw);
 }
 
 // k*G in affine coordinates; returns false for k*G = infinity.
@@ -424,9 +492,13 @@ BM_DEV void gej_pair_to_ge(ge& ra, ge& rb, const gej& a, const gej& b) {
   fe_mul(rb.x, b.x, t);
   fe_mul(t, t, zib);
   fe_mul(rb.y, b.y, t);
+  fe_normalize(ra.x, ra.x);
+  fe_normalize(ra.y, ra.y);
+  fe_normalize(rb.x, rb.x);
+  fe_normalize(rb.y, rb.y);
 }
 
-// 4 big-endian 64-bit words of a field element (the 32-byte big-endian serialization)
+// 4 big-endian 64-bit words of a canonical field element (the 32-byte big-endian serialization)
 BM_DEV void fe_to_be64(uint64_t (&w)[4], const fe& a) {
   w[0] = ((uint64_t)a.d[7] << 32) | a.d[6];
   w[1] = ((uint64_t)a.d[5] << 32) | a.d[4];

@@ -213,3 +213,54 @@ def test_gpu_random_address_property(gpulib):
     assert ao.ripe_of(a['pubSigningKey'], a['pubEncryptionKey']) == a['ripe']
     assert addressgen.wif(priv_s) == a['privSigningKey'] and addressgen.wif(pe) == a['privEncryptionKey']
     assert lib is not None
+
+
+# ------------------------------------------------------------------ GPU: field arithmetic edges
+P = 2 ** 256 - 2 ** 32 - 977
+C = 2 ** 32 + 977  # 2^256 mod p
+
+
+def _fe_edges():
+    """Operands a random key essentially never produces: unreduced values (>= p), values next to
+    0, p and 2^256, and the ones that make a sum carry twice or a difference borrow twice."""
+    import random
+    rng = random.Random(11)
+    base = [0, 1, 2, 977, C - 1, C, C + 1, 2 ** 32, 2 ** 64 - 1, P - 2, P - 1, P, P + 1, P + C - 1,
+            2 ** 256 - C, 2 ** 256 - C - 1, 2 ** 256 - 2, 2 ** 256 - 1, 2 ** 255, 2 ** 255 - 1]
+    base += [P + rng.randrange(C) for _ in range(8)] + [rng.randrange(2 ** 256) for _ in range(8)]
+    base += [rng.randrange(2 ** 66) for _ in range(4)] + [2 ** 256 - 1 - rng.randrange(2 ** 40) for _ in range(4)]
+    pairs = [(a, b) for a in base for b in base]
+    pairs += [(rng.randrange(2 ** 256), rng.randrange(2 ** 256)) for _ in range(2000)]
+    return pairs
+
+
+def _fe_probe(op, pairs):
+    import ctypes
+    lib = _lib.get()
+    n = len(pairs)
+    limbs = lambda v: [(v >> (32 * i)) & 0xFFFFFFFF for i in range(8)]  # noqa: E731
+    a = (ctypes.c_uint32 * (8 * n))(*[w for x, _ in pairs for w in limbs(x)])
+    b = (ctypes.c_uint32 * (8 * n))(*[w for _, y in pairs for w in limbs(y)])
+    out = (ctypes.c_uint32 * (8 * n))()
+    _lib.check(lib, lib.bmpow_fe_probe(op, n, a, b, out), 'bmpow_fe_probe')
+    return [sum(out[8 * k + i] << (32 * i) for i in range(8)) for k in range(n)]
+
+
+@gpu
+@pytest.mark.parametrize('op', [0, 1, 2, 3])
+def test_gpu_field_ops_weakly_reduced_at_the_edges(gpulib, op):
+    """add/sub/mul/sqr on any inputs < 2^256: result < 2^256 and congruent mod p (weak reduction,
+    secp256k1_dev.h), including the second carry/borrow folds."""
+    pairs = _fe_edges()
+    want = [(a + b, a - b, a * b, a * a)[op] % P for a, b in pairs]
+    got = _fe_probe(op, pairs)
+    bad = [(hex(a), hex(b)) for (a, b), g, w in zip(pairs, got, want) if g >= 2 ** 256 or g % P != w]
+    assert not bad, bad[:4]
+
+
+@gpu
+def test_gpu_field_normalize_inverse_is_zero(gpulib):
+    pairs = _fe_edges()
+    assert _fe_probe(4, pairs) == [a % P for a, _ in pairs]
+    assert _fe_probe(5, pairs) == [pow(a % P, -1, P) if a % P else 0 for a, _ in pairs]
+    assert _fe_probe(6, pairs) == [int(a % P == 0) for a, _ in pairs]

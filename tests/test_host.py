@@ -38,9 +38,9 @@ def test_header_declares_the_boundary():
               'bmpow_set_devices', 'bmpow_last_error', 'BitmessagePOW', 'bmpow_pow_values',
               'bmpow_verify_batch', 'bmpow_pow_sufficient', 'bmpow_vbatch_create', 'bmpow_vbatch_run',
               'bmpow_vbatch_destroy', 'bmpow_pubkeys', 'bmpow_address_search', 'bmpow_address_search_random', 'bmpow_batch_set_pending', 'bmpow_verify_batch_ptrs',
-              'bmpow_addr_set_comb', 'bmpow_addr_last_comb']:
+              'bmpow_addr_set_comb', 'bmpow_addr_last_comb', 'bmpow_fe_probe']:
         assert s in syms
-    assert len(syms) == 35
+    assert len(syms) == 36
 
 
 def test_library_exports_every_declared_symbol(rawlib):
