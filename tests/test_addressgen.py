@@ -264,3 +264,15 @@ def test_gpu_field_normalize_inverse_is_zero(gpulib):
     assert _fe_probe(4, pairs) == [a % P for a, _ in pairs]
     assert _fe_probe(5, pairs) == [pow(a % P, -1, P) if a % P else 0 for a, _ in pairs]
     assert _fe_probe(6, pairs) == [int(a % P == 0) for a, _ in pairs]
+
+
+@gpu
+def test_gpu_pubkeys_at_the_group_order(gpulib):
+    """Scalars around the group order n: k = n sums to the point at infinity inside the comb's
+    last window (P + (-P)), n + 1 is G, n - 1 is -G, and 2^256 - 1 = (2^256 - 1 - n) G."""
+    n = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+    ks = [n, n + 1, n - 1, 2 ** 256 - 1, n - 2 ** 240, 2 ** 240]
+    got = addressgen.pubkeys([k.to_bytes(32, 'big') for k in ks])
+    assert got[0] == bytes(65)
+    for k, g in zip(ks[1:], got[1:]):
+        assert g == ao.point_mult((k % n).to_bytes(32, 'big'))
