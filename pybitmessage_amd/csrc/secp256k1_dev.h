@@ -460,8 +460,10 @@ BM_DEV bool comb_pass(gej& acc, const ge* __restrict__ table, const uint64_t (&k
 
 template <int W>
 BM_DEV void scalar_mult_base_jac(gej& acc, const ge* __restrict__ table, const uint64_t (&kw)[4]) {
-  // an addition of a point to itself (never seen with random scalars) sends the lane through
-  // the pass with the doubling path
+  // An addition of a point to itself would send the lane through the pass with the doubling
+  // path.  For scalars < 2^256 it cannot happen: before window i the sum is (k mod 2^(W i)) G and
+  // the entry is v 2^(W i) G with k mod 2^(W i) < v 2^(W i) < n (W i <= 240).  The opposite
+  // case (sum + entry = n G, only k = n) gives infinity on the fast pass.
   if (!comb_pass<W, false>(acc, table, kw)) comb_pass<W, true>(acc, table, kw);
 }
 

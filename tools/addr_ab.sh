@@ -1,9 +1,10 @@
 # Address-search A/B on one GPU box: the address GPU tests on the default library, then the
 # addrgen bench leg alternating the default library and variants/<name> (ABAB, same box).
-#   usage: tools/addr_ab.sh OUTTAG variant
+#   usage: tools/addr_ab.sh OUTTAG variant [variant ...]
 set -e
 OUT=gpurun_out/${1:?tag}
-V=${2:?variant}
+shift
+V="${@:?variant}"
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 300 python -u -m pytest tests/test_addressgen.py -m gpu -x -v --timeout 200 --timeout-method thread > $OUT/pytest_addr.log 2>&1
