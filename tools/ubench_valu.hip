@@ -82,6 +82,20 @@ __global__ __launch_bounds__(256) void kern(uint32_t* out, uint64_t* clk, uint32
 #define X(i) asm volatile("v_alignbit_b32 %0, %0, %1, 7" : "+v"(a##i) : "s"(sb));
         CHAINS8(X)
 #undef X
+      } else if constexpr (OP == 11) {
+        // the address search's field products: 32x32 -> 64 multiply-add
+        uint64_t cc;
+#define X(i) asm volatile("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(q##i), "=s"(cc) : "v"(b), "v"(c));
+        CHAINS8(X)
+#undef X
+      } else if constexpr (OP == 12) {
+#define X(i) asm volatile("v_mul_lo_u32 %0, %0, %1" : "+v"(a##i) : "v"(b));
+        CHAINS8(X)
+#undef X
+      } else if constexpr (OP == 13) {
+#define X(i) asm volatile("v_fma_f64 %0, %0, %1, %2" : "+v"(q##i) : "v"(qb), "v"(qb));
+        CHAINS8(X)
+#undef X
       } else if constexpr (OP == 10) {
 #define X(i) asm volatile("v_lshl_add_u64 %0, %0, 0, %2\n\tv_alignbit_b32 %1, %1, %3, 7" \
                           : "+v"(q##i), "+v"(a##i) : "v"(qb), "v"(b));
@@ -153,6 +167,9 @@ int main() {
   rc |= run<8>("v_add3_u32", 1, blocks, dout, dclk);
   rc |= run<9>("v_alignbit_b32 (sgpr operand)", 1, blocks, dout, dclk);
   rc |= run<10>("v_lshl_add_u64+v_alignbit_b32 (per instr)", 2, blocks, dout, dclk);
+  rc |= run<11>("v_mad_u64_u32", 1, blocks, dout, dclk);
+  rc |= run<12>("v_mul_lo_u32", 1, blocks, dout, dclk);
+  rc |= run<13>("v_fma_f64", 1, blocks, dout, dclk);
   CHECK(hipFree(dout));
   CHECK(hipFree(dclk));
   return rc;
