@@ -106,7 +106,18 @@ class Dist(object):
         if self.world > 1:
             import torch.distributed as dist
             os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-            dist.init_process_group('gloo', rank=self.rank, world_size=self.world)
+            # gloo prints "[Gloo] Rank r is connected to ..." on fd 1 from C++ while it builds its
+            # mesh: send that to stderr so rank 0's stdout holds only the one JSON line
+            sys.stdout.flush()
+            saved = os.dup(1)
+            os.dup2(2, 1)
+            try:
+                dist.init_process_group('gloo', rank=self.rank, world_size=self.world)
+                dist.barrier()
+            finally:
+                sys.stdout.flush()
+                os.dup2(saved, 1)
+                os.close(saved)
             self.dist = dist
 
     def barrier(self):
