@@ -417,22 +417,34 @@ def run_addr_bench(args, dist):
     t0 = time.perf_counter()
     addressgen.search_deterministic(b'comb table build', 1)  # builds the comb table(s) once per device
     table_s = time.perf_counter() - t0
+    if args.addr_mode == 'random':  # createRandomAddress: fixed signing key, fresh encryption keys
+        priv_s = hashlib.sha256(pp).digest()
+        seed = hashlib.sha512(pp).digest()
+
+        def one():
+            r = addressgen.random_address(null_bytes=nb, priv_signing=priv_s, seed=seed)
+            return r['k'], r['ripe']
+        what = 'random address search (class_addressGenerator.py:130-148), %d null bytes, fixed signing key' % nb
+    else:
+        def one():
+            f = addressgen.search_deterministic(pp, nb)
+            return f.k, f.ripe
+        what = 'deterministic address search, %d null bytes, passphrase %r' % (nb, pp)
     for _ in range(args.warmup):
-        f = addressgen.search_deterministic(pp, nb)
+        one()
     dist.barrier()
     lib.bmpow_reset_stats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        f = addressgen.search_deterministic(pp, nb)
+        k, ripe = one()
     dist.barrier()
     elapsed = time.perf_counter() - t0
     st = _lib.BmpowStats()
     lib.bmpow_get_stats(ctypes.byref(st))
-    assert f.ripe[:nb] == b'\x00' * nb
+    assert ripe[:nb] == b'\x00' * nb
     comb = lib.bmpow_addr_last_comb()
-    return {'desc': 'addrgen: deterministic address search, %d null bytes, passphrase %r, found k=%d, '
-                    '%d-bit comb' % (nb, pp, f.k, comb),
-            'tries': float(f.k + 1) * args.steps, 'elapsed': elapsed, 'stats': st, 'k': f.k,
+    return {'desc': 'addrgen: %s, found k=%d, %d-bit comb' % (what, k, comb),
+            'tries': float(k + 1) * args.steps, 'elapsed': elapsed, 'stats': st, 'k': k,
             'comb_bits': comb, 'table_build_s': table_s}
 
 
@@ -442,7 +454,8 @@ def summarize_addr(args, dist, r, lib_version):
     tries = dist.reduce(r['tries'], 'sum')
     launched = dist.reduce(st.addr_tries, 'sum')
     line = {
-        'metric': 'address-search tries/sec (2 x secp256k1 k*G + SHA-512 + RIPEMD-160 per try)',
+        'metric': 'address-search tries/sec (%s secp256k1 k*G + SHA-512 + RIPEMD-160 per try)'
+                  % ('1 x' if args.addr_mode == 'random' else '2 x'),
         'value': round(tries / el_max, 1), 'unit': 'tries/s', 'n_gpus': dist.world, 'steps': args.steps,
         'warmup': args.warmup, 'ms_per_step': round(el_max * 1e3 / args.steps, 3), 'higher_is_better': True,
         'scaling': 'weak', 'vs_baseline': None, 'dtype': 'u32', 'data': 'synthetic',
@@ -458,10 +471,11 @@ def summarize_addr(args, dist, r, lib_version):
     return line
 
 
-def cpu_addr_baseline(seconds):
+def cpu_addr_baseline(seconds, mode='det'):
     """One core: the reference's per-try work with the same library calls it makes -- OpenSSL
-    EC_POINT_mul for both keys (oracle.addrgen_oracle.OpenSSLPointMult), hashlib SHA-512, and
-    RIPEMD-160 (hashlib when OpenSSL's legacy provider is loaded, else the oracle's)."""
+    EC_POINT_mul for both keys (random mode: the encryption key only, the signing key is fixed;
+    oracle.addrgen_oracle.OpenSSLPointMult), hashlib SHA-512, and RIPEMD-160 (hashlib when
+    OpenSSL's legacy provider is loaded, else the oracle's)."""
     import hashlib as hl
 
     from oracle import addrgen_oracle as ao
@@ -472,16 +486,17 @@ def cpu_addr_baseline(seconds):
         which = 'hashlib'
     except ValueError:
         rmd, which = ao.ripemd160, 'pure-Python restatement'
+    pub_s = pm(hl.sha256(ADDR_PASSPHRASE).digest())
     t0 = time.perf_counter()
     k = 0
     while time.perf_counter() - t0 < seconds:
         ps, pe = ao.try_keys(ADDR_PASSPHRASE, k)
-        rmd(hl.sha512(pm(ps) + pm(pe)).digest())
+        rmd(hl.sha512((pub_s if mode == 'random' else pm(ps)) + pm(pe)).digest())
         k += 1
     el = time.perf_counter() - t0
     return {'value': round(k / el, 1), 'unit': 'tries/s', 'cores': 1, 'kind': 'port',
-            'sample': '%d tries in %.1f s: OpenSSL EC_POINT_mul x2 (system libcrypto, as pyelliptic calls it), '
-                      'hashlib SHA-512, RIPEMD-160 via %s; 1 thread' % (k, el, which)}
+            'sample': '%d tries in %.1f s: OpenSSL EC_POINT_mul x%d (system libcrypto, as pyelliptic calls it), '
+                      'hashlib SHA-512, RIPEMD-160 via %s; 1 thread' % (k, el, 1 if mode == 'random' else 2, which)}
 
 
 # ----------------------------------------------------------------------------------------
@@ -541,6 +556,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--config', default='c2', choices=['c1', 'c2', 'c3', 'c4', 'c5', 'verify', 'addrgen'])
     ap.add_argument('--null-bytes', type=int, default=3, help='addrgen: leading zero bytes of the ripe')
+    ap.add_argument('--addr-mode', default='det', choices=['det', 'random'],
+                    help='addrgen: deterministic (passphrase) or random (fixed signing key) keys')
     ap.add_argument('--addr-comb', type=int, default=24, choices=[0, 16, 24],
                     help='addrgen: comb window bits (0 = the library\'s automatic choice)')
     ap.add_argument('--objects', type=int, default=None, help='override the object count (c2/c4/c5)')
@@ -569,7 +586,7 @@ def main():
         r = run_addr_bench(args, dist)
         line = summarize_addr(args, dist, r, lib.bmpow_version().decode())
         if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
-            line['cpu_baseline'] = cpu_addr_baseline(min(args.cpu_seconds, 10.0))
+            line['cpu_baseline'] = cpu_addr_baseline(min(args.cpu_seconds, 10.0), args.addr_mode)
         if dist.rank == 0:
             print(json.dumps(line), flush=True)
         dist.close()

@@ -167,13 +167,13 @@ BM_DEV void ripe_of_points(uint32_t (&rh)[5], const ge& ps, const ge& pe) {
 
 
 #ifndef AR_SINGLE
-// ---- paired tries (the search path): two tries per lane behind ONE inversion ----
-// Lane tries k0 and k0 + 1: four keys (mode 0: 2k0, 2k0+1, 2k0+2, 2k0+3; mode 1: the fixed signing
-// key, k0, the fixed signing key, k0 + 1), four combs left in Jacobian coordinates, then
-// Montgomery's trick over both tries: ZA = Z0 Z1, ZB = Z2 Z3, inv = (ZA ZB)^-1, iA = inv ZB,
-// iB = inv ZA, and per try Zs^-1 = iT Ze, Ze^-1 = iT Zs -- 9 products + 1 inversion for two
-// tries against 6 products + 2 inversions.  X, Y of keys 0..2 wait in LDS (lane-major, so the
-// accesses are bank-conflict free); key 3 stays in registers.
+// ---- four keys per lane behind ONE inversion (the search path) ----
+// Mode 0 (deterministic): the lane runs tries k0 and k0 + 1 -- keys 2k0 .. 2k0 + 3.  Mode 1
+// (random): the signing key is the given affine point, so the lane runs FOUR tries k0 .. k0 + 3,
+// one encryption key each.  Either way four combs end in Jacobian coordinates and Montgomery's
+// trick converts them with one inversion: ZA = Z0 Z1, ZB = Z2 Z3, inv = (ZA ZB)^-1, iA = inv ZB,
+// iB = inv ZA, Z0^-1 = iA Z1, Z1^-1 = iA Z0, Z2^-1 = iB Z3, Z3^-1 = iB Z2.  X, Y of keys 0..2 wait
+// in LDS (lane-major, so the accesses are bank-conflict free); key 3 stays in registers.
 constexpr int kPairLanes = 64;
 
 BM_DEV void fe_sel(fe& r, bool c, const fe& a, const fe& b) {
@@ -208,40 +208,33 @@ BM_DEV void to_affine(ge& r, const fe& x, const fe& y, const fe& zi) {
   ec::fe_normalize(r.y, r.y);
 }
 
-// ripes of tries k0 (rh[0]) and k0 + 1 (rh[1]); ok[t] false when a key of try t is 0 mod n
+// Tries per lane of the search kernel for a mode.
+__host__ __device__ inline uint32_t ar_tries_per_lane(uint32_t mode) { return mode == 0 ? 2u : 4u; }
+
+// The first of the lane's ntries tries (k0, k0 + 1, ...) whose ripe has the prefix; 4 if none.
 template <int W>
-BM_DEV void try_pair(const ar_params* __restrict__ prm, const ge* __restrict__ table, uint64_t k0, uint32_t* st,
-                     uint32_t lane, uint32_t (&rh0)[5], uint32_t (&rh1)[5], bool& ok0, bool& ok1) {
+BM_DEV uint32_t try_quad(const ar_params* __restrict__ prm, const ge* __restrict__ table, uint64_t k0, uint32_t ntries,
+                         uint32_t* st, uint32_t lane) {
   const bool fixed_sign = prm->mode != 0;
   fe z0, z1, z2;
-  ok0 = ok1 = true;
-  gej r;  // after the loop: key 3 (no copy of it is kept live across the loop)
+  uint32_t bad = 0;  // bit t: a key of try t is 0 mod n
+  gej r;             // after the loop: key 3 (no copy of it is kept live across the loop)
 #pragma unroll 1
   for (int q = 0; q < 4; ++q) {  // one hash + one comb body for the four keys
-    if (fixed_sign && (q & 1) == 0) {
-      r.x = prm->pub_s.x;
-      r.y = prm->pub_s.y;
-      ec::fe_set(r.z, 1);
-      r.inf = false;
-    } else {
-      const uint64_t m = fixed_sign ? k0 + (q >> 1) : 2 * k0 + q;
-      uint64_t h[8];
-      key_hash(h, prm, m);
-      const uint64_t kw[4] = {h[0], h[1], h[2], h[3]};
-      ec::scalar_mult_base_jac<W>(r, table, kw);
-    }
+    const uint64_t m = fixed_sign ? k0 + q : 2 * k0 + q;
+    uint64_t h[8];
+    key_hash(h, prm, m);
+    const uint64_t kw[4] = {h[0], h[1], h[2], h[3]};
+    ec::scalar_mult_base_jac<W>(r, table, kw);
     if (r.inf) {  // k = 0 mod n: keep the shared product invertible, drop the try
       ec::fe_set(r.z, 1);
-      if (q < 2) ok0 = false;
-      else ok1 = false;
+      bad |= 1u << (fixed_sign ? q : q >> 1);
     }
     if (q < 3) stash_put(st, q, lane, r.x, r.y);
     fe_sel(z0, q == 0, r.z, z0);
     fe_sel(z1, q == 1, r.z, z1);
     fe_sel(z2, q == 2, r.z, z2);
   }
-  const fe& x3 = r.x;
-  const fe& y3 = r.y;
   const fe& z3 = r.z;
   fe za, zb, inv, ia, ib;
   ec::fe_mul(za, z0, z1);
@@ -250,32 +243,39 @@ BM_DEV void try_pair(const ar_params* __restrict__ prm, const ge* __restrict__ t
   ec::fe_inv(inv, inv);
   ec::fe_mul(ia, inv, zb);
   ec::fe_mul(ib, inv, za);
+  uint32_t hit = 4;
+  ge saved;  // mode 0: the encryption key (odd key) of the try being assembled
 #pragma unroll 1
-  for (int t = 1; t >= 0; --t) {  // one affine + hash body for both tries (try B first: key 3 is live)
-    fe it, zs, ze, zis, zie, xs, ys, xe, ye;
-    fe_sel(it, t == 1, ib, ia);
-    fe_sel(zs, t == 1, z2, z0);
-    fe_sel(ze, t == 1, z3, z1);
-    ec::fe_mul(zis, it, ze);
-    ec::fe_mul(zie, it, zs);
-    stash_get(st, 2 * t, lane, xs, ys);
-    if (t == 1) {
-      xe = x3;
-      ye = y3;
+  for (int q = 3; q >= 0; --q) {  // one affine + hash body for every key (key 3 first: it is live)
+    fe it, zp, zi, x, y;
+    fe_sel(it, q >= 2, ib, ia);
+    fe_sel(zp, q == 0, z1, z0);  // the partner's Z: 0 <-> 1, 2 <-> 3
+    fe_sel(zp, q == 2, z3, zp);
+    fe_sel(zp, q == 3, z2, zp);
+    ec::fe_mul(zi, it, zp);
+    if (q == 3) {
+      x = r.x;
+      y = r.y;
     } else {
-      stash_get(st, 1, lane, xe, ye);
+      stash_get(st, q, lane, x, y);
     }
-    ge ps, pe;
-    to_affine(ps, xs, ys, zis);
-    to_affine(pe, xe, ye, zie);
+    ge a;
+    to_affine(a, x, y, zi);
+    if (!fixed_sign && (q & 1)) {
+      saved = a;
+      continue;
+    }
+    const uint32_t t = fixed_sign ? (uint32_t)q : (uint32_t)q >> 1;
+    ge ps, pe;  // selects, so the hashing is one inlined copy for both modes
+    fe_sel(ps.x, fixed_sign, prm->pub_s.x, a.x);
+    fe_sel(ps.y, fixed_sign, prm->pub_s.y, a.y);
+    fe_sel(pe.x, fixed_sign, a.x, saved.x);
+    fe_sel(pe.y, fixed_sign, a.y, saved.y);
     uint32_t rh[5];
     ripe_of_points(rh, ps, pe);
-#pragma unroll
-    for (int i = 0; i < 5; ++i) {
-      rh1[i] = t == 1 ? rh[i] : rh1[i];
-      rh0[i] = t == 0 ? rh[i] : rh0[i];
-    }
+    if (t < ntries && !((bad >> t) & 1) && prefix_ok(rh, prm->null_bytes)) hit = t;  // q descends
   }
+  return hit;
 }
 #endif  // AR_SINGLE
 
@@ -320,8 +320,8 @@ __global__ __launch_bounds__(64) void ar_table_kernel(const ge* __restrict__ bas
   ec::gej_to_ge(table[t], acc);
 }
 
-// Search: lanes try k in [start, start + count), two consecutive tries per lane (try_pair; one per
-// lane when built with -DAR_SINGLE, the A/B baseline).  best: running minimum k with a hit.
+// Search: lanes try k in [start, start + count), two (mode 0) or four (mode 1) consecutive tries per
+// lane (try_quad; one per lane when built with -DAR_SINGLE, the A/B baseline).  best: running minimum k with a hit.
 // kResolve: the launch instead reports everything about the single try k = start (keys, public
 // keys, ripe) -- the resolve step, sharing this kernel's code; a separate instantiation so the
 // search never keeps the private-key digests live.
@@ -338,16 +338,16 @@ __global__ __launch_bounds__(64) AR_OCC void ar_search_kernel(const ar_params* _
                                                        ar_result* __restrict__ out) {
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
 #ifndef AR_SINGLE
-  if (!kResolve) {  // lane g: tries start + 2g and start + 2g + 1 (the second only below start + count)
+  if (!kResolve) {  // lane g: tries start + T g .. start + T g + T - 1 below start + count (T = 2 or 4)
     __shared__ uint32_t stash[3 * 16 * kPairLanes];
-    if (2ull * g >= count) return;
-    const uint64_t k0 = start + 2ull * g;
+    const uint32_t T = ar_tries_per_lane(prm->mode);
+    const uint64_t first = (uint64_t)T * g;
+    if (first >= count) return;
+    const uint64_t k0 = start + first;
     if (__hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k0) return;
-    uint32_t rh0[5] = {0, 0, 0, 0, 0}, rh1[5] = {0, 0, 0, 0, 0};
-    bool ok0, ok1;
-    try_pair<W>(prm, table, k0, stash, threadIdx.x, rh0, rh1, ok0, ok1);
-    if (ok0 && prefix_ok(rh0, prm->null_bytes)) atomicMin(best, (unsigned long long)k0);
-    else if (ok1 && 2ull * g + 1 < count && prefix_ok(rh1, prm->null_bytes)) atomicMin(best, (unsigned long long)(k0 + 1));
+    const uint32_t ntries = (uint32_t)min((uint64_t)T, count - first);
+    const uint32_t hit = try_quad<W>(prm, table, k0, ntries, stash, threadIdx.x);
+    if (hit < ntries) atomicMin(best, (unsigned long long)(k0 + hit));
     return;
   }
 #endif
@@ -449,14 +449,16 @@ hipError_t ar_launch_table(hipStream_t st, ge* table, int wbits) {
   return wbits == ec::kCombLarge ? launch_table<ec::kCombLarge>(st, table) : launch_table<ec::kCombSmall>(st, table);
 }
 
-hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, const ge* table, int wbits, uint64_t start,
-                            uint32_t count, unsigned long long* best) {
+hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, uint32_t mode, const ge* table, int wbits,
+                            uint64_t start, uint32_t count, unsigned long long* best) {
   if (count == 0) return hipSuccess;
 #ifndef AR_SINGLE
-  const uint32_t lanes = (uint32_t)(((uint64_t)count + 1) / 2);  // two tries per lane
+  const uint32_t tpl = ar_tries_per_lane(mode);  // must match what the kernel reads from prm->mode
 #else
-  const uint32_t lanes = count;
+  const uint32_t tpl = 1;
+  (void)mode;
 #endif
+  const uint32_t lanes = (uint32_t)(((uint64_t)count + tpl - 1) / tpl);
   if (wbits == ec::kCombLarge)
     hipLaunchKernelGGL((ar_search_kernel<false, ec::kCombLarge>), dim3((lanes + 63) / 64), dim3(64), 0, st, prm, table,
                        start, count, best, (ar_result*)nullptr);

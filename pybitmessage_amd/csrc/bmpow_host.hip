@@ -905,8 +905,8 @@ int addr_search_locked(uint32_t mode, const uint8_t* seed, size_t len, const uin
       Shard& sh = g_shards[s];
       HIPTRY(hipSetDevice(sh.dev));
       HIPTRY(hipEventRecord(sh.ev0, sh.stream));
-      HIPTRY(ar_launch_search(sh.stream, as[s].d_prm, sh.d_table[comb], kCombBits[comb], lo[s], (uint32_t)cnt[s],
-                              as[s].d_best));
+      HIPTRY(ar_launch_search(sh.stream, as[s].d_prm, mode, sh.d_table[comb], kCombBits[comb], lo[s],
+                              (uint32_t)cnt[s], as[s].d_best));
       HIPTRY(hipEventRecord(sh.ev1, sh.stream));
     }
     uint64_t best = kU64Max;

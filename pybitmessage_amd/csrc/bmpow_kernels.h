@@ -79,8 +79,9 @@ struct ar_result {
 
 size_t ar_table_entries(int wbits);  // allocation size (entries) of the comb of width wbits
 hipError_t ar_launch_table(hipStream_t st, ec::ge* table, int wbits);
-hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, const ec::ge* table, int wbits, uint64_t start, uint32_t count,
-                            unsigned long long* best);
+// mode: prm->mode (sizes the grid: 2 tries per lane in mode 0, 4 in mode 1)
+hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, uint32_t mode, const ec::ge* table, int wbits,
+                            uint64_t start, uint32_t count, unsigned long long* best);
 hipError_t ar_launch_resolve(hipStream_t st, const ar_params* prm, const ec::ge* table, int wbits, uint64_t k,
                              ar_result* out);
 hipError_t ar_launch_pubkeys(hipStream_t st, const uint64_t* privs, uint32_t n, const ec::ge* table, ec::ge* pubs,

@@ -67,6 +67,20 @@ def test_oracle_matches_reference_fixtures(kats):
         assert ao.ripe_of(ao.point_mult(ps), ao.point_mult(pe)).hex() == t['ripe']
 
 
+def test_oracle_openssl_pointmult_matches_restatement():
+    """The libcrypto EC_POINT_mul binding (bench CPU baseline, random-mode test) against the
+    pure-Python pointMult and the reference's sample keys."""
+    try:
+        pm = ao.OpenSSLPointMult()
+    except Exception as e:  # noqa: BLE001
+        pytest.skip('libcrypto unavailable: %s' % e)
+    import random
+    rng = random.Random(5)
+    for k in [bytes.fromhex(SAMPLE_PRIV_S), bytes.fromhex(SAMPLE_PRIV_E)] + [rng.randbytes(32) for _ in range(8)]:
+        assert pm(k) == ao.point_mult(k)
+    assert pm(bytes.fromhex(SAMPLE_PRIV_S)).hex() == SAMPLE_PUB_S
+
+
 def test_address_formats_match_reference(kats):
     assert addressgen.encodeAddress(2, 1, bytes.fromhex(SAMPLE_RIPE)) == SAMPLE_ADDR_V2
     assert addressgen.encodeAddress(3, 1, bytes.fromhex(SAMPLE_DET_RIPE)) == SAMPLE_DET_ADDR3
@@ -276,3 +290,44 @@ def test_gpu_pubkeys_at_the_group_order(gpulib):
     assert got[0] == bytes(65)
     for k, g in zip(ks[1:], got[1:]):
         assert g == ao.point_mult((k % n).to_bytes(32, 'big'))
+
+
+@gpu
+def test_gpu_random_mode_first_try_and_lane_boundaries(gpulib):
+    """Random mode runs four tries per lane (one inversion for four encryption keys): the search
+    must still return the FIRST k >= start with the prefix, whatever the alignment of start and
+    of the budget to the lanes.  The answer comes from the host restatement of the loop."""
+    import ctypes
+    seed = hashlib.sha512(b'bmpow random-mode test').digest()
+    priv_s = hashlib.sha256(b'bmpow random-mode signing key').digest()
+    try:  # libcrypto's EC_POINT_mul (pinned by test_oracle_openssl_pointmult_matches_restatement)
+        pm = ao.OpenSSLPointMult()
+    except Exception:  # noqa: BLE001
+        pm = ao.point_mult
+    pub_s = pm(priv_s)
+
+    def prefix_at(k):
+        pe = hashlib.sha512(seed + ao.encode_varint(k)).digest()[:32]
+        return ao.ripe_of(pub_s, pm(pe))[:1] == b'\x00'
+
+    hits, k = [], 0
+    while len(hits) < 3 and k < 4000:
+        if prefix_at(k):
+            hits.append(k)
+        k += 1
+    assert len(hits) == 3, hits
+    lib = _lib.get()
+
+    def search(start, n):
+        out = _lib.BmpowAddress()
+        rc = _lib.check(lib, lib.bmpow_address_search_random(priv_s, seed, len(seed), start, n, 1, ctypes.byref(out)),
+                        'bmpow_address_search_random')
+        return out.k if rc == _lib.FOUND else None
+
+    for h in hits[:3]:
+        for start in {max(h - d, 0) for d in (0, 1, 2, 3, 4, 5, 7, 64, 257)}:
+            want = next(x for x in hits if x >= start)
+            assert search(start, 2000) == want, (start, want)
+            assert search(start, h - start + 1) == want  # the budget ends on the hit
+            if want == h and h > start:
+                assert search(start, h - start) is None  # ... or just before it
