@@ -61,9 +61,11 @@ def object_target(L, ttl, ntpb=1000, extra=1000):
     return int(f(L, ttl, ntpb, extra))
 
 
-def make_objects(config, rank, n_override=None):
-    """-> (objects [(target, ih)], workload description)."""
+def make_objects(config, rank, n_override=None, test_mode=False):
+    """-> (objects [(target, ih)], workload description).  test_mode: the reference's -t /
+    extralowdifficulty difficulty (ntpb and extra divided by 100, bitmessagemain.py:167-172)."""
     rng = random.Random(SEED + rank)
+    div = 100 if test_mode else 1
     objs = []
     if config == 'c2':
         n = n_override or 1024
@@ -84,11 +86,12 @@ def make_objects(config, rank, n_override=None):
         for i in range(n):
             if i % 2 == 0:
                 payload = rng.randbytes(46)
-                objs.append((object_target(46, 2419200), hashlib.sha512(payload).digest()))
+                objs.append((object_target(46, 2419200, 1000 // div, 1000 // div), hashlib.sha512(payload).digest()))
             else:
                 payload = rng.randbytes(200)
-                objs.append((object_target(200, 345600), hashlib.sha512(payload).digest()))
-        desc = 'C5: %d objects, 50%% acks (L=46, TTL=28 d) + 50%% pubkey-size (L=200, TTL=4 d)' % n
+                objs.append((object_target(200, 345600, 1000 // div, 1000 // div), hashlib.sha512(payload).digest()))
+        desc = 'C5: %d objects, 50%% acks (L=46, TTL=28 d) + 50%% pubkey-size (L=200, TTL=4 d)%s' % (
+            n, ', test-mode difficulty (ntpb = extra = 10)' if test_mode else '')
     else:
         raise ValueError(config)
     return objs, desc
@@ -385,19 +388,32 @@ def summarize_verify(args, dist, r, lib_version):
     return line
 
 
-def cpu_verify_baseline(seconds):
-    """The reference's per-object check restated with hashlib (targets.pow_value is the
-    protocol.py:280-282 expression), one core, on the same flood."""
+def _verify_pool_worker(seconds):
     from pybitmessage_amd import targets
-    objs = verify_objects(20000, 0)
+    objs = verify_objects(4000, 0)
     t0 = time.perf_counter()
     k = 0
     while time.perf_counter() - t0 < seconds:
         targets.pow_value(objs[k % len(objs)])
         k += 1
-    el = time.perf_counter() - t0
-    return {'value': round(k / el, 1), 'unit': 'objects/s', 'cores': 1, 'kind': 'port',
-            'sample': '%d objects of the same flood hashed by hashlib (OpenSSL) in %.1f s, 1 thread' % (k, el)}
+    return k, time.perf_counter() - t0
+
+
+def cpu_verify_baseline(seconds):
+    """The reference's per-object check (protocol.py:280-282, targets.pow_value: hashlib, i.e.
+    OpenSSL) on the same flood, one process per CPU of the box's share, each hashing for
+    `seconds` (no pickling of objects: every worker builds the flood itself)."""
+    import multiprocessing
+    info = host_cpu_info()
+    p = info['share']
+    with multiprocessing.get_context('fork').Pool(p) as pool:
+        t0 = time.perf_counter()
+        res = pool.map(_verify_pool_worker, [seconds] * p)
+        wall = time.perf_counter() - t0
+    k = sum(r[0] for r in res)
+    return {'value': round(k / wall, 1), 'unit': 'objects/s', 'cores': p, 'kind': 'port',
+            'sample': '%d objects of the same flood hashed by hashlib (OpenSSL) in %.1f s wall on a pool of %d '
+                      'processes' % (k, wall, p), 'host': info}
 
 
 ADDR_PASSPHRASE = b'bmpow address-search benchmark'
@@ -472,20 +488,16 @@ def summarize_addr(args, dist, r, lib_version):
 
 
 def cpu_addr_baseline(seconds, mode='det'):
-    """One core: the reference's per-try work with the same library calls it makes -- OpenSSL
-    EC_POINT_mul for both keys (random mode: the encryption key only, the signing key is fixed;
-    oracle.addrgen_oracle.OpenSSLPointMult), hashlib SHA-512, and RIPEMD-160 (hashlib when
-    OpenSSL's legacy provider is loaded, else the oracle's)."""
+    """One core: the reference's per-try work with the same compiled library calls it makes --
+    OpenSSL EC_POINT_mul for both keys (random mode: the encryption key only, the signing key is
+    fixed; oracle.addrgen_oracle.OpenSSLPointMult), hashlib SHA-512, and libcrypto's RIPEMD160()
+    (oracle.addrgen_oracle.OpenSSLRipemd160; hashlib's ripemd160 needs OpenSSL's legacy provider).
+    The per-call Python overhead is the reference's too (its loop is Python)."""
     import hashlib as hl
 
     from oracle import addrgen_oracle as ao
     pm = ao.OpenSSLPointMult()
-    try:
-        hl.new('ripemd160')
-        rmd = lambda m: hl.new('ripemd160', m).digest()  # noqa: E731
-        which = 'hashlib'
-    except ValueError:
-        rmd, which = ao.ripemd160, 'pure-Python restatement'
+    rmd = ao.OpenSSLRipemd160()
     pub_s = pm(hl.sha256(ADDR_PASSPHRASE).digest())
     t0 = time.perf_counter()
     k = 0
@@ -496,28 +508,69 @@ def cpu_addr_baseline(seconds, mode='det'):
     el = time.perf_counter() - t0
     return {'value': round(k / el, 1), 'unit': 'tries/s', 'cores': 1, 'kind': 'port',
             'sample': '%d tries in %.1f s: OpenSSL EC_POINT_mul x%d (system libcrypto, as pyelliptic calls it), '
-                      'hashlib SHA-512, RIPEMD-160 via %s; 1 thread' % (k, el, 1 if mode == 'random' else 2, which)}
+                      'hashlib SHA-512, libcrypto RIPEMD160(); 1 thread' % (k, el, 1 if mode == 'random' else 2)}
 
 
 # ----------------------------------------------------------------------------------------
-# CPU baseline (rank 0, N=1): the reference's own BitmessagePOW built from its source
+# CPU baseline (rank 0, N=1): the reference's own BitmessagePOW built from its source (the C
+# path, _doCPoW) and its hashlib + multiprocessing path (_doFastPoW), on the host's cores
 # ----------------------------------------------------------------------------------------
-def cpu_baseline_worker(seconds, threads):
-    """Runs in a child process pinned to `threads` CPUs (BitmessagePOW sizes its pool from the
-    affinity mask, bitmsghash.cpp:96,109-121).  Solves C2 objects in order until `seconds`
-    elapse; rate = sum(nonce) / time, the reference's nonce/time convention."""
-    cpus = sorted(os.sched_getaffinity(0))[:threads]
-    os.sched_setaffinity(0, cpus)
+def host_cpu_info():
+    """CPU model, CPU count, this process's affinity and the cgroup CPU quota (the box's share:
+    a one-GPU box may show the whole machine's CPUs while its quota is far smaller)."""
+    model = None
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    quota = None
+    for path in ('/sys/fs/cgroup/cpu.max',):
+        try:
+            q, per = open(path).read().split()[:2]
+            if q != 'max':
+                quota = float(q) / float(per)
+        except (OSError, ValueError):
+            pass
+    if quota is None:
+        try:
+            q = int(open('/sys/fs/cgroup/cpu/cpu.cfs_quota_us').read())
+            per = int(open('/sys/fs/cgroup/cpu/cpu.cfs_period_us').read())
+            quota = q / per if q > 0 else None
+        except (OSError, ValueError):
+            pass
+    aff = len(os.sched_getaffinity(0))
+    share = max(1, int(min(aff, quota))) if quota else aff
+    return {'model': model, 'nproc': os.cpu_count(), 'affinity': aff,
+            'cgroup_quota_cpus': round(quota, 2) if quota else None, 'share': share}
+
+
+def cpu_baseline_worker(seconds, threads, mode):
+    """Child process, never touches the GPU.  Solves C2 objects (the first of the rank-0 batch) in
+    order until `seconds` elapse; rate = sum(nonce) / time, the reference's nonce/time convention.
+    mode 'c': the reference's BitmessagePOW (oracle/_ref) on `threads` CPUs of the affinity mask
+    (it sizes its pthread pool from that mask, bitmsghash.cpp:96,109-121); mode 'fast': the
+    _doFastPoW mechanism (oracle/fastpow.py) with a pool of `threads` processes."""
+    cpus = sorted(os.sched_getaffinity(0))
+    if mode == 'c':
+        os.sched_setaffinity(0, cpus[:threads])
     from oracle import oracle
     objs, _ = make_objects('c2', 0, 64)
-    if oracle.have_ref():
+    if mode == 'fast':
+        from oracle import fastpow
+        kind = 'reference-mechanism'
+        solve = lambda t, ih: fastpow.fast_pow(t, ih, threads)[1]  # noqa: E731
+    elif oracle.have_ref():
         ref = oracle.RefBitmsghash()
         kind = 'reference'
         solve = lambda t, ih: ref.pow(t, ih)[1]  # noqa: E731
     else:
         co = oracle.COracle()
         kind = 'port'
-        solve = lambda t, ih: co.search_mt(ih, t, 1, 1 << 40, threads=len(cpus))[0][1]  # noqa: E731
+        solve = lambda t, ih: co.search_mt(ih, t, 1, 1 << 40, threads=threads)[0][1]  # noqa: E731
     t0 = time.perf_counter()
     total, k = 0, 0
     for t, ih in objs:
@@ -526,26 +579,52 @@ def cpu_baseline_worker(seconds, threads):
         if time.perf_counter() - t0 >= seconds:
             break
     el = time.perf_counter() - t0
-    print(json.dumps({'kind': kind, 'cores': len(cpus), 'objects': k, 'nonce_sum': total, 'seconds': el}))
+    print(json.dumps({'kind': kind, 'mode': mode, 'cores': threads, 'objects': k, 'nonce_sum': total,
+                      'seconds': el}))
 
 
-def cpu_baseline(seconds, threads):
+def _cpu_leg(seconds, threads, mode):
     cmd = [sys.executable, os.path.abspath(__file__), '--cpu-baseline-worker', '--cpu-seconds', str(seconds),
-           '--cpu-threads', str(threads)]
+           '--cpu-threads', str(threads), '--cpu-mode', mode]
     env = dict(os.environ)
     env['HIP_VISIBLE_DEVICES'] = ''  # the baseline never touches the GPU
-    out = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds * 10 + 120, env=env)
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds * 20 + 120, env=env)
     line = [l for l in out.stdout.splitlines() if l.startswith('{')]
     if out.returncode != 0 or not line:
         return {'error': (out.stderr or out.stdout)[-400:]}
     r = json.loads(line[-1])
-    rate = r['nonce_sum'] / r['seconds']
-    lib = 'oracle/_ref/bitmsghash.so (reference BitmessagePOW, OpenSSL SHA512, pthreads)' \
-        if r['kind'] == 'reference' else 'oracle/liboracle.so bmo_search_mt'
-    return {'value': rate / 1e9, 'unit': 'GH/s', 'cores': r['cores'], 'kind': r['kind'],
-            'objects_per_s': r['objects'] / r['seconds'],
-            'sample': '%d C2 objects (first of the rank-0 batch) solved in %.1f s by %s on %d host threads; '
-                      'rate = sum(nonce)/time' % (r['objects'], r['seconds'], lib, r['cores'])}
+    r['ghs'] = r['nonce_sum'] / r['seconds'] / 1e9
+    r['objects_per_s'] = r['objects'] / r['seconds']
+    return r
+
+
+def cpu_baseline(seconds, threads=None):
+    """The C path (reference BitmessagePOW) at the box's CPU share and, when the process may run
+    on more CPUs than that, at every CPU of its affinity mask too; the Fast path (_doFastPoW
+    mechanism) at the share.  `value` = the best rate; every leg is reported."""
+    info = host_cpu_info()
+    share = threads or info['share']
+    legs = {'c_share': _cpu_leg(seconds, share, 'c')}
+    if info['affinity'] > share:
+        legs['c_all_cpus'] = _cpu_leg(max(4.0, seconds / 2), info['affinity'], 'c')
+    legs['fast_share'] = _cpu_leg(seconds, share, 'fast')
+    ok = {k: v for k, v in legs.items() if 'ghs' in v}
+    if not ok:
+        return {'error': legs, 'host': info}
+    best_key = max(ok, key=lambda k: ok[k]['ghs'])
+    best = ok[best_key]
+    what = {'c': 'oracle/_ref/bitmsghash.so (reference BitmessagePOW compiled from its source, OpenSSL SHA512, '
+                 'pthreads)' if best['kind'] == 'reference' else 'oracle/liboracle.so bmo_search_mt (port)',
+            'fast': 'the _doFastPoW mechanism (oracle/fastpow.py: hashlib, multiprocessing Pool, 0.2 s polling)'}
+    return {'value': round(best['ghs'], 6), 'unit': 'GH/s', 'cores': best['cores'],
+            'kind': 'reference' if best['kind'] in ('reference', 'reference-mechanism') else 'port',
+            'objects_per_s': round(best['objects_per_s'], 4), 'best_leg': best_key,
+            'sample': '%d C2 objects (the first of the rank-0 batch) solved in %.1f s by %s on %d host CPUs; '
+                      'rate = sum(nonce)/time' % (best['objects'], best['seconds'], what[best['mode']], best['cores']),
+            'host': info,
+            'legs': {k: ({'ghs': round(v['ghs'], 6), 'cores': v['cores'], 'objects': v['objects'],
+                          'seconds': round(v['seconds'], 2), 'kind': v['kind']} if 'ghs' in v else v)
+                     for k, v in legs.items()}}
 
 
 # ----------------------------------------------------------------------------------------
@@ -564,13 +643,14 @@ def main():
     ap.add_argument('--c3-log2', type=int, default=36)
     ap.add_argument('--step-trials', type=int, default=0, help='per-launch trial budget per GPU (0 = lib default)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
-    ap.add_argument('--cpu-threads', type=int, default=16)
+    ap.add_argument('--cpu-threads', type=int, default=0, help='CPU-baseline threads (0 = the box\'s CPU share)')
+    ap.add_argument('--cpu-mode', default='c', choices=['c', 'fast'], help=argparse.SUPPRESS)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--share-device', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--cpu-baseline-worker', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_baseline_worker:
-        cpu_baseline_worker(args.cpu_seconds, args.cpu_threads)
+        cpu_baseline_worker(args.cpu_seconds, args.cpu_threads, args.cpu_mode)
         return
 
     dist = Dist()
@@ -605,7 +685,7 @@ def main():
     r = runner(args, dist)
     line = summarize(args, dist, r, lib.bmpow_version().decode())
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
-        line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_threads)
+        line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_threads or None)
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     dist.close()

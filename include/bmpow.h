@@ -50,6 +50,7 @@ extern "C" {
 #define BMPOW_DONE_FOUND 1
 #define BMPOW_DONE_EXHAUSTED 2 /* reached nonce 2^64-1 without a hit */
 #define BMPOW_PARKED 3         /* in the table but not scheduled (bmpow_batch_set_pending) */
+#define BMPOW_FREE 4           /* released slot (bmpow_batch_take_done), reused by bmpow_batch_add */
 
 /* ---- lifecycle (replaces proofofwork.init / bmpow global, src/proofofwork.py:336-394) ---- */
 
@@ -103,6 +104,19 @@ BMPOW_API int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start
 BMPOW_API int bmpow_search_batch(size_t n, const uint8_t *ihs, const uint64_t *targets, uint64_t *next_start,
                        uint64_t budget, uint64_t *nonce_out, uint64_t *trial_out, uint8_t *done);
 
+/* Min-trial probe: *min_out = min{ trial(m, ih) : start <= m < start + count } (never past
+ * 2^64-1) and *argmin_out = the first m reaching it; count == 0 gives UINT64_MAX and start.
+ * It hashes every nonce of the range (no target, no early exit) and reduces, a code path apart
+ * from the search's hit logic, so it proves a search answer n minimal at any size: n is the
+ * _doSafePoW answer (src/proofofwork.py:100-111) iff trial(n) <= target and the min over
+ * [1, n) is > target.  No reference counterpart (test and bench instrument).  0 or < 0. */
+BMPOW_API int bmpow_min_trial(const uint8_t ih[64], uint64_t start, uint64_t count, uint64_t *min_out,
+                              uint64_t *argmin_out);
+
+/* The same for n objects (ihs: n x 64 bytes) with their own ranges, in one pass over the devices. */
+BMPOW_API int bmpow_min_trial_batch(size_t n, const uint8_t *ihs, const uint64_t *start, const uint64_t *count,
+                                    uint64_t *min_out, uint64_t *argmin_out);
+
 /* ---- device-resident batch session (the object table stays in HBM across steps) ---- */
 typedef struct bmpow_batch bmpow_batch;
 
@@ -127,6 +141,21 @@ BMPOW_API int bmpow_batch_reset(bmpow_batch *b, const uint64_t *start);
  * affected.  Lets a caller feed a resident table in pieces (bench.py hands out pieces of one
  * global batch to the ranks on demand).  Returns the pending count or < 0. */
 BMPOW_API int bmpow_batch_set_pending(bmpow_batch *b, size_t first, size_t count, int pending);
+
+/* Append n objects to a live session (between steps; start may be NULL = nonce 1): they join the
+ * next bmpow_batch_step.  Slots released by bmpow_batch_take_done are reused first, then the
+ * table grows; slot_out[i] (may be NULL) receives object i's slot.  Only the new objects cross
+ * PCIe.  Returns the pending count or < 0.  (The continuous-batching feed of worker.PowService:
+ * producers join at any step boundary without a re-upload of the table.) */
+BMPOW_API int bmpow_batch_add(bmpow_batch *b, size_t n, const uint8_t *ihs, const uint64_t *targets,
+                              const uint64_t *start, uint32_t *slot_out);
+
+/* Pop up to `cap` objects finished (FOUND or EXHAUSTED) since the last call, in the order the
+ * steps finished them: slot, nonce, trial, done state (any output but slot_out may be NULL).
+ * Their slots become BMPOW_FREE, for reuse by bmpow_batch_add.  Cost O(returned), so a caller
+ * never scans the whole table per step.  Returns the count (>= 0) or < 0. */
+BMPOW_API int bmpow_batch_take_done(bmpow_batch *b, size_t cap, uint32_t *slot_out, uint64_t *nonce_out,
+                                    uint64_t *trial_out, uint8_t *done_out);
 
 BMPOW_API void bmpow_batch_destroy(bmpow_batch *b);
 
@@ -237,6 +266,9 @@ typedef struct bmpow_stats {
     uint64_t addr_launches;   /* search steps */
     uint64_t addr_tries;      /* tries launched (each: 2 SHA-512, 2 k*G, SHA-512, RIPEMD-160) */
     double addr_kernel_ms;    /* max over shards per step, summed (HIP events) */
+    /* min-trial probe (bmpow_min_trial*) */
+    uint64_t probe_trials;    /* nonces hashed by the probe */
+    double probe_kernel_ms;   /* sum over launches of probe-kernel time (HIP events) */
 } bmpow_stats;
 
 BMPOW_API int bmpow_get_stats(bmpow_stats *out);

@@ -146,6 +146,26 @@ int bmo_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
     return 0;
 }
 
+/* Minimum trial value over [start, start+count) (never past 2^64-1) and the FIRST nonce that
+ * reaches it -- the checker for the device probe bmpow_min_trial.  Minimality of a search
+ * answer n follows from min over [1, n) > target (no earlier nonce satisfies _doSafePoW's
+ * `trialValue <= target`, src/proofofwork.py:104).  count == 0: *min_out = UINT64_MAX and
+ * *argmin_out = start, returns 0; else returns 1. */
+int bmo_min_trial(const uint8_t ih[64], uint64_t start, uint64_t count, uint64_t *min_out,
+                  uint64_t *argmin_out) {
+    uint64_t best = UINT64_MAX, arg = start;
+    int any = 0;
+    for (uint64_t i = 0; i < count; i++) {
+        uint64_t n = start + i;
+        uint64_t tv = bmo_trial(ih, n);
+        if (!any || tv < best) { best = tv; arg = n; any = 1; }
+        if (n == UINT64_MAX) break;
+    }
+    *min_out = best;
+    *argmin_out = arg;
+    return any;
+}
+
 /* ---- multi-threaded exact search (CPU baseline port) ---- */
 #define MT_CHUNK 4096u
 

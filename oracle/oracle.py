@@ -68,6 +68,8 @@ class COracle(object):
         lib.bmo_search_mt.argtypes = [ctypes.c_char_p, u64, u64, u64, ctypes.c_int, p64, p64, p64]
         lib.bmo_sha512.restype = None
         lib.bmo_sha512.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
+        lib.bmo_min_trial.restype = ctypes.c_int
+        lib.bmo_min_trial.argtypes = [ctypes.c_char_p, u64, u64, p64, p64]
 
     def sha512(self, data):
         out = ctypes.create_string_buffer(64)
@@ -91,6 +93,13 @@ class COracle(object):
         if self.lib.bmo_search(ih, min(target, U64_MAX), start, max_trials, ctypes.byref(n), ctypes.byref(t)):
             return t.value, n.value
         return None
+
+    def min_trial(self, ih, start, count):
+        """(min trial over [start, start+count), first nonce reaching it); (U64_MAX, start)
+        for an empty range."""
+        m, a = ctypes.c_uint64(), ctypes.c_uint64()
+        self.lib.bmo_min_trial(ih, start, count, ctypes.byref(m), ctypes.byref(a))
+        return m.value, a.value
 
     def search_mt(self, ih, target, start=1, max_trials=U64_MAX, threads=1):
         """Exact multi-threaded search; returns ((trialValue, nonce) | None, trials_performed)."""

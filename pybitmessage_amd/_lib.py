@@ -24,6 +24,7 @@ PENDING = 0
 DONE_FOUND = 1
 DONE_EXHAUSTED = 2
 PARKED = 3
+FREE = 4
 
 U64_MAX = (1 << 64) - 1
 
@@ -46,7 +47,8 @@ class BmpowStats(ctypes.Structure):
                 ('steps', ctypes.c_uint64), ('verify_launches', ctypes.c_uint64),
                 ('verify_objects', ctypes.c_uint64), ('verify_blocks', ctypes.c_uint64),
                 ('verify_kernel_ms', ctypes.c_double), ('addr_launches', ctypes.c_uint64),
-                ('addr_tries', ctypes.c_uint64), ('addr_kernel_ms', ctypes.c_double)]
+                ('addr_tries', ctypes.c_uint64), ('addr_kernel_ms', ctypes.c_double),
+                ('probe_trials', ctypes.c_uint64), ('probe_kernel_ms', ctypes.c_double)]
 
 
 class BmpowAddress(ctypes.Structure):
@@ -59,6 +61,7 @@ class BmpowAddress(ctypes.Structure):
 # (name, restype, argtypes) for every symbol include/bmpow.h declares
 _u64, _p64, _pu8 = ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint8)
 _vp = ctypes.c_void_p
+_pu32 = ctypes.POINTER(ctypes.c_uint32)
 SIGNATURES = [
     ('bmpow_init', ctypes.c_int, []),
     ('bmpow_device_count', ctypes.c_int, []),
@@ -71,6 +74,8 @@ SIGNATURES = [
     ('bmpow_clear_abort', None, []),
     ('bmpow_trials', ctypes.c_int, [ctypes.c_char_p, _p64, ctypes.c_size_t, _p64]),
     ('bmpow_search', ctypes.c_int, [ctypes.c_char_p, _u64, _u64, _u64, _p64, _p64]),
+    ('bmpow_min_trial', ctypes.c_int, [ctypes.c_char_p, _u64, _u64, _p64, _p64]),
+    ('bmpow_min_trial_batch', ctypes.c_int, [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _p64, _p64]),
     ('bmpow_search_batch', ctypes.c_int,
      [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _u64, _p64, _p64, _pu8]),
     ('bmpow_batch_create', _vp, [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64]),
@@ -78,6 +83,8 @@ SIGNATURES = [
     ('bmpow_batch_results', ctypes.c_int, [_vp, _p64, _p64, _pu8, _p64]),
     ('bmpow_batch_reset', ctypes.c_int, [_vp, _p64]),
     ('bmpow_batch_set_pending', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]),
+    ('bmpow_batch_add', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _pu32]),
+    ('bmpow_batch_take_done', ctypes.c_int, [_vp, ctypes.c_size_t, _pu32, _p64, _p64, _pu8]),
     ('bmpow_batch_destroy', None, [_vp]),
     ('bmpow_get_stats', ctypes.c_int, [ctypes.POINTER(BmpowStats)]),
     ('bmpow_reset_stats', None, []),

@@ -69,6 +69,10 @@ struct Shard {
   // step bookkeeping
   uint32_t nitems = 0, nchunks = 0;
   std::vector<uint32_t> item_obj;
+  // min-trial probe: one bm_minpart per workgroup of a launch (grow-only)
+  bm_minpart* d_parts = nullptr;
+  bm_minpart* h_parts = nullptr;  // pinned
+  size_t parts_cap = 0;
   // stats
   double kernel_ms = 0.0;
   // address search: the fixed-base comb tables (v * 2^(W i) * G) for W = 16 ([0]) and 24 ([1]),
@@ -92,19 +96,27 @@ std::vector<Shard> g_shards;
 bool g_inited = false;
 bmpow_stats g_stats{};
 
+// Grow the shard's item staging to hold n items.  Called while a step's item list is being
+// filled, so the host items already written (s.nitems of them) move to the new buffer; the device
+// copies and the results are (re)written after the fill.
 int ensure_items(Shard& s, size_t n) {
   if (n <= s.item_cap) return 0;
   size_t cap = std::max<size_t>(n, 2 * s.item_cap);
   HIPTRY(hipSetDevice(s.dev));
+  bm_item* h_items = nullptr;
+  HIPTRY(hipHostMalloc(&h_items, cap * sizeof(bm_item), hipHostMallocDefault));
+  if (s.h_items) {
+    std::memcpy(h_items, s.h_items, std::min<size_t>(s.nitems, s.item_cap) * sizeof(bm_item));
+    HIPTRY(hipHostFree(s.h_items));
+  }
+  s.h_items = h_items;
   if (s.d_items) {
     HIPTRY(hipFree(s.d_items));
     HIPTRY(hipFree(s.d_res));
-    HIPTRY(hipHostFree(s.h_items));
     HIPTRY(hipHostFree(s.h_res));
   }
   HIPTRY(hipMalloc(&s.d_items, cap * sizeof(bm_item)));
   HIPTRY(hipMalloc(&s.d_res, cap * sizeof(bm_result)));
-  HIPTRY(hipHostMalloc(&s.h_items, cap * sizeof(bm_item), hipHostMallocDefault));
   HIPTRY(hipHostMalloc(&s.h_res, cap * sizeof(bm_result), hipHostMallocDefault));
   s.item_cap = cap;
   return 0;
@@ -119,6 +131,8 @@ void free_shard(Shard& s) {
   if (s.h_items) (void)hipHostFree(s.h_items);
   if (s.h_res) (void)hipHostFree(s.h_res);
   if (s.h_trials) (void)hipHostFree(s.h_trials);
+  if (s.d_parts) (void)hipFree(s.d_parts);
+  if (s.h_parts) (void)hipHostFree(s.h_parts);
   for (int c = 0; c < 2; ++c)
     if (s.d_table[c] && s.owns_table[c]) (void)hipFree(s.d_table[c]);
   for (int c = 0; c < 2; ++c) {
@@ -215,15 +229,20 @@ void pack_obj(const uint8_t* ih, uint64_t target, bm_obj* o) {
 // lifetime of the batch (one copy per shard).
 // ---------------------------------------------------------------------------------------
 struct bmpow_batch {
-  size_t n = 0;
+  size_t n = 0;    // slots in the table (objects, finished ones and free slots included)
+  size_t cap = 0;  // device allocation, in objects (grows geometrically with bmpow_batch_add)
   std::vector<bm_obj> objs;
   std::vector<uint64_t> next, nonce, trial;
   std::vector<uint8_t> done;
   size_t first_pending = 0;
   size_t pending = 0;
+  std::vector<uint32_t> finished;  // slots finished since the last bmpow_batch_take_done, in order
+  size_t finished_head = 0;
+  std::vector<uint32_t> free_slots;  // slots released by bmpow_batch_take_done, reused by adds
   struct Dev {
     bm_obj* d_obj = nullptr;
-    unsigned long long* d_best = nullptr;
+    unsigned long long* d_best = nullptr;  // running minimum hit nonce (valid where d_found)
+    uint32_t* d_found = nullptr;           // 1 once the object has a hit on this shard
   };
   std::vector<Dev> dev;  // one per shard (indexed like g_shards)
 };
@@ -235,22 +254,26 @@ void batch_free_dev(bmpow_batch* b) {
     (void)hipSetDevice(g_shards[s].dev);
     if (b->dev[s].d_obj) (void)hipFree(b->dev[s].d_obj);
     if (b->dev[s].d_best) (void)hipFree(b->dev[s].d_best);
+    if (b->dev[s].d_found) (void)hipFree(b->dev[s].d_found);
   }
   b->dev.clear();
 }
 
 int batch_upload(bmpow_batch* b) {
   b->dev.assign(g_shards.size(), bmpow_batch::Dev());
-  const size_t n = std::max<size_t>(b->n, 1);
+  const size_t n = std::max<size_t>(b->cap, std::max<size_t>(b->n, 1));
+  b->cap = n;
   for (size_t s = 0; s < g_shards.size(); ++s) {
     Shard& sh = g_shards[s];
     HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(hipMalloc(&b->dev[s].d_obj, n * sizeof(bm_obj)));
     HIPTRY(hipMalloc(&b->dev[s].d_best, n * sizeof(unsigned long long)));
+    HIPTRY(hipMalloc(&b->dev[s].d_found, n * sizeof(uint32_t)));
     if (b->n) {
       HIPTRY(hipMemcpyAsync(b->dev[s].d_obj, b->objs.data(), b->n * sizeof(bm_obj), hipMemcpyHostToDevice,
                             sh.stream));
       HIPTRY(hipMemsetAsync(b->dev[s].d_best, 0xFF, b->n * sizeof(unsigned long long), sh.stream));
+      HIPTRY(hipMemsetAsync(b->dev[s].d_found, 0, b->n * sizeof(uint32_t), sh.stream));
     }
   }
   for (auto& sh : g_shards) {
@@ -273,43 +296,96 @@ int batch_init(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* tar
   }
   b->first_pending = 0;
   b->pending = n;
+  b->cap = n;
   return batch_upload(b);
 }
 
-// One bounded step.  Returns pending count (>= 0) or < 0.
-int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
-  if (trials_out) *trials_out = 0;
-  if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
-  if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
-  while (b->first_pending < b->n && b->done[b->first_pending] != BMPOW_PENDING) ++b->first_pending;
-  if (b->pending == 0) return 0;
-  const size_t S = g_shards.size();
-  if (budget == 0) budget = g_step_trials * S;
-  budget = std::min<uint64_t>(budget, (uint64_t)S << 36);  // grid.x stays far below 2^31
-  // workgroup size in nonces: short rounds for small steps (below ~6 full rounds of the chip
-  // per shard), full chunks otherwise
-  const uint32_t iters = budget < ((uint64_t)1 << 26) * S ? BM_ITERS_SMALL : BM_ITERS;
-  const uint64_t chunk = (uint64_t)BM_BLOCK * iters;
-  uint64_t total_chunks = std::max<uint64_t>(budget / chunk, S);
-
-  // 1. windows: pending objects in index order, k chunks each
-  struct Win { uint32_t obj; uint64_t start, count, chunks, chunk0; };
-  std::vector<Win> wins;
-  const uint64_t k = std::max<uint64_t>(1, total_chunks / b->pending);
-  uint64_t chunk_acc = 0;
-  for (size_t i = b->first_pending; i < b->n && chunk_acc < total_chunks; ++i) {
-    if (b->done[i] != BMPOW_PENDING) continue;
-    const uint64_t st = b->next[i];
-    uint64_t want = k * chunk;
-    const uint64_t room = kU64Max - st;  // nonces remaining after st
-    if (room < want - 1) want = room + 1;   // st + want - 1 <= 2^64-1
-    const uint64_t ch = (want + chunk - 1) / chunk;
-    wins.push_back({(uint32_t)i, st, want, ch, chunk_acc});
-    chunk_acc += ch;
+void batch_mark_finished(bmpow_batch* b, uint32_t slot) {
+  if (b->finished_head > 4096 && b->finished_head * 2 > b->finished.size()) {  // drop the consumed prefix
+    b->finished.erase(b->finished.begin(), b->finished.begin() + b->finished_head);
+    b->finished_head = 0;
   }
-  const uint64_t C = chunk_acc;
+  b->finished.push_back(slot);
+}
 
-  // 2. slice the chunk list over shards
+// Append m objects to a live session between steps: released slots are reused first (LIFO), then
+// the table grows (device buffers reallocated at twice the size and re-uploaded from the host
+// mirror).  Only the slots written are uploaded, one copy per contiguous run.  Resetting best[]
+// and found[] over those runs is safe between steps: a pending object's device state is always
+// (UINT64_MAX, 0) there, since a hit finishes its object in the step that finds it.
+int batch_add_locked(bmpow_batch* b, size_t m, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
+                     uint32_t* slot_out) {
+  if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
+  const size_t fresh = m > b->free_slots.size() ? m - b->free_slots.size() : 0;
+  if (b->n + fresh > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many objects");
+  std::vector<uint32_t> slots(m);
+  const size_t n0 = b->n;
+  for (size_t i = 0; i < m; ++i) {
+    uint32_t slot;
+    if (!b->free_slots.empty()) {
+      slot = b->free_slots.back();
+      b->free_slots.pop_back();
+    } else {
+      slot = (uint32_t)b->n++;
+    }
+    slots[i] = slot;
+  }
+  if (b->n > n0) {
+    b->objs.resize(b->n);
+    b->next.resize(b->n);
+    b->nonce.resize(b->n);
+    b->trial.resize(b->n);
+    b->done.resize(b->n, BMPOW_FREE);
+  }
+  for (size_t i = 0; i < m; ++i) {
+    const uint32_t k = slots[i];
+    pack_obj(ihs + 64 * i, targets[i], &b->objs[k]);
+    b->next[k] = start ? start[i] : 1;
+    b->nonce[k] = b->trial[k] = 0;
+    b->done[k] = BMPOW_PENDING;
+    b->pending++;
+    if (k < b->first_pending) b->first_pending = k;
+    if (slot_out) slot_out[i] = k;
+  }
+  if (b->n > b->cap) {  // grow: fresh device buffers, everything re-uploaded
+    b->cap = std::max<size_t>({b->n, 2 * b->cap, 1024});
+    batch_free_dev(b);
+    return batch_upload(b);
+  }
+  std::vector<uint32_t> sorted(slots);
+  std::sort(sorted.begin(), sorted.end());
+  for (size_t s = 0; s < g_shards.size(); ++s) {
+    Shard& sh = g_shards[s];
+    HIPTRY(hipSetDevice(sh.dev));
+    for (size_t i = 0; i < sorted.size();) {
+      size_t j = i + 1;
+      while (j < sorted.size() && sorted[j] == sorted[j - 1] + 1) ++j;
+      const size_t lo = sorted[i], cnt = j - i;
+      HIPTRY(hipMemcpyAsync(b->dev[s].d_obj + lo, b->objs.data() + lo, cnt * sizeof(bm_obj), hipMemcpyHostToDevice,
+                            sh.stream));
+      HIPTRY(hipMemsetAsync(b->dev[s].d_best + lo, 0xFF, cnt * sizeof(unsigned long long), sh.stream));
+      HIPTRY(hipMemsetAsync(b->dev[s].d_found + lo, 0, cnt * sizeof(uint32_t), sh.stream));
+      i = j;
+    }
+  }
+  for (auto& sh : g_shards) {
+    HIPTRY(hipSetDevice(sh.dev));
+    HIPTRY(hipStreamSynchronize(sh.stream));
+  }
+  return 0;
+}
+
+// One object's contiguous nonce window in a step: `chunks` chunks from chunk index `chunk0` of the
+// step's flattened chunk list.
+struct Win {
+  uint32_t obj;
+  uint64_t start, count, chunks, chunk0;
+};
+
+// Cut the step's C chunks (windows in ascending chunk0) into S contiguous slices, one per shard, and
+// fill each shard's item list: big windows are nonce-sharded, small ones object-sharded.
+int slice_windows(const std::vector<Win>& wins, uint64_t C, uint64_t chunk) {
+  const size_t S = g_shards.size();
   std::vector<uint64_t> cut(S + 1);
   for (size_t s = 0; s <= S; ++s) cut[s] = C * s / S;
   for (size_t s = 0; s < S; ++s) {
@@ -344,6 +420,47 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     }
   }
 
+  return 0;
+}
+
+// One bounded step.  Returns pending count (>= 0) or < 0.
+int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
+  if (trials_out) *trials_out = 0;
+  if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
+  if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
+  while (b->first_pending < b->n && b->done[b->first_pending] != BMPOW_PENDING) ++b->first_pending;
+  if (b->pending == 0) return 0;
+  const size_t S = g_shards.size();
+  if (budget == 0) budget = g_step_trials * S;
+  budget = std::min<uint64_t>(budget, (uint64_t)S << 36);  // grid.x stays far below 2^31
+  // workgroup size in nonces: short rounds for small steps (below ~6 full rounds of the chip
+  // per shard), full chunks otherwise
+  const uint32_t iters = budget < ((uint64_t)1 << 26) * S ? BM_ITERS_SMALL : BM_ITERS;
+  const uint64_t chunk = (uint64_t)BM_BLOCK * iters;
+  uint64_t total_chunks = std::max<uint64_t>(budget / chunk, S);
+
+  // 1. windows: pending objects in index order, k chunks each
+  std::vector<Win> wins;
+  const uint64_t k = std::max<uint64_t>(1, total_chunks / b->pending);
+  uint64_t chunk_acc = 0;
+  for (size_t i = b->first_pending; i < b->n && chunk_acc < total_chunks; ++i) {
+    if (b->done[i] != BMPOW_PENDING) continue;
+    const uint64_t st = b->next[i];
+    uint64_t want = k * chunk;
+    const uint64_t room = kU64Max - st;  // nonces remaining after st
+    if (room < want - 1) want = room + 1;   // st + want - 1 <= 2^64-1
+    const uint64_t ch = (want + chunk - 1) / chunk;
+    wins.push_back({(uint32_t)i, st, want, ch, chunk_acc});
+    chunk_acc += ch;
+  }
+  const uint64_t C = chunk_acc;
+
+  // 2. slice the chunk list over shards
+  {
+    const int rc = slice_windows(wins, C, chunk);
+    if (rc < 0) return rc;
+  }
+
   // 3. launch on every shard, then collect
   for (size_t s = 0; s < S; ++s) {
     Shard& sh = g_shards[s];
@@ -353,9 +470,10 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     HIPTRY(hipMemsetAsync(sh.d_trials, 0, sizeof(unsigned long long), sh.stream));
     HIPTRY(hipEventRecord(sh.ev0, sh.stream));
     HIPTRY(bm_launch_search(sh.stream, sh.nchunks, iters, b->dev[s].d_obj, sh.d_items, sh.nitems,
-                            b->dev[s].d_best, sh.d_trials));
+                            b->dev[s].d_best, b->dev[s].d_found, sh.d_trials));
     HIPTRY(hipEventRecord(sh.ev1, sh.stream));
-    HIPTRY(bm_launch_resolve(sh.stream, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best, sh.d_res));
+    HIPTRY(bm_launch_resolve(sh.stream, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best,
+                             b->dev[s].d_found, sh.d_res));
     HIPTRY(hipMemcpyAsync(sh.h_res, sh.d_res, sh.nitems * sizeof(bm_result), hipMemcpyDeviceToHost, sh.stream));
     HIPTRY(hipMemcpyAsync(sh.h_trials, sh.d_trials, sizeof(unsigned long long), hipMemcpyDeviceToHost, sh.stream));
   }
@@ -381,8 +499,9 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
   g_stats.max_shard_kernel_ms = mx;
   if (trials_out) *trials_out = step_trials;
 
-  // 4. host min-reduction over shards per object
+  // 4. host min-reduction over shards per object (hit[] marks a hit: kU64Max is a legal nonce)
   std::vector<uint64_t> bestn(wins.size(), kU64Max), bestt(wins.size(), 0);
+  std::vector<uint8_t> hit(wins.size(), 0);
   // wins are in ascending object order: map obj -> win index by binary search
   auto win_of = [&](uint32_t obj) {
     size_t lo = 0, hi = wins.size();
@@ -396,9 +515,10 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     Shard& sh = g_shards[s];
     for (uint32_t k2 = 0; k2 < sh.nitems; ++k2) {
       const bm_result& r = sh.h_res[k2];
-      if (r.nonce == kU64Max) continue;
+      if (!r.found) continue;
       const size_t wi = win_of(sh.item_obj[k2]);
-      if (r.nonce < bestn[wi]) {
+      if (!hit[wi] || r.nonce < bestn[wi]) {
+        hit[wi] = 1;
         bestn[wi] = r.nonce;
         bestt[wi] = r.trial;
       }
@@ -406,21 +526,152 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
   }
   for (size_t wi = 0; wi < wins.size(); ++wi) {
     const Win& w = wins[wi];
-    if (bestn[wi] != kU64Max) {
+    if (hit[wi]) {
       b->done[w.obj] = BMPOW_DONE_FOUND;
       b->nonce[w.obj] = bestn[wi];
       b->trial[w.obj] = bestt[wi];
-      b->next[w.obj] = bestn[wi] + 1;
+      b->next[w.obj] = bestn[wi] == kU64Max ? kU64Max : bestn[wi] + 1;
       b->pending--;
+      batch_mark_finished(b, w.obj);
     } else if (w.count - 1 == kU64Max - w.start) {
       b->done[w.obj] = BMPOW_DONE_EXHAUSTED;
       b->next[w.obj] = kU64Max;
       b->pending--;
+      batch_mark_finished(b, w.obj);
     } else {
       b->next[w.obj] = w.start + w.count;
     }
   }
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
+}
+
+int ensure_parts(Shard& s, size_t n) {
+  if (n <= s.parts_cap) return 0;
+  const size_t cap = std::max<size_t>(n, 2 * s.parts_cap);
+  HIPTRY(hipSetDevice(s.dev));
+  if (s.d_parts) HIPTRY(hipFree(s.d_parts));
+  if (s.h_parts) HIPTRY(hipHostFree(s.h_parts));
+  s.d_parts = nullptr;
+  s.h_parts = nullptr;
+  s.parts_cap = 0;
+  HIPTRY(hipMalloc(&s.d_parts, cap * sizeof(bm_minpart)));
+  HIPTRY(hipHostMalloc(&s.h_parts, cap * sizeof(bm_minpart), hipHostMallocDefault));
+  s.parts_cap = cap;
+  return 0;
+}
+
+// Min-trial probe over n (object, range) pairs: min_out[i] = min{trial(m) : m in [start[i],
+// start[i] + count[i])} (clipped at 2^64-1) and argmin_out[i] = the first such m reaching it.
+// Steps of ~g_step_trials per shard; ranges are covered in ascending order, cut over the shards
+// like a search step, and each workgroup's (trial, nonce) minimum is reduced here,
+// lexicographically, so ties keep the smaller nonce.
+int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const uint64_t* count, uint64_t* min_out,
+                     uint64_t* argmin_out) {
+  if (n > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many objects");
+  const size_t S = g_shards.size();
+  std::vector<bm_obj> objs(n);
+  std::vector<uint64_t> cur(n), left(n);
+  std::vector<uint8_t> any(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    pack_obj(ihs + 64 * i, 0, &objs[i]);
+    cur[i] = start[i];
+    left[i] = count[i];
+    if (left[i] && left[i] - 1 > kU64Max - start[i]) left[i] = kU64Max - start[i] + 1;  // stop at 2^64-1
+    min_out[i] = kU64Max;
+    argmin_out[i] = start[i];
+  }
+  std::vector<bm_obj*> d_obj(S, nullptr);
+  auto release = [&]() {
+    for (size_t s = 0; s < S; ++s)
+      if (d_obj[s]) {
+        (void)hipSetDevice(g_shards[s].dev);
+        (void)hipFree(d_obj[s]);
+      }
+  };
+  int rc = 0;
+  for (size_t s = 0; s < S && rc == 0; ++s) {
+    Shard& sh = g_shards[s];
+    hipError_t e = hipSetDevice(sh.dev);
+    if (e == hipSuccess) e = hipMalloc(&d_obj[s], std::max<size_t>(n, 1) * sizeof(bm_obj));
+    if (e == hipSuccess && n)
+      e = hipMemcpyAsync(d_obj[s], objs.data(), n * sizeof(bm_obj), hipMemcpyHostToDevice, sh.stream);
+    if (e != hipSuccess) rc = set_err(BMPOW_E_HIP, std::string("min-trial upload: ") + hipGetErrorString(e));
+  }
+  const uint64_t chunk = BM_CHUNK;
+  const uint64_t total_chunks = std::max<uint64_t>(g_step_trials * S / chunk, S);
+  size_t first = 0;
+  while (rc == 0) {
+    if (g_abort.load()) {
+      rc = set_err(BMPOW_E_ABORTED, "aborted");
+      break;
+    }
+    while (first < n && left[first] == 0) ++first;
+    if (first == n) break;
+    std::vector<Win> wins;
+    uint64_t acc = 0;
+    for (size_t i = first; i < n && acc < total_chunks; ++i) {
+      if (left[i] == 0) continue;
+      const uint64_t room = (total_chunks - acc) * chunk;
+      const uint64_t want = std::min(left[i], room);
+      const uint64_t ch = (want + chunk - 1) / chunk;
+      wins.push_back({(uint32_t)i, cur[i], want, ch, acc});
+      acc += ch;
+    }
+    rc = slice_windows(wins, acc, chunk);
+    if (rc < 0) break;
+    for (size_t s = 0; s < S && rc == 0; ++s) {
+      Shard& sh = g_shards[s];
+      if (sh.nitems == 0) continue;
+      rc = ensure_parts(sh, sh.nchunks);
+      if (rc < 0) break;
+      hipError_t e = hipSetDevice(sh.dev);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream);
+      if (e == hipSuccess) e = hipEventRecord(sh.ev0, sh.stream);
+      if (e == hipSuccess)
+        e = bm_launch_mintrial(sh.stream, sh.nchunks, BM_ITERS, d_obj[s], sh.d_items, sh.nitems, sh.d_parts);
+      if (e == hipSuccess) e = hipEventRecord(sh.ev1, sh.stream);
+      if (e == hipSuccess)
+        e = hipMemcpyAsync(sh.h_parts, sh.d_parts, sh.nchunks * sizeof(bm_minpart), hipMemcpyDeviceToHost,
+                           sh.stream);
+      if (e != hipSuccess) rc = set_err(BMPOW_E_HIP, std::string("min-trial launch: ") + hipGetErrorString(e));
+    }
+    for (size_t s = 0; s < S && rc == 0; ++s) {
+      Shard& sh = g_shards[s];
+      if (sh.nitems == 0) continue;
+      hipError_t e = hipSetDevice(sh.dev);
+      if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
+      float ms = 0;
+      if (e == hipSuccess) e = hipEventElapsedTime(&ms, sh.ev0, sh.ev1);
+      if (e != hipSuccess) {
+        rc = set_err(BMPOW_E_HIP, std::string("min-trial: ") + hipGetErrorString(e));
+        break;
+      }
+      g_stats.probe_kernel_ms += ms;
+      for (uint32_t k = 0; k < sh.nitems; ++k) {
+        const bm_item& it = sh.h_items[k];
+        const uint64_t nch = (it.count + chunk - 1) / chunk;
+        for (uint64_t c = it.chunk_base; c < it.chunk_base + nch; ++c) {
+          const bm_minpart& p = sh.h_parts[c];
+          uint64_t& mt = min_out[it.obj];
+          uint64_t& mn = argmin_out[it.obj];
+          if (!any[it.obj] || p.trial < mt || (p.trial == mt && p.nonce < mn)) {
+            any[it.obj] = 1;
+            mt = p.trial;
+            mn = p.nonce;
+          }
+        }
+      }
+    }
+    if (rc < 0) break;
+    for (const Win& w : wins) {
+      left[w.obj] -= w.count;
+      g_stats.probe_trials += w.count;
+      if (left[w.obj]) cur[w.obj] += w.count;
+    }
+  }
+  release();
+  return rc;
 }
 
 // Library-owned scratch batch reused by the stateless entry points.
@@ -1085,6 +1336,24 @@ int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t
   return BMPOW_NOT_FOUND;
 }
 
+int bmpow_min_trial(const uint8_t ih[64], uint64_t start, uint64_t count, uint64_t* min_out, uint64_t* argmin_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (!ih || !min_out || !argmin_out) return set_err(BMPOW_E_ARG, "null pointer");
+  return min_trial_locked(1, ih, &start, &count, min_out, argmin_out);
+}
+
+int bmpow_min_trial_batch(size_t n, const uint8_t* ihs, const uint64_t* start, const uint64_t* count,
+                          uint64_t* min_out, uint64_t* argmin_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (n == 0) return 0;
+  if (!ihs || !start || !count || !min_out || !argmin_out) return set_err(BMPOW_E_ARG, "null pointer");
+  return min_trial_locked(n, ihs, start, count, min_out, argmin_out);
+}
+
 int bmpow_search_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* next_start,
                        uint64_t budget, uint64_t* nonce_out, uint64_t* trial_out, uint8_t* done) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -1166,17 +1435,22 @@ int bmpow_batch_reset(bmpow_batch* b, const uint64_t* start) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
+  b->pending = 0;
   for (size_t i = 0; i < b->n; ++i) {
     b->next[i] = start ? start[i] : 1;
     b->nonce[i] = b->trial[i] = 0;
+    if (b->done[i] == BMPOW_FREE) continue;  // released slots stay free
     b->done[i] = BMPOW_PENDING;
+    b->pending++;
   }
   b->first_pending = 0;
-  b->pending = b->n;
+  b->finished.clear();
+  b->finished_head = 0;
   for (size_t s = 0; s < g_shards.size(); ++s) {
     Shard& sh = g_shards[s];
     HIPTRY(hipSetDevice(sh.dev));
     if (b->n) HIPTRY(hipMemsetAsync(b->dev[s].d_best, 0xFF, b->n * sizeof(unsigned long long), sh.stream));
+    if (b->n) HIPTRY(hipMemsetAsync(b->dev[s].d_found, 0, b->n * sizeof(uint32_t), sh.stream));
   }
   for (auto& sh : g_shards) {
     HIPTRY(hipSetDevice(sh.dev));
@@ -1200,6 +1474,41 @@ int bmpow_batch_set_pending(bmpow_batch* b, size_t first, size_t count, int pend
   }
   if (pending && first < b->first_pending) b->first_pending = first;
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
+}
+
+int bmpow_batch_add(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
+                    uint32_t* slot_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!b) return set_err(BMPOW_E_STATE, "null batch");
+  if (n == 0) return (int)std::min<size_t>(b->pending, 0x7fffffff);
+  if (!ihs || !targets) return set_err(BMPOW_E_ARG, "null pointer");
+  const int rc = batch_add_locked(b, n, ihs, targets, start, slot_out);
+  if (rc < 0) return rc;
+  return (int)std::min<size_t>(b->pending, 0x7fffffff);
+}
+
+int bmpow_batch_take_done(bmpow_batch* b, size_t cap, uint32_t* slot_out, uint64_t* nonce_out, uint64_t* trial_out,
+                          uint8_t* done_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!b) return set_err(BMPOW_E_STATE, "null batch");
+  if (cap && !slot_out) return set_err(BMPOW_E_ARG, "null pointer");
+  size_t k = 0;
+  cap = std::min<size_t>(cap, 0x7fffffff);
+  while (k < cap && b->finished_head < b->finished.size()) {
+    const uint32_t s = b->finished[b->finished_head++];
+    slot_out[k] = s;
+    if (nonce_out) nonce_out[k] = b->nonce[s];
+    if (trial_out) trial_out[k] = b->trial[s];
+    if (done_out) done_out[k] = b->done[s];
+    b->done[s] = BMPOW_FREE;
+    b->free_slots.push_back(s);
+    ++k;
+  }
+  if (b->finished_head == b->finished.size()) {
+    b->finished.clear();
+    b->finished_head = 0;
+  }
+  return (int)k;
 }
 
 void bmpow_batch_destroy(bmpow_batch* b) {

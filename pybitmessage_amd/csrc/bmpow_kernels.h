@@ -33,8 +33,17 @@ struct bm_item {
 };
 
 struct bm_result {
-  uint64_t nonce;  // UINT64_MAX = no hit in this item's object yet
+  uint64_t nonce;  // the object's minimum hit so far (meaningful only when found)
   uint64_t trial;
+  uint32_t found;  // 1: the object has a hit (nonce 2^64-1 included); 0: none yet
+  uint32_t pad;
+};
+
+// One workgroup's minimum of the min-trial probe: the lowest trial value over its chunk and the
+// first nonce reaching it.
+struct bm_minpart {
+  uint64_t trial;
+  uint64_t nonce;
 };
 
 // Receive-side verification (bv_*): one finished object (nonce || payload) per lane.  The
@@ -50,10 +59,12 @@ struct bv_obj {
 hipError_t bv_launch_pow(hipStream_t st, const bv_obj* objs, uint32_t n, const uint4* pool, uint64_t* pow_out);
 
 hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
-                            const bm_item* items, uint32_t nitems, unsigned long long* best,
+                            const bm_item* items, uint32_t nitems, unsigned long long* best, uint32_t* found,
                             unsigned long long* trials_done);
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
-                             const unsigned long long* best, bm_result* res);
+                             const unsigned long long* best, const uint32_t* found, bm_result* res);
+hipError_t bm_launch_mintrial(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
+                              const bm_item* items, uint32_t nitems, bm_minpart* parts);
 hipError_t bm_launch_trials(hipStream_t st, const bm_obj* obj, const uint64_t* nonces, uint64_t n,
                             uint64_t* out);
 

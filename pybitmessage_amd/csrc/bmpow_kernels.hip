@@ -8,7 +8,9 @@
 //   * the launch covers a list of work items; item = (object, contiguous nonce window);
 //   * each item is cut into CHUNKs of BM_BLOCK x BM_ITERS nonces; one workgroup per chunk;
 //     lane l of iteration i hashes nonce  chunk_first + i*BM_BLOCK + l;
-//   * a hit does atomicMin(best[obj], nonce) -- the per-object minimum over the launch;
+//   * a hit does atomicMin(best[obj], nonce) -- the per-object minimum over the launch -- and
+//     sets found[obj]: best[] starts at UINT64_MAX, which is also a legal nonce (2^64-1), so
+//     "no hit" is found[obj] == 0, never a best[] value;
 //   * exact first-nonce semantics: a chunk whose first nonce is above best[obj] cannot
 //     hold the minimum, so it is skipped (checked at chunk start and after every iteration
 //     with an agent-scope load: the early exit never skips a nonce below the answer);
@@ -28,6 +30,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __res
                                                              const bm_item* __restrict__ items,
                                                              uint32_t nitems,
                                                              unsigned long long* __restrict__ best,
+                                                             uint32_t* __restrict__ found,
                                                              unsigned long long* __restrict__ trials_done,
                                                              uint32_t iters) {
   const uint32_t b = blockIdx.x;
@@ -63,7 +66,10 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __res
     const uint64_t j = base + threadIdx.x;
     const uint64_t nonce = first + j;
     const uint64_t tv = trial_of(ihw, nonce);
-    if (j < cnt && tv <= target) atomicMin(bestp, (unsigned long long)nonce);
+    if (j < cnt && tv <= target) {
+      atomicMin(bestp, (unsigned long long)nonce);
+      __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     done += (cnt - base < BM_BLOCK) ? (uint32_t)(cnt - base) : BM_BLOCK;
     if (seen < first + base + BM_BLOCK) break;  // every later nonce of this chunk is above it
   }
@@ -74,9 +80,9 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __res
 // Launch wrappers (C++ linkage, used by bmpow_host.hip).
 // ---------------------------------------------------------------------------------------
 hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
-                            const bm_item* items, uint32_t nitems, unsigned long long* best,
+                            const bm_item* items, uint32_t nitems, unsigned long long* best, uint32_t* found,
                             unsigned long long* trials_done) {
-  hipLaunchKernelGGL(bm_search_kernel, dim3(nchunks), dim3(BM_BLOCK), 0, st, objs, items, nitems, best,
+  hipLaunchKernelGGL(bm_search_kernel, dim3(nchunks), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
                      trials_done, iters);
   return hipGetLastError();
 }

@@ -25,18 +25,20 @@ __device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce) {
 }
 
 // For each launched item whose object has a hit, recompute the trial value at the winning
-// nonce (one thread per item).  res[k] = {nonce, trial} or {UINT64_MAX, 0}.
+// nonce (one thread per item).  res[k] = {nonce, trial, found = 1} or {UINT64_MAX, 0, found = 0}:
+// the found flag, not the nonce, says whether there is a hit (2^64-1 is a legal answer).
 __global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
                                   uint32_t nitems, const unsigned long long* __restrict__ best,
-                                  bm_result* __restrict__ res) {
+                                  const uint32_t* __restrict__ found, bm_result* __restrict__ res) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nitems) return;
   const uint32_t obj = items[k].obj;
-  const uint64_t n = best[obj];
   bm_result r;
-  r.nonce = n;
+  r.nonce = best[obj];
   r.trial = 0;
-  if (n != ~0ULL) r.trial = trial_obj(objs + obj, n);
+  r.found = found[obj];
+  r.pad = 0;
+  if (r.found) r.trial = trial_obj(objs + obj, r.nonce);
   res[k] = r;
 }
 
@@ -53,10 +55,10 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_trials_kernel(const bm_obj* __res
 // Launch wrappers (C++ linkage, used by bmpow_host.hip).
 // ---------------------------------------------------------------------------------------
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
-                             const unsigned long long* best, bm_result* res) {
+                             const unsigned long long* best, const uint32_t* found, bm_result* res) {
   const uint32_t bs = 64;
   hipLaunchKernelGGL(bm_resolve_kernel, dim3((nitems + bs - 1) / bs), dim3(bs), 0, st, objs, items, nitems,
-                     best, res);
+                     best, found, res);
   return hipGetLastError();
 }
 

@@ -166,12 +166,11 @@ def send_msgs(jobs, build_msg, rng=random, now=None, step_trials=0):
 # continuous batching across producer threads
 # ------------------------------------------------------------------------------------------
 class _Entry(object):
-    __slots__ = ('ih', 'target', 'next', 'future')
+    __slots__ = ('ih', 'target', 'future')
 
     def __init__(self, ih, target, future):
         self.ih = ih
         self.target = target
-        self.next = 1
         self.future = future
 
 
@@ -180,12 +179,17 @@ class PowService(object):
 
     ``submit(target, initialHash)`` returns a ``concurrent.futures.Future`` that resolves to
     ``[trialValue, nonce]`` (the ``run`` answer) or raises ``StopIteration('Interrupted')``
-    when ``state.shutdown`` is set.  One service thread drives ``bmpow_search_batch``: each
-    call is one bounded step over every pending object (its ``next_start`` carries the
-    resume point), so an object submitted mid-flight joins the next step (~45 ms on one
-    MI355X) instead of waiting for the objects ahead of it, and producers never contend for
-    the device.  Replaces concurrent blocking ``run`` calls from the worker and API threads
-    (``class_singleWorker.py:236,1276``, ``api.py:1304,1350``)."""
+    when ``state.shutdown`` is set.  One service thread owns a resident device session
+    (``bmpow_batch_create``): new objects are appended to it between steps
+    (``bmpow_batch_add``, only their 64-byte hashes and targets cross PCIe), each
+    ``bmpow_batch_step`` is one bounded launch per device over every pending object, and
+    finished objects are popped with ``bmpow_batch_take_done`` -- the per-step host work is
+    O(new + finished), never a walk over the whole table.  An object submitted mid-flight joins
+    the next step (~40 ms on one MI355X) instead of waiting for the objects ahead of it, and
+    producers never contend for the device.  Replaces concurrent blocking ``run`` calls from the
+    worker and API threads (``class_singleWorker.py:236,1276``, ``api.py:1304,1350``)."""
+
+    TAKE = 4096  # finished objects popped per bmpow_batch_take_done call
 
     def __init__(self, step_trials=0):
         self.step_trials = step_trials
@@ -234,69 +238,93 @@ class PowService(object):
             raise RuntimeError('No active exception to reraise')
         return self.submit(target, initialHash).result()
 
-    def _fail(self, entries, exc):
+    @staticmethod
+    def _fail(entries, exc):
         for e in entries:
             if not e.future.done():
                 e.future.set_exception(exc)
 
     def _loop(self):
         import numpy as np
-        active = []
+        p64 = ctypes.POINTER(ctypes.c_uint64)
+        pu32 = ctypes.POINTER(ctypes.c_uint32)
+        slot_buf = np.zeros(self.TAKE, dtype=np.uint32)
+        nonce_buf = np.zeros(self.TAKE, dtype=np.uint64)
+        trial_buf = np.zeros(self.TAKE, dtype=np.uint64)
+        done_buf = np.zeros(self.TAKE, dtype=np.uint8)
         try:
             lib = _lib.get()
         except Exception as e:  # noqa: BLE001 -- no device: every submitter sees why
             lib, lib_err = None, e
-        while True:
-            with self._cv:
-                while not self._incoming and not active and not self._stopping:
-                    self._cv.wait(0.5)
-                if self._stopping:
-                    self._fail(active + self._incoming, RuntimeError('PowService stopped'))
-                    self._incoming = []
-                    return
-                active.extend(self._incoming)
-                self._incoming = []
-            if lib is None:
-                self._fail(active, lib_err)
-                active = []
-                continue
-            if state.shutdown != 0:
-                self._fail(active, StopIteration('Interrupted'))
-                active = []
-                continue
-            n = len(active)
-            ihs = b''.join(e.ih for e in active)
-            tg = np.array([e.target for e in active], dtype=np.uint64)
-            nxt = np.array([e.next for e in active], dtype=np.uint64)
-            nonce = np.zeros(n, dtype=np.uint64)
-            trial = np.zeros(n, dtype=np.uint64)
-            done = np.zeros(n, dtype=np.uint8)
-            p64 = ctypes.POINTER(ctypes.c_uint64)
-            try:
-                _lib.check(lib, lib.bmpow_search_batch(n, ihs, tg.ctypes.data_as(p64), nxt.ctypes.data_as(p64),
-                                                       self.step_trials, nonce.ctypes.data_as(p64),
-                                                       trial.ctypes.data_as(p64),
-                                                       done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
-                           'bmpow_search_batch')
-            except Exception as e:  # noqa: BLE001
-                self._fail(active, e)
-                active = []
-                continue
-            self.calls += 1
-            keep = []
-            for i, e in enumerate(active):
-                if done[i] == _lib.DONE_FOUND:
-                    tv, nn = int(trial[i]), int(nonce[i])
-                    try:
-                        proofofwork._verify(e.target, e.ih, tv, nn)
-                    except Exception as err:  # noqa: BLE001
-                        e.future.set_exception(err)
-                        continue
-                    self.solved += 1
-                    e.future.set_result([tv, nn])
-                elif done[i] == _lib.DONE_EXHAUSTED:
-                    e.future.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
-                else:
-                    e.next = int(nxt[i])
-                    keep.append(e)
-            active = keep
+        h = None
+        live = {}  # slot -> _Entry
+
+        def drop(exc):
+            nonlocal h
+            self._fail(list(live.values()), exc)
+            live.clear()
+            if h is not None:
+                lib.bmpow_batch_destroy(h)
+                h = None
+
+        try:
+            while True:
+                with self._cv:
+                    while not self._incoming and not live and not self._stopping:
+                        self._cv.wait(0.5)
+                    if self._stopping:
+                        self._fail(self._incoming, RuntimeError('PowService stopped'))
+                        self._incoming = []
+                        drop(RuntimeError('PowService stopped'))
+                        return
+                    new, self._incoming = self._incoming, []
+                if lib is None:
+                    self._fail(new, lib_err)
+                    continue
+                if state.shutdown != 0:
+                    self._fail(new, StopIteration('Interrupted'))
+                    drop(StopIteration('Interrupted'))
+                    continue
+                try:
+                    if new:
+                        if h is None:
+                            h = lib.bmpow_batch_create(0, None, None, None)
+                            if not h:
+                                raise _lib.BmpowError(_lib.E_HIP, 'bmpow_batch_create: %s'
+                                                      % lib.bmpow_last_error().decode())
+                        tg = np.array([e.target for e in new], dtype=np.uint64)
+                        slots = np.zeros(len(new), dtype=np.uint32)
+                        _lib.check(lib, lib.bmpow_batch_add(h, len(new), b''.join(e.ih for e in new),
+                                                            tg.ctypes.data_as(p64), None, slots.ctypes.data_as(pu32)),
+                                   'bmpow_batch_add')
+                        for e, sl in zip(new, slots.tolist()):
+                            live[sl] = e
+                        new = []
+                    _lib.check(lib, lib.bmpow_batch_step(h, self.step_trials), 'bmpow_batch_step')
+                    self.calls += 1
+                    while True:
+                        k = _lib.check(lib, lib.bmpow_batch_take_done(
+                            h, self.TAKE, slot_buf.ctypes.data_as(pu32), nonce_buf.ctypes.data_as(p64),
+                            trial_buf.ctypes.data_as(p64), done_buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
+                            'bmpow_batch_take_done')
+                        for j in range(k):
+                            e = live.pop(int(slot_buf[j]))
+                            if done_buf[j] == _lib.DONE_FOUND:
+                                tv, nn = int(trial_buf[j]), int(nonce_buf[j])
+                                try:
+                                    proofofwork._verify(e.target, e.ih, tv, nn)
+                                except Exception as err:  # noqa: BLE001
+                                    e.future.set_exception(err)
+                                    continue
+                                self.solved += 1
+                                e.future.set_result([tv, nn])
+                            else:
+                                e.future.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
+                        if k < self.TAKE:
+                            break
+                except Exception as e:  # noqa: BLE001
+                    self._fail(new, e)
+                    drop(e)
+        finally:
+            if h is not None and lib is not None:
+                lib.bmpow_batch_destroy(h)

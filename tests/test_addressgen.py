@@ -48,6 +48,22 @@ def test_oracle_ripemd160_vectors():
         assert ao.ripemd160(m).hex() == h
 
 
+def test_oracle_openssl_ripemd160_matches_restatement():
+    """The libcrypto RIPEMD160() binding (bench CPU baseline) against the specification vectors
+    and the pure-Python restatement."""
+    try:
+        rmd = ao.OpenSSLRipemd160()
+    except Exception as e:  # noqa: BLE001
+        pytest.skip('libcrypto unavailable: %s' % e)
+    import random
+    for m, h in RIPEMD_VECTORS.items():
+        assert rmd(m).hex() == h
+    rng = random.Random(9)
+    for n in (0, 55, 56, 63, 64, 65, 130, 1000):
+        m = rng.randbytes(n)
+        assert rmd(m) == ao.ripemd160(m)
+
+
 def test_oracle_matches_reference_samples():
     assert ao.point_mult_xy(SAMPLE_FACTOR) == SAMPLE_POINT
     ps = ao.point_mult(bytes.fromhex(SAMPLE_PRIV_S))

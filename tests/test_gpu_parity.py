@@ -59,11 +59,6 @@ def test_first_nonce_kats(gpulib, golden):
         assert got == (k['trial'], k['nonce']), k['note']
 
 
-def test_openclpow_vector_and_c1(gpulib, golden):
-    notes = [k['note'] for k in golden('first_nonce_kats.json')['kats']]
-    assert any('224121278' in n for n in notes) and any('10909138' in n for n in notes)
-
-
 def test_batch_kats_run_batch(gpulib, golden):
     d = golden('batch_kats.json')
     objs = [(k['target'], bytes.fromhex(k['ih'])) for k in d['kats']]
@@ -100,6 +95,18 @@ def test_shard_layouts_and_step_sizes(gpulib, shards, coracle, golden, layout, s
     assert proofofwork.run_batch(objs) == want
     for k in golden('first_nonce_kats.json')['kats'][:10]:
         assert gpu_search(gpulib, bytes.fromhex(k['ih']), k['target']) == (k['trial'], k['nonce'])
+
+
+@pytest.mark.parametrize('layout,step', [([0], 1 << 28), ([0, 0], 1 << 24)])
+def test_many_objects_per_step(gpulib, shards, coracle, layout, step):
+    """Thousands of objects in one step (more work items per shard than the scheduler's initial
+    staging holds, so it grows mid-step; round 1 lost the items already written there)."""
+    shards(layout)
+    gpulib.bmpow_set_step_trials(step)
+    rng = random.Random(4242 + len(layout))
+    objs = [(U64 // rng.choice([2, 40, 300, 9000]), rng.randbytes(64)) for _ in range(6000)]
+    want = [list(coracle.search(ih, t)) for t, ih in objs]
+    assert proofofwork.run_batch(objs) == want
 
 
 def test_edge_targets(gpulib, coracle):
@@ -142,6 +149,83 @@ def test_top_of_nonce_space(gpulib, coracle):
         assert done[0] == _lib.DONE_EXHAUSTED
     finally:
         gpulib.bmpow_batch_destroy(h)
+
+
+def test_hit_at_nonce_2_64_minus_1(gpulib, coracle):
+    """Nonce 2^64-1 is a legal answer (the device's 'no hit yet' is a separate flag, not a
+    sentinel nonce): found by bmpow_search, the batch session and bmpow_search_batch."""
+    ih = hashlib.sha512(b'top').digest()
+    t_top = coracle.trial(U64, ih)
+    assert gpu_search(gpulib, ih, U64, U64, 1) == (t_top, U64)
+    assert gpu_search(gpulib, ih, t_top, U64, 1) == (t_top, U64)
+    assert gpu_search(gpulib, ih, t_top - 1, U64, 1) is None if t_top else True
+    # a window ending at 2^64-1 whose only hit is the last nonce: target = trial(2^64-1) when
+    # every earlier nonce of the window is above it
+    start = U64 - 4000
+    m, _ = coracle.min_trial(ih, start, 4000)  # [start, 2^64-1)
+    if m > t_top:
+        assert gpu_search(gpulib, ih, t_top, start, 1 << 20) == (t_top, U64)
+    # batch session starting at the top, and the stateless batch call
+    h = gpulib.bmpow_batch_create(2, ih + ih, _lib.u64_array([U64, 0]), _lib.u64_array([U64, U64]))
+    assert h
+    try:
+        assert gpulib.bmpow_batch_step(h, 0) == 0
+        nonce, trial = (ctypes.c_uint64 * 2)(), (ctypes.c_uint64 * 2)()
+        done, nxt = (ctypes.c_uint8 * 2)(), (ctypes.c_uint64 * 2)()
+        gpulib.bmpow_batch_results(h, nonce, trial, done, nxt)
+        assert (done[0], nonce[0], trial[0], nxt[0]) == (_lib.DONE_FOUND, U64, t_top, U64)
+        assert done[1] == (_lib.DONE_FOUND if t_top == 0 else _lib.DONE_EXHAUSTED)
+    finally:
+        gpulib.bmpow_batch_destroy(h)
+    nxt = _lib.u64_array([U64])
+    nonce, trial, done = (ctypes.c_uint64 * 1)(), (ctypes.c_uint64 * 1)(), (ctypes.c_uint8 * 1)()
+    assert gpulib.bmpow_search_batch(1, ih, _lib.u64_array([U64]), nxt, 0, nonce, trial, done) == 0
+    assert (done[0], nonce[0], trial[0]) == (_lib.DONE_FOUND, U64, t_top)
+    assert proofofwork.run_batch([(U64, ih)]) == [[coracle.trial(1, ih), 1]]
+
+
+def gpu_min_trial(lib, ihs, starts, counts):
+    n = len(starts)
+    mn, arg = np.zeros(n, dtype=np.uint64), np.zeros(n, dtype=np.uint64)
+    st, ct = np.array(starts, dtype=np.uint64), np.array(counts, dtype=np.uint64)
+    _lib.check(lib, lib.bmpow_min_trial_batch(n, b''.join(ihs), st.ctypes.data_as(P64), ct.ctypes.data_as(P64),
+                                              mn.ctypes.data_as(P64), arg.ctypes.data_as(P64)),
+               'bmpow_min_trial_batch')
+    return [(int(a), int(b)) for a, b in zip(mn, arg)]
+
+
+@pytest.mark.parametrize('layout,step', [([0], 1 << 28), ([0, 0, 0], 8192 * 3), ([0, 0], 5000)])
+def test_min_trial_probe_vs_c_oracle(gpulib, shards, coracle, layout, step):
+    """The min-trial probe is bit-exact against the C oracle on ranges the oracle finishes in
+    seconds: ragged sizes, empty ranges, ranges ending at 2^64-1, several shards and tiny steps."""
+    shards(layout)
+    gpulib.bmpow_set_step_trials(step)
+    rng = random.Random(len(layout) * 31 + step)
+    ihs, starts, counts = [], [], []
+    for k in range(40):
+        ihs.append(rng.randbytes(64))
+        if k % 10 == 0:
+            starts.append(U64 - rng.randrange(0, 3000))
+            counts.append(rng.randrange(0, 5000))   # clipped at 2^64-1
+        else:
+            starts.append(rng.choice([0, 1, rng.randrange(1 << 40)]))
+            counts.append(rng.choice([0, 1, 255, 256, 257, 8191, 8192, 8193, rng.randrange(1, 60000)]))
+    want = [coracle.min_trial(ih, s, c) for ih, s, c in zip(ihs, starts, counts)]
+    assert gpu_min_trial(gpulib, ihs, starts, counts) == want
+    m, a = ctypes.c_uint64(), ctypes.c_uint64()
+    assert gpulib.bmpow_min_trial(ihs[1], starts[1], counts[1], ctypes.byref(m), ctypes.byref(a)) == 0
+    assert (m.value, a.value) == want[1]
+
+
+def test_min_trial_large_range(gpulib, coracle):
+    """Two million nonces (hundreds of workgroups, several steps at 2^20 trials) against the
+    oracle's sequential minimum."""
+    gpulib.bmpow_set_step_trials(1 << 20)
+    try:
+        ih = hashlib.sha512(b'min-trial').digest()
+        assert gpu_min_trial(gpulib, [ih], [12345], [2000000]) == [coracle.min_trial(ih, 12345, 2000000)]
+    finally:
+        gpulib.bmpow_set_step_trials(1 << 28)
 
 
 def test_search_batch_stateless_resume(gpulib, coracle):
@@ -265,3 +349,58 @@ def test_batch_park_and_schedule(gpulib, coracle):
         assert gpulib.bmpow_batch_set_pending(h, n, 1, 1) < 0  # range outside the batch
     finally:
         gpulib.bmpow_batch_destroy(h)
+
+
+def test_session_add_and_take_done(gpulib, coracle):
+    """The resident session PowService runs on: objects appended between steps
+    (bmpow_batch_add) join the next step, finished ones are popped in finishing order
+    (bmpow_batch_take_done) and their slots are reused by later adds; every answer exact."""
+    rng = random.Random(8)
+    h = gpulib.bmpow_batch_create(0, None, None, None)
+    assert h
+    pu32 = ctypes.POINTER(ctypes.c_uint32)
+    cap = 256
+    slot_b, nonce_b = np.zeros(cap, dtype=np.uint32), np.zeros(cap, dtype=np.uint64)
+    trial_b, done_b = np.zeros(cap, dtype=np.uint64), np.zeros(cap, dtype=np.uint8)
+    live, got, max_slot = {}, {}, -1
+    try:
+        serial = 0
+        for rnd in range(12):
+            objs = [(U64 // rng.choice([3, 500, 20000, 300000]), rng.randbytes(64)) for _ in range(rng.randrange(1, 400))]
+            tg = np.array([t for t, _ in objs], dtype=np.uint64)
+            slots = np.zeros(len(objs), dtype=np.uint32)
+            assert gpulib.bmpow_batch_add(h, len(objs), b''.join(ih for _, ih in objs), tg.ctypes.data_as(P64), None,
+                                          slots.ctypes.data_as(pu32)) >= len(objs)
+            assert len(set(slots.tolist()) | set(live)) == len(live) + len(objs)  # no live slot handed out twice
+            if rnd >= 4:
+                assert slots.min() <= max_slot  # released slots are reused
+            for o, sl in zip(objs, slots.tolist()):
+                live[sl] = (serial, o)
+                serial += 1
+                max_slot = max(max_slot, sl)
+            gpulib.bmpow_set_step_trials(1 << 22)
+            assert gpulib.bmpow_batch_step(h, 0) >= 0
+            while True:
+                k = gpulib.bmpow_batch_take_done(h, cap, slot_b.ctypes.data_as(pu32), nonce_b.ctypes.data_as(P64),
+                                                 trial_b.ctypes.data_as(P64),
+                                                 done_b.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+                for j in range(k):
+                    sid, o = live.pop(int(slot_b[j]))
+                    assert done_b[j] == _lib.DONE_FOUND
+                    got[sid] = (o, (int(trial_b[j]), int(nonce_b[j])))
+                if k < cap:
+                    break
+        while live:
+            gpulib.bmpow_batch_step(h, 0)
+            k = gpulib.bmpow_batch_take_done(h, cap, slot_b.ctypes.data_as(pu32), nonce_b.ctypes.data_as(P64),
+                                             trial_b.ctypes.data_as(P64),
+                                             done_b.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+            for j in range(k):
+                sid, o = live.pop(int(slot_b[j]))
+                got[sid] = (o, (int(trial_b[j]), int(nonce_b[j])))
+    finally:
+        gpulib.bmpow_batch_destroy(h)
+        gpulib.bmpow_set_step_trials(1 << 28)
+    assert len(got) == serial
+    for (t, ih), res in got.values():
+        assert res == coracle.search(ih, t)

@@ -38,9 +38,10 @@ def test_header_declares_the_boundary():
               'bmpow_set_devices', 'bmpow_last_error', 'BitmessagePOW', 'bmpow_pow_values',
               'bmpow_verify_batch', 'bmpow_pow_sufficient', 'bmpow_vbatch_create', 'bmpow_vbatch_run',
               'bmpow_vbatch_destroy', 'bmpow_pubkeys', 'bmpow_address_search', 'bmpow_address_search_random', 'bmpow_batch_set_pending', 'bmpow_verify_batch_ptrs',
-              'bmpow_addr_set_comb', 'bmpow_addr_last_comb', 'bmpow_fe_probe']:
+              'bmpow_addr_set_comb', 'bmpow_addr_last_comb', 'bmpow_fe_probe', 'bmpow_min_trial',
+              'bmpow_min_trial_batch', 'bmpow_batch_add', 'bmpow_batch_take_done']:
         assert s in syms
-    assert len(syms) == 36
+    assert len(syms) == 40
 
 
 def test_library_exports_every_declared_symbol(rawlib):

@@ -130,3 +130,20 @@ def test_config_targets_formula(golden):
     c1 = [t for t in golden('config_targets.json')['targets'] if t['L'] == 1024 and t.get('ttl') == 345600
           and t['ntpb'] == 1000][0]
     assert c1['target'] == 1447073009577
+
+
+def test_min_trial_oracle_vs_python(coracle):
+    """bmo_min_trial (the checker of the device min-trial probe) against a hashlib loop:
+    ragged ranges, empty ranges, ranges clipped at 2^64-1."""
+    import random as _r
+    from oracle.oracle import U64_MAX, trial
+    rng = _r.Random(11)
+    for start, count in [(0, 1), (1, 500), (12345, 77), (U64_MAX - 30, 31), (U64_MAX - 5, 100), (7, 0)]:
+        ih = rng.randbytes(64)
+        got = coracle.min_trial(ih, start, count)
+        if count == 0:
+            assert got == (U64_MAX, start)
+            continue
+        end = min(start + count, U64_MAX + 1)
+        tv = [(trial(n, ih), n) for n in range(start, end)]
+        assert got == min(tv)

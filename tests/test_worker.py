@@ -40,35 +40,75 @@ def oracle_batch(monkeypatch, coracle):
 
 
 class BatchLib(object):
-    """bmpow_search_batch double: each call advances every pending object by WINDOW nonces,
-    searched with the C oracle, exactly the resume contract of include/bmpow.h."""
+    """Test double of the resident-session ABI (bmpow_batch_create/add/step/take_done/destroy,
+    include/bmpow.h): each step advances every pending object by WINDOW nonces, searched with the
+    C oracle; finished slots are queued for take_done and freed for reuse, as the library does."""
     WINDOW = 3000
 
     def __init__(self, coracle):
         self.co = coracle
         self.calls = 0
         self.sizes = []
+        self.sessions = {}
+        self.next_handle = 1
 
-    def bmpow_search_batch(self, n, ihs, tg, nxt, budget, nonce, trial, done):
-        self.calls += 1
-        self.sizes.append(n)
-        view = lambda p, t: np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(t)), shape=(n,))  # noqa: E731
-        tg, nxt = view(tg, ctypes.c_uint64), view(nxt, ctypes.c_uint64)
-        nonce, trial, done = view(nonce, ctypes.c_uint64), view(trial, ctypes.c_uint64), view(done, ctypes.c_uint8)
-        pending = 0
+    def bmpow_batch_create(self, n, ihs, tg, start):
+        assert n == 0
+        h = self.next_handle
+        self.next_handle += 1
+        self.sessions[h] = {'objs': [], 'queue': [], 'free': []}
+        return h
+
+    def bmpow_batch_add(self, h, n, ihs, tg, start, slot_out):
+        assert start is None
+        ses = self.sessions[h]
+        tg = np.ctypeslib.as_array(ctypes.cast(tg, ctypes.POINTER(ctypes.c_uint64)), shape=(n,))
+        slots = np.ctypeslib.as_array(ctypes.cast(slot_out, ctypes.POINTER(ctypes.c_uint32)), shape=(n,))
         for i in range(n):
-            if done[i]:
-                continue
-            r = self.co.search(ihs[64 * i:64 * i + 64], int(tg[i]), int(nxt[i]), self.WINDOW)
-            if r is None:
-                nxt[i] += self.WINDOW
-                pending += 1
+            o = {'ih': ihs[64 * i:64 * i + 64], 't': int(tg[i]), 'next': 1, 'state': _lib.PENDING}
+            if ses['free']:
+                k = ses['free'].pop()
+                ses['objs'][k] = o
             else:
-                trial[i], nonce[i] = r
-                nxt[i] = r[1] + 1
-                done[i] = _lib.DONE_FOUND
+                k = len(ses['objs'])
+                ses['objs'].append(o)
+            slots[i] = k
+        return sum(o['state'] == _lib.PENDING for o in ses['objs'])
+
+    def bmpow_batch_step(self, h, budget):
+        self.calls += 1
+        ses = self.sessions[h]
+        pend = [k for k, o in enumerate(ses['objs']) if o['state'] == _lib.PENDING]
+        self.sizes.append(len(pend))
+        for k in pend:
+            o = ses['objs'][k]
+            r = self.co.search(o['ih'], o['t'], o['next'], self.WINDOW)
+            if r is None:
+                o['next'] += self.WINDOW
+            else:
+                o['trial'], o['nonce'] = r
+                o['state'] = _lib.DONE_FOUND
+                ses['queue'].append(k)
         time.sleep(0.002)
-        return pending
+        return sum(o['state'] == _lib.PENDING for o in ses['objs'])
+
+    def bmpow_batch_take_done(self, h, cap, slot_out, nonce_out, trial_out, done_out):
+        ses = self.sessions[h]
+        view = lambda p, t: np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(t)), shape=(cap,))  # noqa: E731
+        slots, nonce = view(slot_out, ctypes.c_uint32), view(nonce_out, ctypes.c_uint64)
+        trial, done = view(trial_out, ctypes.c_uint64), view(done_out, ctypes.c_uint8)
+        k = 0
+        while k < cap and ses['queue']:
+            j = ses['queue'].pop(0)
+            o = ses['objs'][j]
+            slots[k], nonce[k], trial[k], done[k] = j, o['nonce'], o['trial'], o['state']
+            o['state'] = _lib.FREE
+            ses['free'].append(j)
+            k += 1
+        return k
+
+    def bmpow_batch_destroy(self, h):
+        del self.sessions[h]
 
     def bmpow_last_error(self):
         return b''
@@ -172,6 +212,7 @@ def test_powservice_concurrent_producers(batchlib, coracle):
         for j, (t, ih) in enumerate(jobs):
             assert results[j] == list(coracle.search(ih, t))
         assert max(batchlib.sizes) > 1  # producers shared device calls
+        assert not batchlib.sessions or all(not ses['queue'] for ses in batchlib.sessions.values())
     finally:
         svc.stop(5)
 
