@@ -31,6 +31,7 @@
 
 #include "../../include/bmpow.h"
 #include "bmpow_kernels.h"
+#include "bmpow_sched.h"
 
 namespace {
 
@@ -40,7 +41,7 @@ constexpr uint64_t kDefaultStepTrials = 1ULL << 28;  // per shard per step, ~40-
 thread_local std::string g_err;
 std::mutex g_mu;
 std::atomic<int> g_abort{0};
-uint64_t g_step_trials = kDefaultStepTrials;
+std::atomic<uint64_t> g_step_trials{kDefaultStepTrials};  // read without the lock (bmpow_get_step_trials)
 
 int set_err(int code, const std::string& msg) {
   g_err = msg;
@@ -68,7 +69,6 @@ struct Shard {
   size_t item_cap = 0;
   // step bookkeeping
   uint32_t nitems = 0, nchunks = 0;
-  std::vector<uint32_t> item_obj;
   // min-trial probe: one bm_minpart per workgroup of a launch (grow-only)
   bm_minpart* d_parts = nullptr;
   bm_minpart* h_parts = nullptr;  // pinned
@@ -212,15 +212,7 @@ int init_locked() {
   return rc;
 }
 
-void pack_obj(const uint8_t* ih, uint64_t target, bm_obj* o) {
-  std::memset(o, 0, sizeof(*o));
-  for (int i = 0; i < 8; ++i) {
-    uint64_t v = 0;
-    for (int j = 0; j < 8; ++j) v = (v << 8) | ih[8 * i + j];
-    o->w[i] = v;
-  }
-  o->target = target;
-}
+using bmsched::pack_obj;
 
 }  // namespace
 
@@ -228,17 +220,7 @@ void pack_obj(const uint8_t* ih, uint64_t target, bm_obj* o) {
 // Batch state: the object table and per-object running minimum stay in HBM for the
 // lifetime of the batch (one copy per shard).
 // ---------------------------------------------------------------------------------------
-struct bmpow_batch {
-  size_t n = 0;    // slots in the table (objects, finished ones and free slots included)
-  size_t cap = 0;  // device allocation, in objects (grows geometrically with bmpow_batch_add)
-  std::vector<bm_obj> objs;
-  std::vector<uint64_t> next, nonce, trial;
-  std::vector<uint8_t> done;
-  size_t first_pending = 0;
-  size_t pending = 0;
-  std::vector<uint32_t> finished;  // slots finished since the last bmpow_batch_take_done, in order
-  size_t finished_head = 0;
-  std::vector<uint32_t> free_slots;  // slots released by bmpow_batch_take_done, reused by adds
+struct bmpow_batch : bmsched::BatchState {
   struct Dev {
     bm_obj* d_obj = nullptr;
     unsigned long long* d_best = nullptr;  // running minimum hit nonce (valid where d_found)
@@ -284,83 +266,36 @@ int batch_upload(bmpow_batch* b) {
 }
 
 int batch_init(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
-  b->n = n;
-  b->objs.resize(n);
-  b->next.resize(n);
-  b->nonce.assign(n, 0);
-  b->trial.assign(n, 0);
-  b->done.assign(n, BMPOW_PENDING);
-  for (size_t i = 0; i < n; ++i) {
-    pack_obj(ihs + 64 * i, targets[i], &b->objs[i]);
-    b->next[i] = start ? start[i] : 1;
-  }
-  b->first_pending = 0;
-  b->pending = n;
-  b->cap = n;
+  bmsched::init(*b, n, ihs, targets, start);
   return batch_upload(b);
 }
 
-void batch_mark_finished(bmpow_batch* b, uint32_t slot) {
-  if (b->finished_head > 4096 && b->finished_head * 2 > b->finished.size()) {  // drop the consumed prefix
-    b->finished.erase(b->finished.begin(), b->finished.begin() + b->finished_head);
-    b->finished_head = 0;
-  }
-  b->finished.push_back(slot);
-}
-
-// Append m objects to a live session between steps: released slots are reused first (LIFO), then
-// the table grows (device buffers reallocated at twice the size and re-uploaded from the host
-// mirror).  Only the slots written are uploaded, one copy per contiguous run.  Resetting best[]
-// and found[] over those runs is safe between steps: a pending object's device state is always
-// (UINT64_MAX, 0) there, since a hit finishes its object in the step that finds it.
+// Append m objects to a live session between steps (bmsched::add: released slots first, then the
+// table grows -- device buffers reallocated at twice the size and re-uploaded from the host
+// mirror).  Otherwise only the slots written are uploaded, one copy per contiguous run.
+// Resetting best[] and found[] over those runs is safe between steps: a pending object's device
+// state is always (UINT64_MAX, 0) there, since a hit finishes its object in the step that finds it.
 int batch_add_locked(bmpow_batch* b, size_t m, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
                      uint32_t* slot_out) {
   if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
   const size_t fresh = m > b->free_slots.size() ? m - b->free_slots.size() : 0;
   if (b->n + fresh > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many objects");
-  std::vector<uint32_t> slots(m);
-  const size_t n0 = b->n;
-  for (size_t i = 0; i < m; ++i) {
-    uint32_t slot;
-    if (!b->free_slots.empty()) {
-      slot = b->free_slots.back();
-      b->free_slots.pop_back();
-    } else {
-      slot = (uint32_t)b->n++;
-    }
-    slots[i] = slot;
-  }
-  if (b->n > n0) {
-    b->objs.resize(b->n);
-    b->next.resize(b->n);
-    b->nonce.resize(b->n);
-    b->trial.resize(b->n);
-    b->done.resize(b->n, BMPOW_FREE);
-  }
-  for (size_t i = 0; i < m; ++i) {
-    const uint32_t k = slots[i];
-    pack_obj(ihs + 64 * i, targets[i], &b->objs[k]);
-    b->next[k] = start ? start[i] : 1;
-    b->nonce[k] = b->trial[k] = 0;
-    b->done[k] = BMPOW_PENDING;
-    b->pending++;
-    if (k < b->first_pending) b->first_pending = k;
-    if (slot_out) slot_out[i] = k;
-  }
-  if (b->n > b->cap) {  // grow: fresh device buffers, everything re-uploaded
+  std::vector<uint32_t> slots;
+  const bool grew = bmsched::add(*b, m, ihs, targets, start, slots);
+  if (slot_out) std::copy(slots.begin(), slots.end(), slot_out);
+  if (grew) {
     b->cap = std::max<size_t>({b->n, 2 * b->cap, 1024});
     batch_free_dev(b);
     return batch_upload(b);
   }
-  std::vector<uint32_t> sorted(slots);
-  std::sort(sorted.begin(), sorted.end());
+  std::sort(slots.begin(), slots.end());
   for (size_t s = 0; s < g_shards.size(); ++s) {
     Shard& sh = g_shards[s];
     HIPTRY(hipSetDevice(sh.dev));
-    for (size_t i = 0; i < sorted.size();) {
+    for (size_t i = 0; i < slots.size();) {
       size_t j = i + 1;
-      while (j < sorted.size() && sorted[j] == sorted[j - 1] + 1) ++j;
-      const size_t lo = sorted[i], cnt = j - i;
+      while (j < slots.size() && slots[j] == slots[j - 1] + 1) ++j;
+      const size_t lo = slots[i], cnt = j - i;
       HIPTRY(hipMemcpyAsync(b->dev[s].d_obj + lo, b->objs.data() + lo, cnt * sizeof(bm_obj), hipMemcpyHostToDevice,
                             sh.stream));
       HIPTRY(hipMemsetAsync(b->dev[s].d_best + lo, 0xFF, cnt * sizeof(unsigned long long), sh.stream));
@@ -375,51 +310,19 @@ int batch_add_locked(bmpow_batch* b, size_t m, const uint8_t* ihs, const uint64_
   return 0;
 }
 
-// One object's contiguous nonce window in a step: `chunks` chunks from chunk index `chunk0` of the
-// step's flattened chunk list.
-struct Win {
-  uint32_t obj;
-  uint64_t start, count, chunks, chunk0;
-};
-
-// Cut the step's C chunks (windows in ascending chunk0) into S contiguous slices, one per shard, and
-// fill each shard's item list: big windows are nonce-sharded, small ones object-sharded.
-int slice_windows(const std::vector<Win>& wins, uint64_t C, uint64_t chunk) {
-  const size_t S = g_shards.size();
-  std::vector<uint64_t> cut(S + 1);
-  for (size_t s = 0; s <= S; ++s) cut[s] = C * s / S;
-  for (size_t s = 0; s < S; ++s) {
+// Stage the plan's per-shard item lists in the shards' pinned buffers (sized once per step, so
+// nothing written is ever reallocated under the copy).
+int stage_items(const bmsched::StepPlan& p) {
+  for (size_t s = 0; s < g_shards.size(); ++s) {
     Shard& sh = g_shards[s];
+    const std::vector<bm_item>& items = p.items[s];
     sh.nitems = 0;
-    sh.nchunks = (uint32_t)(cut[s + 1] - cut[s]);
-    sh.item_obj.clear();
+    const int rc = ensure_items(sh, std::max<size_t>(items.size(), 1));
+    if (rc < 0) return rc;
+    if (!items.empty()) std::memcpy(sh.h_items, items.data(), items.size() * sizeof(bm_item));
+    sh.nitems = (uint32_t)items.size();
+    sh.nchunks = p.nchunks[s];
   }
-  // items per shard
-  {
-    size_t s = 0;
-    for (const Win& w : wins) {
-      uint64_t c = w.chunk0;
-      const uint64_t cend = w.chunk0 + w.chunks;
-      while (c < cend) {
-        while (s < S && cut[s + 1] <= c) ++s;
-        const uint64_t seg_end = std::min(cend, cut[s + 1]);
-        Shard& sh = g_shards[s];
-        int rc = ensure_items(sh, sh.nitems + 1);
-        if (rc < 0) return rc;
-        bm_item& it = sh.h_items[sh.nitems];
-        const uint64_t off = (c - w.chunk0) * chunk;
-        it.start = w.start + off;
-        it.count = std::min<uint64_t>(w.count - off, (seg_end - c) * chunk);
-        it.obj = w.obj;
-        it.chunk_base = (uint32_t)(c - cut[s]);
-        it.pad = 0;
-        sh.item_obj.push_back(w.obj);
-        sh.nitems++;
-        c = seg_end;
-      }
-    }
-  }
-
   return 0;
 }
 
@@ -428,36 +331,13 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
   if (trials_out) *trials_out = 0;
   if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
   if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
-  while (b->first_pending < b->n && b->done[b->first_pending] != BMPOW_PENDING) ++b->first_pending;
-  if (b->pending == 0) return 0;
   const size_t S = g_shards.size();
-  if (budget == 0) budget = g_step_trials * S;
-  budget = std::min<uint64_t>(budget, (uint64_t)S << 36);  // grid.x stays far below 2^31
-  // workgroup size in nonces: short rounds for small steps (below ~6 full rounds of the chip
-  // per shard), full chunks otherwise
-  const uint32_t iters = budget < ((uint64_t)1 << 26) * S ? BM_ITERS_SMALL : BM_ITERS;
-  const uint64_t chunk = (uint64_t)BM_BLOCK * iters;
-  uint64_t total_chunks = std::max<uint64_t>(budget / chunk, S);
-
-  // 1. windows: pending objects in index order, k chunks each
-  std::vector<Win> wins;
-  const uint64_t k = std::max<uint64_t>(1, total_chunks / b->pending);
-  uint64_t chunk_acc = 0;
-  for (size_t i = b->first_pending; i < b->n && chunk_acc < total_chunks; ++i) {
-    if (b->done[i] != BMPOW_PENDING) continue;
-    const uint64_t st = b->next[i];
-    uint64_t want = k * chunk;
-    const uint64_t room = kU64Max - st;  // nonces remaining after st
-    if (room < want - 1) want = room + 1;   // st + want - 1 <= 2^64-1
-    const uint64_t ch = (want + chunk - 1) / chunk;
-    wins.push_back({(uint32_t)i, st, want, ch, chunk_acc});
-    chunk_acc += ch;
-  }
-  const uint64_t C = chunk_acc;
-
-  // 2. slice the chunk list over shards
+  // 1-2. windows for the pending objects, sliced over the shards (bmpow_sched.cpp)
+  bmsched::StepPlan plan;
+  if (!bmsched::plan_step(*b, budget, g_step_trials, S, plan)) return 0;
+  const uint32_t iters = plan.iters;
   {
-    const int rc = slice_windows(wins, C, chunk);
+    const int rc = stage_items(plan);
     if (rc < 0) return rc;
   }
 
@@ -499,49 +379,10 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
   g_stats.max_shard_kernel_ms = mx;
   if (trials_out) *trials_out = step_trials;
 
-  // 4. host min-reduction over shards per object (hit[] marks a hit: kU64Max is a legal nonce)
-  std::vector<uint64_t> bestn(wins.size(), kU64Max), bestt(wins.size(), 0);
-  std::vector<uint8_t> hit(wins.size(), 0);
-  // wins are in ascending object order: map obj -> win index by binary search
-  auto win_of = [&](uint32_t obj) {
-    size_t lo = 0, hi = wins.size();
-    while (hi - lo > 1) {
-      size_t mid = (lo + hi) / 2;
-      if (wins[mid].obj <= obj) lo = mid; else hi = mid;
-    }
-    return lo;
-  };
-  for (size_t s = 0; s < S; ++s) {
-    Shard& sh = g_shards[s];
-    for (uint32_t k2 = 0; k2 < sh.nitems; ++k2) {
-      const bm_result& r = sh.h_res[k2];
-      if (!r.found) continue;
-      const size_t wi = win_of(sh.item_obj[k2]);
-      if (!hit[wi] || r.nonce < bestn[wi]) {
-        hit[wi] = 1;
-        bestn[wi] = r.nonce;
-        bestt[wi] = r.trial;
-      }
-    }
-  }
-  for (size_t wi = 0; wi < wins.size(); ++wi) {
-    const Win& w = wins[wi];
-    if (hit[wi]) {
-      b->done[w.obj] = BMPOW_DONE_FOUND;
-      b->nonce[w.obj] = bestn[wi];
-      b->trial[w.obj] = bestt[wi];
-      b->next[w.obj] = bestn[wi] == kU64Max ? kU64Max : bestn[wi] + 1;
-      b->pending--;
-      batch_mark_finished(b, w.obj);
-    } else if (w.count - 1 == kU64Max - w.start) {
-      b->done[w.obj] = BMPOW_DONE_EXHAUSTED;
-      b->next[w.obj] = kU64Max;
-      b->pending--;
-      batch_mark_finished(b, w.obj);
-    } else {
-      b->next[w.obj] = w.start + w.count;
-    }
-  }
+  // 4. host min-reduction over shards per object (bmpow_sched.cpp)
+  std::vector<const bm_result*> res(S);
+  for (size_t s = 0; s < S; ++s) res[s] = g_shards[s].h_res;
+  bmsched::apply_step(*b, plan, res);
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
@@ -570,16 +411,9 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
   if (n > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many objects");
   const size_t S = g_shards.size();
   std::vector<bm_obj> objs(n);
-  std::vector<uint64_t> cur(n), left(n);
-  std::vector<uint8_t> any(n, 0);
-  for (size_t i = 0; i < n; ++i) {
-    pack_obj(ihs + 64 * i, 0, &objs[i]);
-    cur[i] = start[i];
-    left[i] = count[i];
-    if (left[i] && left[i] - 1 > kU64Max - start[i]) left[i] = kU64Max - start[i] + 1;  // stop at 2^64-1
-    min_out[i] = kU64Max;
-    argmin_out[i] = start[i];
-  }
+  for (size_t i = 0; i < n; ++i) pack_obj(ihs + 64 * i, 0, &objs[i]);
+  bmsched::MinTrial mt;
+  mt.init(n, start, count, min_out, argmin_out);
   std::vector<bm_obj*> d_obj(S, nullptr);
   auto release = [&]() {
     for (size_t s = 0; s < S; ++s)
@@ -597,27 +431,17 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
       e = hipMemcpyAsync(d_obj[s], objs.data(), n * sizeof(bm_obj), hipMemcpyHostToDevice, sh.stream);
     if (e != hipSuccess) rc = set_err(BMPOW_E_HIP, std::string("min-trial upload: ") + hipGetErrorString(e));
   }
-  const uint64_t chunk = BM_CHUNK;
-  const uint64_t total_chunks = std::max<uint64_t>(g_step_trials * S / chunk, S);
-  size_t first = 0;
+  const uint64_t total_chunks = std::max<uint64_t>(g_step_trials * S / BM_CHUNK, S);
+  bmsched::StepPlan plan;
   while (rc == 0) {
     if (g_abort.load()) {
       rc = set_err(BMPOW_E_ABORTED, "aborted");
       break;
     }
-    while (first < n && left[first] == 0) ++first;
-    if (first == n) break;
-    std::vector<Win> wins;
-    uint64_t acc = 0;
-    for (size_t i = first; i < n && acc < total_chunks; ++i) {
-      if (left[i] == 0) continue;
-      const uint64_t room = (total_chunks - acc) * chunk;
-      const uint64_t want = std::min(left[i], room);
-      const uint64_t ch = (want + chunk - 1) / chunk;
-      wins.push_back({(uint32_t)i, cur[i], want, ch, acc});
-      acc += ch;
-    }
-    rc = slice_windows(wins, acc, chunk);
+    uint64_t C = 0;
+    if (!mt.plan(total_chunks, plan.wins, C)) break;
+    bmsched::slice(plan.wins, C, BM_CHUNK, S, plan);
+    rc = stage_items(plan);
     if (rc < 0) break;
     for (size_t s = 0; s < S && rc == 0; ++s) {
       Shard& sh = g_shards[s];
@@ -648,27 +472,11 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
         break;
       }
       g_stats.probe_kernel_ms += ms;
-      for (uint32_t k = 0; k < sh.nitems; ++k) {
-        const bm_item& it = sh.h_items[k];
-        const uint64_t nch = (it.count + chunk - 1) / chunk;
-        for (uint64_t c = it.chunk_base; c < it.chunk_base + nch; ++c) {
-          const bm_minpart& p = sh.h_parts[c];
-          uint64_t& mt = min_out[it.obj];
-          uint64_t& mn = argmin_out[it.obj];
-          if (!any[it.obj] || p.trial < mt || (p.trial == mt && p.nonce < mn)) {
-            any[it.obj] = 1;
-            mt = p.trial;
-            mn = p.nonce;
-          }
-        }
-      }
+      mt.reduce_parts(plan.items[s], sh.h_parts, min_out, argmin_out);
     }
     if (rc < 0) break;
-    for (const Win& w : wins) {
-      left[w.obj] -= w.count;
-      g_stats.probe_trials += w.count;
-      if (left[w.obj]) cur[w.obj] += w.count;
-    }
+    for (const bmsched::Win& w : plan.wins) g_stats.probe_trials += w.count;
+    mt.advance(plan.wins);
   }
   release();
   return rc;
@@ -700,10 +508,7 @@ int scratch_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, const u
 // ---------------------------------------------------------------------------------------
 struct bmpow_vbatch {
   size_t n = 0;
-  struct Part {
-    size_t shard = 0;
-    std::vector<uint32_t> orig;  // sorted position -> input index
-    uint64_t blocks = 0;
+  struct Part : bmsched::VPart {  // shard, sorted order, bv_obj list, blocks (bmpow_sched.h)
     bv_obj* d_obj = nullptr;
     uint4* d_pool = nullptr;
     uint64_t* d_pow = nullptr;
@@ -716,31 +521,8 @@ struct bmpow_vbatch {
 
 namespace {
 
-struct Span {
-  const uint8_t* p;
-  uint64_t len;  // >= 8
-};
-
-uint64_t load_be64(const uint8_t* p) {
-  uint64_t v = 0;
-  for (int j = 0; j < 8; ++j) v = (v << 8) | p[j];
-  return v;
-}
-
-// blocks of SHA-512 padding for an m-byte message: m + 1 (0x80) + 16 (bit length) rounded up
-uint64_t padded_blocks(uint64_t m) { return (m + 17 + 127) / 128; }
-
-void pad_into(const uint8_t* msg, uint64_t m, uint8_t* dst, uint64_t nblk) {
-  const uint64_t total = nblk * 128;
-  std::memcpy(dst, msg, m);
-  std::memset(dst + m, 0, total - m);
-  dst[m] = 0x80;
-  const uint64_t bits_lo = m << 3, bits_hi = m >> 61;  // 128-bit big-endian bit length
-  for (int j = 0; j < 8; ++j) {
-    dst[total - 16 + j] = (uint8_t)(bits_hi >> (56 - 8 * j));
-    dst[total - 8 + j] = (uint8_t)(bits_lo >> (56 - 8 * j));
-  }
-}
+using bmsched::load_be64;
+using bmsched::Span;
 
 void vbatch_free(bmpow_vbatch* vb) {
   for (auto& pt : vb->parts) {
@@ -752,29 +534,6 @@ void vbatch_free(bmpow_vbatch* vb) {
     if (pt.h_pow) (void)hipHostFree(pt.h_pow);
   }
   vb->parts.clear();
-}
-
-// Pad objects [j0, j1) of a part (sorted order) into dst (their blocks from blk0 on), over up to 16
-// host threads: a memory-bound copy of every payload.
-void pad_range(const std::vector<Span>& objs, const bmpow_vbatch::Part& pt, const std::vector<bv_obj>& ho,
-               size_t j0, size_t j1, uint64_t blk0, uint8_t* dst) {
-  if (j1 <= j0) return;
-  const size_t m = j1 - j0;
-  const uint64_t bytes = (uint64_t)(ho[j1 - 1].blk + ho[j1 - 1].nblk - ho[j0].blk) * 128;
-  // a thread per ~2 MB (and per >= 64 objects), at most 16
-  const size_t nth = std::max<size_t>(
-      1, std::min<size_t>({16, std::thread::hardware_concurrency(), bytes / (2u << 20) + 1, m / 64 + 1}));
-  auto work = [&](size_t t) {
-    for (size_t j = j0 + m * t / nth; j < j0 + m * (t + 1) / nth; ++j) {
-      const Span& sp = objs[pt.orig[j]];
-      pad_into(sp.p + 8, sp.len - 8, dst + (uint64_t)(ho[j].blk - blk0) * 128, ho[j].nblk);
-    }
-  };
-  if (nth == 1) return work(0);
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < nth; ++t) th.emplace_back(work, t);
-  work(0);
-  for (auto& x : th) x.join();
 }
 
 template <typename T>
@@ -792,8 +551,8 @@ constexpr uint64_t kVStageBytes = 64ull << 20;  // pinned staging chunk (x2 per 
 
 // One-shot path: the part's pool goes up through the shard's two pinned staging chunks, padding of
 // chunk c+1 overlapping the DMA of chunk c; device buffers are the shard's, reused across calls.
-int vbatch_upload_transient(bmpow_vbatch::Part& pt, const std::vector<Span>& objs, const std::vector<bv_obj>& ho,
-                            const std::vector<uint32_t>& nblk) {
+int vbatch_upload_transient(bmpow_vbatch::Part& pt, const std::vector<Span>& objs) {
+  const std::vector<bv_obj>& ho = pt.ho;
   Shard& sh = g_shards[pt.shard];
   const size_t m = pt.orig.size();
   if (m > sh.vobj_cap || !sh.d_vobj) {
@@ -835,8 +594,8 @@ int vbatch_upload_transient(bmpow_vbatch::Part& pt, const std::vector<Span>& obj
     const uint64_t blk0 = ho[j].blk;
     size_t j1 = j;
     uint64_t bytes = 0;
-    while (j1 < m && (j1 == j || bytes + (uint64_t)nblk[pt.orig[j1]] * 128 <= kVStageBytes)) {
-      bytes += (uint64_t)nblk[pt.orig[j1]] * 128;
+    while (j1 < m && (j1 == j || bytes + (uint64_t)ho[j1].nblk * 128 <= kVStageBytes)) {
+      bytes += (uint64_t)ho[j1].nblk * 128;
       ++j1;
     }
     uint8_t* dst;
@@ -847,7 +606,7 @@ int vbatch_upload_transient(bmpow_vbatch::Part& pt, const std::vector<Span>& obj
       if (used[c]) HIPTRY(hipEventSynchronize(sh.ev_vstage[c]));  // its previous DMA is done
       dst = sh.h_vstage[c];
     }
-    pad_range(objs, pt, ho, j, j1, blk0, dst);
+    bmsched::pad_range(objs, pt, j, j1, blk0, dst);
     HIPTRY(hipMemcpyAsync((uint8_t*)pt.d_pool + blk0 * 128, dst, bytes, hipMemcpyHostToDevice, sh.stream));
     if (dst == big.get()) {
       HIPTRY(hipStreamSynchronize(sh.stream));
@@ -863,63 +622,29 @@ int vbatch_upload_transient(bmpow_vbatch::Part& pt, const std::vector<Span>& obj
 }
 
 int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs, bool transient = false) {
-  const size_t n = objs.size();
-  if (n > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many objects");
-  vb->n = n;
-  std::vector<uint32_t> nblk(n);
-  uint64_t total = 0;
-  for (size_t i = 0; i < n; ++i) {
-    const uint64_t b = padded_blocks(objs[i].len - 8);
-    if (b > 0xffffffffULL) return set_err(BMPOW_E_ARG, "object too large");
-    nblk[i] = (uint32_t)b;
-    total += b;
-  }
-  if (total > 0xffffffffULL) return set_err(BMPOW_E_ARG, "payload pool above 2^32 blocks (512 GiB)");
-  vb->blocks = total;
-  std::vector<uint32_t> order(n);
-  for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return nblk[a] > nblk[b]; });
-  const size_t S = g_shards.size();
-  size_t k = 0;
-  uint64_t acc = 0;
-  for (size_t s = 0; s < S && k < n; ++s) {
-    bmpow_vbatch::Part pt;
-    pt.shard = s;
-    const uint64_t goal = total * (s + 1) / S;
-    while (k < n && (acc < goal || s == S - 1)) {
-      pt.orig.push_back(order[k]);
-      pt.blocks += nblk[order[k]];
-      acc += nblk[order[k]];
-      ++k;
-    }
-    if (!pt.orig.empty()) vb->parts.push_back(std::move(pt));
-  }
+  vb->n = objs.size();
+  std::vector<bmsched::VPart> plan;
+  if (bmsched::plan_verify(objs, g_shards.size(), plan, vb->blocks) < 0)
+    return set_err(BMPOW_E_ARG, "too many objects, an object too large, or a payload pool above 2^32 blocks");
+  vb->parts.resize(plan.size());
+  for (size_t i = 0; i < plan.size(); ++i) static_cast<bmsched::VPart&>(vb->parts[i]) = std::move(plan[i]);
   for (auto& pt : vb->parts) {
     Shard& sh = g_shards[pt.shard];
     HIPTRY(hipSetDevice(sh.dev));
     const size_t m = pt.orig.size();
-    std::vector<bv_obj> ho(m);
-    uint64_t blk = 0;
-    for (size_t j = 0; j < m; ++j) {
-      const uint32_t nb = nblk[pt.orig[j]];
-      ho[j].blk = (uint32_t)blk;
-      ho[j].nblk = nb;
-      ho[j].nonce = load_be64(objs[pt.orig[j]].p);
-      blk += nb;
-    }
     if (transient) {
-      const int rc = vbatch_upload_transient(pt, objs, ho, nblk);
+      const int rc = vbatch_upload_transient(pt, objs);
       if (rc < 0) return rc;
       continue;
     }
     // padding is a memory-bound copy of every payload: spread it over host threads
     std::unique_ptr<uint8_t[]> pool(new uint8_t[pt.blocks * 128]);  // pad_into writes every byte
-    pad_range(objs, pt, ho, 0, m, 0, pool.get());
+    bmsched::pad_range(objs, pt, 0, m, 0, pool.get());
     HIPTRY(hipMalloc(&pt.d_obj, m * sizeof(bv_obj)));
     HIPTRY(hipMalloc(&pt.d_pool, std::max<size_t>(pt.blocks * 128, 16)));
     HIPTRY(hipMalloc(&pt.d_pow, m * sizeof(uint64_t)));
     HIPTRY(hipHostMalloc(&pt.h_pow, m * sizeof(uint64_t), hipHostMallocDefault));
-    HIPTRY(hipMemcpy(pt.d_obj, ho.data(), m * sizeof(bv_obj), hipMemcpyHostToDevice));
+    HIPTRY(hipMemcpy(pt.d_obj, pt.ho.data(), m * sizeof(bv_obj), hipMemcpyHostToDevice));
     HIPTRY(hipMemcpy(pt.d_pool, pool.get(), pt.blocks * 128, hipMemcpyHostToDevice));
   }
   return 0;
@@ -962,24 +687,7 @@ int spans_from(size_t n, const uint8_t* objs, const uint64_t* offsets, std::vect
   return 0;
 }
 
-// protocol.isProofOfWorkSufficient's comparison (src/protocol.py:272-286) in the reference's
-// arithmetic: Python ints until the true division by 2**16 (correctly rounded: the exact
-// 128-bit product converted once, then an exact power-of-two scale), IEEE doubles after,
-// and an exact int-vs-float comparison at the end.
-int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, int64_t recv, uint64_t eol) {
-  if (ntpb < 1000) ntpb = 1000;
-  if (extra < 1000) extra = 1000;
-  __int128 ttl = (__int128)eol - (__int128)recv;
-  if (ttl < 300) ttl = 300;
-  const unsigned __int128 le = (unsigned __int128)len + extra;
-  const unsigned __int128 prod = (unsigned __int128)ttl * le;
-  const double q = (double)prod / 65536.0;
-  const double x = (double)le + q;
-  const double y = (double)ntpb * x;
-  const double t = 18446744073709551616.0 / y;
-  if (t >= 18446744073709551616.0) return 1;
-  return pow <= (uint64_t)t ? 1 : 0;
-}
+using bmsched::pow_sufficient;
 
 }  // namespace
 
@@ -1305,7 +1013,7 @@ int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t
   if (rc < 0) return rc;
   bmpow_batch* b = g_scratch;
   uint64_t left = max_trials;
-  const uint64_t full = g_step_trials * g_shards.size();
+  const uint64_t full = g_step_trials.load() * g_shards.size();
   // The first step is sized to the object's expected trial count, 2^64 / (target + 1): an easy
   // object does not launch (and drain) a full grid.  Steps then double up to the default; they
   // cover consecutive windows, so exactness is unaffected.
@@ -1376,7 +1084,7 @@ int bmpow_search_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, ui
   int pending = (int)b->pending;
   while (pending > 0 && spent < budget) {
     uint64_t t = 0;
-    pending = batch_step_locked(b, std::min(budget - spent, g_step_trials * g_shards.size()), &t);
+    pending = batch_step_locked(b, std::min<uint64_t>(budget - spent, g_step_trials.load() * g_shards.size()), &t);
     if (pending < 0) return pending;
     spent += std::max<uint64_t>(t, BM_CHUNK);
   }
@@ -1435,17 +1143,7 @@ int bmpow_batch_reset(bmpow_batch* b, const uint64_t* start) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
-  b->pending = 0;
-  for (size_t i = 0; i < b->n; ++i) {
-    b->next[i] = start ? start[i] : 1;
-    b->nonce[i] = b->trial[i] = 0;
-    if (b->done[i] == BMPOW_FREE) continue;  // released slots stay free
-    b->done[i] = BMPOW_PENDING;
-    b->pending++;
-  }
-  b->first_pending = 0;
-  b->finished.clear();
-  b->finished_head = 0;
+  bmsched::reset(*b, start);
   for (size_t s = 0; s < g_shards.size(); ++s) {
     Shard& sh = g_shards[s];
     HIPTRY(hipSetDevice(sh.dev));
@@ -1463,16 +1161,7 @@ int bmpow_batch_set_pending(bmpow_batch* b, size_t first, size_t count, int pend
   std::lock_guard<std::mutex> lk(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (first > b->n || count > b->n - first) return set_err(BMPOW_E_ARG, "range outside the batch");
-  for (size_t i = first; i < first + count; ++i) {
-    if (pending && b->done[i] == BMPOW_PARKED) {
-      b->done[i] = BMPOW_PENDING;
-      b->pending++;
-    } else if (!pending && b->done[i] == BMPOW_PENDING) {
-      b->done[i] = BMPOW_PARKED;
-      b->pending--;
-    }
-  }
-  if (pending && first < b->first_pending) b->first_pending = first;
+  bmsched::set_pending(*b, first, count, pending != 0);
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
@@ -1492,22 +1181,7 @@ int bmpow_batch_take_done(bmpow_batch* b, size_t cap, uint32_t* slot_out, uint64
   std::lock_guard<std::mutex> lk(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (cap && !slot_out) return set_err(BMPOW_E_ARG, "null pointer");
-  size_t k = 0;
-  cap = std::min<size_t>(cap, 0x7fffffff);
-  while (k < cap && b->finished_head < b->finished.size()) {
-    const uint32_t s = b->finished[b->finished_head++];
-    slot_out[k] = s;
-    if (nonce_out) nonce_out[k] = b->nonce[s];
-    if (trial_out) trial_out[k] = b->trial[s];
-    if (done_out) done_out[k] = b->done[s];
-    b->done[s] = BMPOW_FREE;
-    b->free_slots.push_back(s);
-    ++k;
-  }
-  if (b->finished_head == b->finished.size()) {
-    b->finished.clear();
-    b->finished_head = 0;
-  }
+  const size_t k = bmsched::take_done(*b, std::min<size_t>(cap, 0x7fffffff), slot_out, nonce_out, trial_out, done_out);
   return (int)k;
 }
 
@@ -1749,11 +1423,11 @@ void bmpow_reset_stats(void) {
   for (auto& s : g_shards) s.kernel_ms = 0;
 }
 
-uint64_t bmpow_get_step_trials(void) { return g_step_trials; }
+uint64_t bmpow_get_step_trials(void) { return g_step_trials.load(); }
 
 void bmpow_set_step_trials(uint64_t t) {
   std::lock_guard<std::mutex> lk(g_mu);
-  g_step_trials = std::max<uint64_t>(t, BM_CHUNK);
+  g_step_trials.store(std::max<uint64_t>(t, BM_CHUNK));
 }
 
 unsigned long long BitmessagePOW(unsigned char* starthash, unsigned long long target) {

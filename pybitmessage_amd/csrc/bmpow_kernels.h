@@ -3,58 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "bmpow_layout.h"
 #include "secp256k1_dev.h"
-
-// One workgroup = BM_BLOCK lanes x iters nonces = one CHUNK of a work item.  Full steps use
-// BM_ITERS iterations per workgroup; small steps (a single easy object) use BM_ITERS_SMALL so a
-// "round" of resident workgroups is short and the answer is reached sooner.  BM_CHUNK (the full
-// chunk) is a multiple of every chunk size, so windows rounded to it fit either.
-#ifndef BM_ITERS
-#define BM_ITERS 32
-#endif
-#define BM_ITERS_SMALL 4
-#define BM_BLOCK 256
-#define BM_CHUNK ((uint64_t)BM_BLOCK * BM_ITERS)
-
-// Per-object record, device resident for the life of a batch (128 B, one per object).
-struct bm_obj {
-  uint64_t w[8];     // initialHash as 8 big-endian words = W1..W8 of SHA-512 block 1
-  uint64_t target;   // accept trial <= target
-  uint64_t pad[7];
-};
-
-// Work item = one object's contiguous nonce window inside one launch (32 B).
-struct bm_item {
-  uint64_t start;       // first nonce of the window
-  uint64_t count;       // trials in the window (> 0; start + count - 1 <= 2^64 - 1)
-  uint32_t obj;         // object index (into bm_obj[] and best[])
-  uint32_t chunk_base;  // first chunk (workgroup) index of this item in the launch
-  uint64_t pad;
-};
-
-struct bm_result {
-  uint64_t nonce;  // the object's minimum hit so far (meaningful only when found)
-  uint64_t trial;
-  uint32_t found;  // 1: the object has a hit (nonce 2^64-1 included); 0: none yet
-  uint32_t pad;
-};
-
-// One workgroup's minimum of the min-trial probe: the lowest trial value over its chunk and the
-// first nonce reaching it.
-struct bm_minpart {
-  uint64_t trial;
-  uint64_t nonce;
-};
-
-// Receive-side verification (bv_*): one finished object (nonce || payload) per lane.  The
-// payload is stored SHA-512-padded in a pool of 128-B blocks; objects are sorted by block
-// count (descending) on the host so the lanes of a wave loop the same number of times.
-#define BV_BLOCK 64
-struct bv_obj {
-  uint32_t blk;    // first 128-B block of the padded payload in the pool
-  uint32_t nblk;   // padded blocks (>= 1)
-  uint64_t nonce;  // BE64(object[0:8])
-};
 
 hipError_t bv_launch_pow(hipStream_t st, const bv_obj* objs, uint32_t n, const uint4* pool, uint64_t* pow_out);
 

@@ -52,7 +52,12 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __res
   const bm_obj* o = objs + it.obj;
   uint64_t ihw[8];
 #pragma unroll
-  for (int i = 0; i < 8; ++i) ihw[i] = o->w[i];
+  for (int i = 0; i < 8; ++i) {
+    ihw[i] = o->w[i];
+#ifdef BM_IHW_VGPR
+    asm volatile("" : "+v"(ihw[i]));  // A/B variant: per-object words (and what is hoisted from them) in VGPRs
+#endif
+  }
   const uint64_t target = o->target;
 
   uint32_t done = 0;

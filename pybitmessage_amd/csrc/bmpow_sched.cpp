@@ -1,0 +1,392 @@
+// bmpow_sched.cpp -- host-only scheduler logic of libbmpow_hip.so (see bmpow_sched.h).  No HIP:
+// compiled into the library by hipcc and, for tests/native/, by g++ under the sanitizers.
+#include "bmpow_sched.h"
+
+#include <algorithm>
+#include <cstring>
+#include <thread>
+
+namespace bmsched {
+
+uint64_t load_be64(const uint8_t* p) {
+  uint64_t v = 0;
+  for (int j = 0; j < 8; ++j) v = (v << 8) | p[j];
+  return v;
+}
+
+void pack_obj(const uint8_t* ih, uint64_t target, bm_obj* o) {
+  std::memset(o, 0, sizeof(*o));
+  for (int i = 0; i < 8; ++i) o->w[i] = load_be64(ih + 8 * i);
+  o->target = target;
+}
+
+// ---------------------------------------------------------------------------------------
+// sessions
+// ---------------------------------------------------------------------------------------
+void init(BatchState& b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
+  b = BatchState();
+  b.n = n;
+  b.objs.resize(n);
+  b.next.resize(n);
+  b.nonce.assign(n, 0);
+  b.trial.assign(n, 0);
+  b.done.assign(n, BMPOW_PENDING);
+  for (size_t i = 0; i < n; ++i) {
+    pack_obj(ihs + 64 * i, targets[i], &b.objs[i]);
+    b.next[i] = start ? start[i] : 1;
+  }
+  b.pending = n;
+  b.cap = n;
+}
+
+namespace {
+
+void mark_finished(BatchState& b, uint32_t slot) {
+  if (b.finished_head > 4096 && b.finished_head * 2 > b.finished.size()) {  // drop the consumed prefix
+    b.finished.erase(b.finished.begin(), b.finished.begin() + (ptrdiff_t)b.finished_head);
+    b.finished_head = 0;
+  }
+  b.finished.push_back(slot);
+}
+
+}  // namespace
+
+bool add(BatchState& b, size_t m, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
+         std::vector<uint32_t>& slots) {
+  slots.resize(m);
+  const size_t n0 = b.n;
+  for (size_t i = 0; i < m; ++i) {
+    if (!b.free_slots.empty()) {
+      slots[i] = b.free_slots.back();
+      b.free_slots.pop_back();
+    } else {
+      slots[i] = (uint32_t)b.n++;
+    }
+  }
+  if (b.n > n0) {
+    b.objs.resize(b.n);
+    b.next.resize(b.n);
+    b.nonce.resize(b.n);
+    b.trial.resize(b.n);
+    b.done.resize(b.n, BMPOW_FREE);
+  }
+  for (size_t i = 0; i < m; ++i) {
+    const uint32_t k = slots[i];
+    pack_obj(ihs + 64 * i, targets[i], &b.objs[k]);
+    b.next[k] = start ? start[i] : 1;
+    b.nonce[k] = b.trial[k] = 0;
+    b.done[k] = BMPOW_PENDING;
+    b.pending++;
+    if (k < b.first_pending) b.first_pending = k;
+  }
+  return b.n > b.cap;
+}
+
+size_t take_done(BatchState& b, size_t cap, uint32_t* slot_out, uint64_t* nonce_out, uint64_t* trial_out,
+                 uint8_t* done_out) {
+  size_t k = 0;
+  while (k < cap && b.finished_head < b.finished.size()) {
+    const uint32_t s = b.finished[b.finished_head++];
+    slot_out[k] = s;
+    if (nonce_out) nonce_out[k] = b.nonce[s];
+    if (trial_out) trial_out[k] = b.trial[s];
+    if (done_out) done_out[k] = b.done[s];
+    b.done[s] = BMPOW_FREE;
+    b.free_slots.push_back(s);
+    ++k;
+  }
+  if (b.finished_head == b.finished.size()) {
+    b.finished.clear();
+    b.finished_head = 0;
+  }
+  return k;
+}
+
+void reset(BatchState& b, const uint64_t* start) {
+  b.pending = 0;
+  for (size_t i = 0; i < b.n; ++i) {
+    b.next[i] = start ? start[i] : 1;
+    b.nonce[i] = b.trial[i] = 0;
+    if (b.done[i] == BMPOW_FREE) continue;  // released slots stay free
+    b.done[i] = BMPOW_PENDING;
+    b.pending++;
+  }
+  b.first_pending = 0;
+  b.finished.clear();
+  b.finished_head = 0;
+}
+
+void set_pending(BatchState& b, size_t first, size_t count, bool pending) {
+  for (size_t i = first; i < first + count; ++i) {
+    if (pending && b.done[i] == BMPOW_PARKED) {
+      b.done[i] = BMPOW_PENDING;
+      b.pending++;
+    } else if (!pending && b.done[i] == BMPOW_PENDING) {
+      b.done[i] = BMPOW_PARKED;
+      b.pending--;
+    }
+  }
+  if (pending && first < b.first_pending) b.first_pending = first;
+}
+
+// ---------------------------------------------------------------------------------------
+// search steps
+// ---------------------------------------------------------------------------------------
+void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p) {
+  std::vector<uint64_t> cut(S + 1);
+  for (size_t s = 0; s <= S; ++s) cut[s] = C * s / S;
+  p.items.assign(S, std::vector<bm_item>());
+  p.nchunks.assign(S, 0);
+  for (size_t s = 0; s < S; ++s) p.nchunks[s] = (uint32_t)(cut[s + 1] - cut[s]);
+  size_t s = 0;
+  for (const Win& w : wins) {
+    uint64_t c = w.chunk0;
+    const uint64_t cend = w.chunk0 + w.chunks;
+    while (c < cend) {
+      while (s < S && cut[s + 1] <= c) ++s;
+      const uint64_t seg_end = std::min(cend, cut[s + 1]);
+      bm_item it;
+      const uint64_t off = (c - w.chunk0) * chunk;
+      it.start = w.start + off;
+      it.count = std::min<uint64_t>(w.count - off, (seg_end - c) * chunk);
+      it.obj = w.obj;
+      it.chunk_base = (uint32_t)(c - cut[s]);
+      it.pad = 0;
+      p.items[s].push_back(it);
+      c = seg_end;
+    }
+  }
+}
+
+bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p) {
+  while (b.first_pending < b.n && b.done[b.first_pending] != BMPOW_PENDING) ++b.first_pending;
+  if (b.pending == 0) return false;
+  if (budget == 0) budget = step_trials * S;
+  budget = std::min<uint64_t>(budget, (uint64_t)S << 36);  // grid.x stays far below 2^31
+  // workgroup size in nonces: short rounds for small steps (below ~6 full rounds of the chip
+  // per shard), full chunks otherwise
+  p.iters = budget < ((uint64_t)1 << 26) * S ? BM_ITERS_SMALL : BM_ITERS;
+  p.chunk = (uint64_t)BM_BLOCK * p.iters;
+  const uint64_t total_chunks = std::max<uint64_t>(budget / p.chunk, S);
+  // windows: pending objects in slot order, k chunks each
+  p.wins.clear();
+  const uint64_t k = std::max<uint64_t>(1, total_chunks / b.pending);
+  uint64_t acc = 0;
+  for (size_t i = b.first_pending; i < b.n && acc < total_chunks; ++i) {
+    if (b.done[i] != BMPOW_PENDING) continue;
+    const uint64_t st = b.next[i];
+    uint64_t want = k * p.chunk;
+    const uint64_t room = kU64Max - st;  // nonces remaining after st
+    if (room < want - 1) want = room + 1;   // st + want - 1 <= 2^64-1
+    const uint64_t ch = (want + p.chunk - 1) / p.chunk;
+    p.wins.push_back({(uint32_t)i, st, want, ch, acc});
+    acc += ch;
+  }
+  p.C = acc;
+  slice(p.wins, p.C, p.chunk, S, p);
+  return true;
+}
+
+void apply_step(BatchState& b, const StepPlan& p, const std::vector<const bm_result*>& res) {
+  const std::vector<Win>& wins = p.wins;
+  std::vector<uint64_t> bestn(wins.size(), kU64Max), bestt(wins.size(), 0);
+  std::vector<uint8_t> hit(wins.size(), 0);  // kU64Max is a legal nonce: hits are flagged, not encoded
+  // wins are in ascending object order: obj -> win index by binary search
+  auto win_of = [&](uint32_t obj) {
+    size_t lo = 0, hi = wins.size();
+    while (hi - lo > 1) {
+      const size_t mid = (lo + hi) / 2;
+      if (wins[mid].obj <= obj) lo = mid; else hi = mid;
+    }
+    return lo;
+  };
+  for (size_t s = 0; s < p.items.size(); ++s) {
+    const std::vector<bm_item>& items = p.items[s];
+    for (size_t k = 0; k < items.size(); ++k) {
+      const bm_result& r = res[s][k];
+      if (!r.found) continue;
+      const size_t wi = win_of(items[k].obj);
+      if (!hit[wi] || r.nonce < bestn[wi]) {
+        hit[wi] = 1;
+        bestn[wi] = r.nonce;
+        bestt[wi] = r.trial;
+      }
+    }
+  }
+  for (size_t wi = 0; wi < wins.size(); ++wi) {
+    const Win& w = wins[wi];
+    if (hit[wi]) {
+      b.done[w.obj] = BMPOW_DONE_FOUND;
+      b.nonce[w.obj] = bestn[wi];
+      b.trial[w.obj] = bestt[wi];
+      b.next[w.obj] = bestn[wi] == kU64Max ? kU64Max : bestn[wi] + 1;
+      b.pending--;
+      mark_finished(b, w.obj);
+    } else if (w.count - 1 == kU64Max - w.start) {
+      b.done[w.obj] = BMPOW_DONE_EXHAUSTED;
+      b.next[w.obj] = kU64Max;
+      b.pending--;
+      mark_finished(b, w.obj);
+    } else {
+      b.next[w.obj] = w.start + w.count;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// min-trial probe
+// ---------------------------------------------------------------------------------------
+void MinTrial::init(size_t n, const uint64_t* start, const uint64_t* count, uint64_t* min_out, uint64_t* argmin_out) {
+  cur.assign(start, start + n);
+  left.assign(count, count + n);
+  any.assign(n, 0);
+  first = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (left[i] && left[i] - 1 > kU64Max - start[i]) left[i] = kU64Max - start[i] + 1;  // stop at 2^64-1
+    min_out[i] = kU64Max;
+    argmin_out[i] = start[i];
+  }
+}
+
+bool MinTrial::plan(uint64_t total_chunks, std::vector<Win>& wins, uint64_t& C) {
+  const uint64_t chunk = BM_CHUNK;
+  while (first < left.size() && left[first] == 0) ++first;
+  if (first == left.size()) return false;
+  wins.clear();
+  uint64_t acc = 0;
+  for (size_t i = first; i < left.size() && acc < total_chunks; ++i) {
+    if (left[i] == 0) continue;
+    const uint64_t room = (total_chunks - acc) * chunk;
+    const uint64_t want = std::min(left[i], room);
+    const uint64_t ch = (want + chunk - 1) / chunk;
+    wins.push_back({(uint32_t)i, cur[i], want, ch, acc});
+    acc += ch;
+  }
+  C = acc;
+  return true;
+}
+
+void MinTrial::reduce_parts(const std::vector<bm_item>& items, const bm_minpart* parts, uint64_t* min_out,
+                            uint64_t* argmin_out) {
+  const uint64_t chunk = BM_CHUNK;
+  for (const bm_item& it : items) {
+    const uint64_t nch = (it.count + chunk - 1) / chunk;
+    uint64_t& mt = min_out[it.obj];
+    uint64_t& mn = argmin_out[it.obj];
+    for (uint64_t c = it.chunk_base; c < it.chunk_base + nch; ++c) {
+      const bm_minpart& q = parts[c];
+      if (!any[it.obj] || q.trial < mt || (q.trial == mt && q.nonce < mn)) {
+        any[it.obj] = 1;
+        mt = q.trial;
+        mn = q.nonce;
+      }
+    }
+  }
+}
+
+void MinTrial::advance(const std::vector<Win>& wins) {
+  for (const Win& w : wins) {
+    left[w.obj] -= w.count;
+    if (left[w.obj]) cur[w.obj] += w.count;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// receive-side verification
+// ---------------------------------------------------------------------------------------
+uint64_t padded_blocks(uint64_t m) { return (m + 17 + 127) / 128; }
+
+void pad_into(const uint8_t* msg, uint64_t m, uint8_t* dst, uint64_t nblk) {
+  const uint64_t total = nblk * 128;
+  std::memcpy(dst, msg, m);
+  std::memset(dst + m, 0, total - m);
+  dst[m] = 0x80;
+  const uint64_t bits_lo = m << 3, bits_hi = m >> 61;  // 128-bit big-endian bit length
+  for (int j = 0; j < 8; ++j) {
+    dst[total - 16 + j] = (uint8_t)(bits_hi >> (56 - 8 * j));
+    dst[total - 8 + j] = (uint8_t)(bits_lo >> (56 - 8 * j));
+  }
+}
+
+int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& parts, uint64_t& total_blocks) {
+  const size_t n = objs.size();
+  parts.clear();
+  if (n > 0xffffffffULL) return BMPOW_E_ARG;
+  std::vector<uint32_t> nblk(n);
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t b = padded_blocks(objs[i].len - 8);
+    if (b > 0xffffffffULL) return BMPOW_E_ARG;
+    nblk[i] = (uint32_t)b;
+    total += b;
+  }
+  if (total > 0xffffffffULL) return BMPOW_E_ARG;  // payload pool above 2^32 blocks (512 GiB)
+  total_blocks = total;
+  std::vector<uint32_t> order(n);
+  for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
+  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return nblk[a] > nblk[b]; });
+  size_t k = 0;
+  uint64_t acc = 0;
+  for (size_t s = 0; s < S && k < n; ++s) {
+    VPart pt;
+    pt.shard = s;
+    const uint64_t goal = total * (s + 1) / S;
+    uint64_t blk = 0;
+    while (k < n && (acc < goal || s == S - 1)) {
+      const uint32_t i = order[k];
+      pt.orig.push_back(i);
+      bv_obj o;
+      o.blk = (uint32_t)blk;
+      o.nblk = nblk[i];
+      o.nonce = load_be64(objs[i].p);
+      pt.ho.push_back(o);
+      blk += nblk[i];
+      acc += nblk[i];
+      ++k;
+    }
+    pt.blocks = blk;
+    if (!pt.orig.empty()) parts.push_back(std::move(pt));
+  }
+  return 0;
+}
+
+void pad_range(const std::vector<Span>& objs, const VPart& pt, size_t j0, size_t j1, uint64_t blk0, uint8_t* dst) {
+  if (j1 <= j0) return;
+  const std::vector<bv_obj>& ho = pt.ho;
+  const size_t m = j1 - j0;
+  const uint64_t bytes = (uint64_t)(ho[j1 - 1].blk + ho[j1 - 1].nblk - ho[j0].blk) * 128;
+  // a thread per ~2 MB (and per >= 64 objects), at most 16
+  const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency());
+  const size_t nth = std::max<size_t>(1, std::min<size_t>({16, hw, bytes / (2u << 20) + 1, m / 64 + 1}));
+  auto work = [&](size_t t) {
+    for (size_t j = j0 + m * t / nth; j < j0 + m * (t + 1) / nth; ++j) {
+      const Span& sp = objs[pt.orig[j]];
+      pad_into(sp.p + 8, sp.len - 8, dst + (uint64_t)(ho[j].blk - blk0) * 128, ho[j].nblk);
+    }
+  };
+  if (nth == 1) return work(0);
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nth; ++t) th.emplace_back(work, t);
+  work(0);
+  for (auto& x : th) x.join();
+}
+
+// Python ints until the true division by 2**16 (correctly rounded: the exact 128-bit product
+// converted once, then an exact power-of-two scale), IEEE doubles after, and an exact
+// int-vs-float comparison at the end.
+int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, int64_t recv, uint64_t eol) {
+  if (ntpb < 1000) ntpb = 1000;
+  if (extra < 1000) extra = 1000;
+  __int128 ttl = (__int128)eol - (__int128)recv;
+  if (ttl < 300) ttl = 300;
+  const unsigned __int128 le = (unsigned __int128)len + extra;
+  const unsigned __int128 prod = (unsigned __int128)ttl * le;
+  const double q = (double)prod / 65536.0;
+  const double x = (double)le + q;
+  const double y = (double)ntpb * x;
+  const double t = 18446744073709551616.0 / y;
+  if (t >= 18446744073709551616.0) return 1;
+  return pow <= (uint64_t)t ? 1 : 0;
+}
+
+}  // namespace bmsched

@@ -1,0 +1,131 @@
+// bmpow_sched.h -- the host-only half of libbmpow_hip.so's scheduler: everything between the C ABI
+// and the HIP calls that needs no device.  bmpow_host.hip drives the devices with it; the same
+// source builds with g++ for the sanitizer tests (tests/native/: ThreadSanitizer, ASan/UBSan),
+// which run it against a CPU stand-in for the kernels.
+//
+//   search steps   plan_step -> (launch per shard) -> apply_step        (bmpow_batch_step)
+//   sessions       init / add / take_done / reset / set_pending          (bmpow_batch_*)
+//   min-trial      MinTrial::plan -> (launch) -> reduce_parts -> advance (bmpow_min_trial*)
+//   verification   plan_verify, pad_range, pow_sufficient                (bmpow_verify*, bmpow_pow_values)
+//
+// Semantics reproduced: the reference's _doSafePoW first nonce (src/proofofwork.py:100-111) over
+// contiguous windows per object, and protocol.isProofOfWorkSufficient (src/protocol.py:258-286).
+#pragma once
+#include <stddef.h>
+#include <stdint.h>
+
+#include <vector>
+
+#include "../../include/bmpow.h"
+#include "bmpow_layout.h"
+
+namespace bmsched {
+
+constexpr uint64_t kU64Max = ~0ULL;
+
+uint64_t load_be64(const uint8_t* p);
+void pack_obj(const uint8_t* ih, uint64_t target, bm_obj* o);
+
+// Host mirror of a device-resident batch (one slot per object; slots of finished objects are
+// released by take_done and reused by add).
+struct BatchState {
+  size_t n = 0;    // slots in the table (objects, finished ones and free slots included)
+  size_t cap = 0;  // device allocation, in objects (set by the device side; add() reports growth)
+  std::vector<bm_obj> objs;
+  std::vector<uint64_t> next, nonce, trial;
+  std::vector<uint8_t> done;
+  size_t first_pending = 0;
+  size_t pending = 0;
+  std::vector<uint32_t> finished;  // slots finished since the last take_done, in finishing order
+  size_t finished_head = 0;
+  std::vector<uint32_t> free_slots;  // slots released by take_done, reused by add (LIFO)
+};
+
+void init(BatchState& b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start);
+
+// Append m objects (slots reused first).  slots[i] = object i's slot.  Returns true when the table
+// outgrew b.cap (the caller reallocates and re-uploads); false when only `slots` need uploading.
+bool add(BatchState& b, size_t m, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
+         std::vector<uint32_t>& slots);
+
+// Pop up to cap finished slots (any output but slot_out may be null); they become BMPOW_FREE.
+size_t take_done(BatchState& b, size_t cap, uint32_t* slot_out, uint64_t* nonce_out, uint64_t* trial_out,
+                 uint8_t* done_out);
+
+void reset(BatchState& b, const uint64_t* start);  // released slots stay free
+void set_pending(BatchState& b, size_t first, size_t count, bool pending);
+
+// One object's contiguous nonce window in a step: `chunks` chunks from chunk index `chunk0` of the
+// step's flattened chunk list.
+struct Win {
+  uint32_t obj;
+  uint64_t start, count, chunks, chunk0;
+};
+
+struct StepPlan {
+  uint32_t iters = 0;   // workgroup iterations (chunk = BM_BLOCK x iters nonces)
+  uint64_t chunk = 0;
+  uint64_t C = 0;       // chunks in the step
+  std::vector<Win> wins;                    // ascending object order
+  std::vector<std::vector<bm_item>> items;  // per shard, ascending chunk_base
+  std::vector<uint32_t> nchunks;            // per shard: workgroups of its launch
+};
+
+// Cut C chunks of windows (ascending chunk0) into S contiguous per-shard slices: big windows are
+// nonce-sharded, small ones object-sharded; each item's chunk_base is relative to its shard.
+void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p);
+
+// Windows for the next step over S shards with about `budget` trials (0 = step_trials x S): pending
+// objects in slot order, k chunks each.  Returns false (p untouched) when nothing is pending.
+bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p);
+
+// Fold the step's per-shard results (res[s][k] for p.items[s][k]) into the state: the min over
+// shards of each object's hits is final (every lower nonce of its window was hashed); no hit moves
+// next past the window; a window ending at 2^64-1 without a hit exhausts the object.
+void apply_step(BatchState& b, const StepPlan& p, const std::vector<const bm_result*>& res);
+
+// Min-trial probe over n (object, range) pairs, in steps.
+struct MinTrial {
+  std::vector<uint64_t> cur, left;
+  std::vector<uint8_t> any;
+  size_t first = 0;
+  void init(size_t n, const uint64_t* start, const uint64_t* count, uint64_t* min_out, uint64_t* argmin_out);
+  // windows of the next step (<= total_chunks chunks of BM_CHUNK); false when every range is done
+  bool plan(uint64_t total_chunks, std::vector<Win>& wins, uint64_t& C);
+  // fold one shard's workgroup minima (parts[c] for the chunks of `items`) into min/argmin,
+  // lexicographically on (trial, nonce) so ties keep the smaller nonce
+  void reduce_parts(const std::vector<bm_item>& items, const bm_minpart* parts, uint64_t* min_out,
+                    uint64_t* argmin_out);
+  void advance(const std::vector<Win>& wins);
+};
+
+// ---- receive-side verification ----
+struct Span {
+  const uint8_t* p;
+  uint64_t len;  // >= 8 (nonce || payload)
+};
+
+// blocks of SHA-512 padding for an m-byte message: m + 1 (0x80) + 16 (bit length) rounded up
+uint64_t padded_blocks(uint64_t m);
+void pad_into(const uint8_t* msg, uint64_t m, uint8_t* dst, uint64_t nblk);
+
+struct VPart {
+  size_t shard = 0;
+  std::vector<uint32_t> orig;  // sorted position -> input index
+  std::vector<bv_obj> ho;      // per sorted position: first block (part-relative), blocks, nonce
+  uint64_t blocks = 0;
+};
+
+// Sort objects by padded block count (descending, stable) and cut them into per-shard parts of
+// equal block totals.  Returns BMPOW_E_ARG on size limits, else 0.
+int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& parts, uint64_t& total_blocks);
+
+// Pad objects [j0, j1) of a part (sorted order) into dst (their blocks from blk0 on), over up to 16
+// host threads: a memory-bound copy of every payload.
+void pad_range(const std::vector<Span>& objs, const VPart& pt, size_t j0, size_t j1, uint64_t blk0, uint8_t* dst);
+
+// protocol.isProofOfWorkSufficient's comparison (src/protocol.py:272-286) in the reference's
+// arithmetic.  1 sufficient, 0 not.
+int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, int64_t recv, uint64_t eol);
+
+}  // namespace bmsched

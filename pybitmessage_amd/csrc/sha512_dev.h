@@ -120,6 +120,23 @@ BM_DEV uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
   return opaque(r);
 }
 
+// 64-bit add of two nonce-dependent values.  Default: the compiler's v_lshl_add_u64 (one VOP3,
+// half rate).  BM_ADD64_VOP2 (A/B variant): v_add_co_u32_e32 +
+// v_addc_co_u32_e32, the VOP2 pair with the carry in VCC.
+BM_DEV uint64_t add64(uint64_t a, uint64_t b) {
+#ifdef BM_ADD64_VOP2
+  if (!(__builtin_constant_p(a) && __builtin_constant_p(b))) {
+    uint32_t lo, hi;
+    asm("v_add_co_u32_e32 %0, vcc, %2, %3\n\tv_addc_co_u32_e32 %1, vcc, %4, %5, vcc"
+        : "=&v"(lo), "=v"(hi)
+        : "v"(lo32(a)), "v"(lo32(b)), "v"(hi32(a)), "v"(hi32(b))
+        : "vcc");
+    return opaque(mk64(lo, hi));
+  }
+#endif
+  return a + b;
+}
+
 template <bool kHoist = false>
 BM_DEV uint64_t xor3(uint64_t a, uint64_t b, uint64_t c) { return bitop3_64<0x96, kHoist>(a, b, c); }
 
@@ -176,9 +193,9 @@ BM_DEV void round_step(uint64_t (&s)[8], uint64_t (&w)[16]) {
     // are summed first and hoisted out of the nonce loop by LICM
     w[T & 15] = (w[(T - 7) & 15] + sig0<kU0>(w[(T - 15) & 15]) + w[(T - 16) & 15]) + sig1<kU1>(w[(T - 2) & 15]);
   }
-  const uint64_t t1 = s[H] + Sig1(s[E]) + Ch(s[E], s[F], s[G]) + (K(T) + w[T & 15]);
-  s[D] += t1;
-  s[H] = t1 + Sig0(s[A]) + Maj(s[A], s[B], s[C]);
+  const uint64_t t1 = add64(add64(add64(s[H], Sig1(s[E])), Ch(s[E], s[F], s[G])), K(T) + w[T & 15]);
+  s[D] = add64(s[D], t1);
+  s[H] = add64(add64(t1, Sig0(s[A])), Maj(s[A], s[B], s[C]));
 }
 
 template <int T, int END, bool kTrial1 = false>

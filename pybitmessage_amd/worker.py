@@ -163,6 +163,165 @@ def send_msgs(jobs, build_msg, rng=random, now=None, step_trials=0):
 
 
 # ------------------------------------------------------------------------------------------
+# every other object kind the worker PoWs (class_singleWorker.py:252-715, 1375-1493): the
+# TTL rules and the unencrypted object header are the PoW-relevant part; signatures and the
+# ECIES encryption are produced by the caller (out of scope) and passed in
+# as bytes.  Each builder returns a PowObject whose target is the reference's
+# (_doPOWDefaults, :219-231) at the given difficulty (network default, or the test-mode /
+# extralowdifficulty ÷100 of bitmessagemain.py:167-172 when ntpb/extra are passed).
+# ------------------------------------------------------------------------------------------
+#: ``protocol.OBJECT_ONIONPEER`` (``protocol.py:54``) and ``BITFIELD_DOESACK`` (``:42``)
+OBJECT_ONIONPEER = 0x746f72
+BITFIELD_DOESACK = 1
+_DAY = 24 * 60 * 60
+
+
+def _varint(i):
+    from .addressgen import encodeVarint
+    return encodeVarint(i)
+
+
+def _embedded(ttl, now):
+    return int((time.time() if now is None else now) + ttl)
+
+
+def _defaults(ntpb, extra):
+    return (targets.networkDefaultProofOfWorkNonceTrialsPerByte if ntpb is None else ntpb,
+            targets.networkDefaultPayloadLengthExtraBytes if extra is None else extra)
+
+
+def pubkey_ttl(rng=random):
+    """28 days +- 5 minutes (``doPOWForMyV2Pubkey`` / ``sendOutOrStoreMyV3Pubkey`` /
+    ``sendOutOrStoreMyV4Pubkey``, ``:262``, ``:331``, ``:410``)."""
+    return int(28 * _DAY + rng.randrange(-300, 300))
+
+
+def get_bitfield(does_ack=True):
+    """``protocol.getBitfield`` (``protocol.py:70-77``)."""
+    return pack('>I', BITFIELD_DOESACK if does_ack else 0)
+
+
+def pubkey_object(address_version, stream, body, rng=random, now=None, ntpb=None, extra=None, tag=None):
+    """A pubkey object (type 1) around ``body``: for v2 the bitfield and the two 64-byte public
+    keys (``:264-292``); for v3 those plus varint ntpb, varint extra, varint len(signature) and
+    the signature (``:342-378``); for v4 the 32-byte tag then the encrypted blob (``:420-465``).
+    ``pubkey_v2_body`` / ``pubkey_v3_body`` assemble the first two."""
+    ttl = pubkey_ttl(rng)
+    payload = pack('>Q', _embedded(ttl, now)) + b'\x00\x00\x00\x01'
+    payload += _varint(address_version) + _varint(stream) + bytes(body)
+    n, e = _defaults(ntpb, extra)
+    return PowObject(payload, ttl, n, e, tag=tag)
+
+
+def pubkey_v2_body(pub_signing, pub_encryption, does_ack=True):
+    """Bitfield + the keys without their 0x04 prefix (``:269``, ``:287-289``)."""
+    return get_bitfield(does_ack) + bytes(pub_signing)[-64:] + bytes(pub_encryption)[-64:]
+
+
+def pubkey_v3_body(pub_signing, pub_encryption, ntpb, extra, signature, does_ack=True):
+    """v2 body + the address's own difficulty + the length-prefixed signature (``:363-378``)."""
+    return (pubkey_v2_body(pub_signing, pub_encryption, does_ack) + _varint(ntpb) + _varint(extra)
+            + _varint(len(signature)) + bytes(signature))
+
+
+def onionpeer_ttl(rng=random):
+    """7 days +- 5 minutes (``sendOnionPeerObj``, ``:503``)."""
+    return int(7 * _DAY + rng.randrange(-300, 300))
+
+
+def encode_host(host):
+    """``protocol.encodeHost`` (``protocol.py:102-110``)."""
+    import base64
+    import socket
+    if host.endswith('.onion'):
+        return b'\xfd\x87\xd8\x7e\xeb\x43' + base64.b32decode(host.split('.')[0], True)
+    if host.find(':') == -1:
+        return b'\x00' * 10 + b'\xff\xff' + socket.inet_aton(host)
+    return socket.inet_pton(socket.AF_INET6, host)
+
+
+def onionpeer_object(host, port, rng=random, now=None, ntpb=None, extra=None):
+    """The onionpeer object (``:494-530``): object type 0x746f72, version 2 for a 22-character
+    (v2) onion host else 3, stream 1, varint(port) + encodeHost(host)."""
+    ttl = onionpeer_ttl(rng)
+    payload = pack('>Q', _embedded(ttl, now)) + pack('>I', OBJECT_ONIONPEER)
+    payload += _varint(2 if len(host) == 22 else 3) + _varint(1) + _varint(port) + encode_host(host)
+    n, e = _defaults(ntpb, extra)
+    return PowObject(payload, ttl, n, e)
+
+
+def broadcast_ttl(ttl, rng=random):
+    """The broadcast's TTL clamped to [1 hour, 28 days] +- 5 minutes (``sendBroadcast``,
+    ``:599-604``)."""
+    if ttl > 28 * _DAY:
+        ttl = 28 * _DAY
+    if ttl < 60 * 60:
+        ttl = 60 * 60
+    return int(ttl + rng.randrange(-300, 300))
+
+
+def broadcast_object(address_version, stream, encrypted, ttl, tag=b'', rng=random, now=None, ntpb=None,
+                     extra=None):
+    """A broadcast object (type 3, ``:605-675``): broadcast version 4 for address version <= 3
+    (no tag), 5 with the 32-byte tag otherwise, stream, tag, then the encrypted body."""
+    ttl = broadcast_ttl(ttl, rng)
+    payload = pack('>Q', _embedded(ttl, now)) + b'\x00\x00\x00\x03'
+    payload += _varint(4 if address_version <= 3 else 5) + _varint(stream)
+    if address_version >= 4:
+        payload += bytes(tag)
+    payload += bytes(encrypted)
+    n, e = _defaults(ntpb, extra)
+    return PowObject(payload, ttl, n, e)
+
+
+def getpubkey_ttl(retry_number, rng=random):
+    """2.5 days x 2^retryNumber, capped at 28 days, +- 5 minutes -- a float, as the reference
+    leaves it (``requestPubKey``, ``:1429-1434``)."""
+    ttl = 2.5 * _DAY
+    ttl *= 2 ** retry_number
+    if ttl > 28 * _DAY:
+        ttl = 28 * _DAY
+    return ttl + rng.randrange(-300, 300)
+
+
+def getpubkey_object(address_version, stream, ripe_or_tag, retry_number=0, rng=random, now=None, ntpb=None,
+                     extra=None):
+    """A getpubkey object (type 0, ``:1436-1445``): the 20-byte ripe for address versions <= 3,
+    the 32-byte tag for v4."""
+    ttl = getpubkey_ttl(retry_number, rng)
+    payload = pack('>Q', int((time.time() if now is None else now) + ttl)) + b'\x00\x00\x00\x00'
+    payload += _varint(address_version) + _varint(stream) + bytes(ripe_or_tag)
+    n, e = _defaults(ntpb, extra)
+    return PowObject(payload, ttl, n, e)
+
+
+def msg_ttl(ttl, retry_number=0, rng=random):
+    """sendMsg's TTL: x 2^retryNumber, capped at 28 days, +- 5 minutes (``:900-905``)."""
+    ttl *= 2 ** retry_number
+    if ttl > 28 * _DAY:
+        ttl = 28 * _DAY
+    return int(ttl + rng.randrange(-300, 300))
+
+
+def msg_difficulty(to_address_version, ntpb=None, extra=None, default_ntpb=None, default_extra=None):
+    """The recipient's difficulty as sendMsg applies it (``:1008-1027``): v2 addresses use the
+    network defaults; v3+ demand at least the defaults."""
+    dn, de = _defaults(default_ntpb, default_extra)
+    if to_address_version <= 2 or ntpb is None:
+        return dn, de
+    return max(ntpb, dn), max(extra, de)
+
+
+def msg_object(encrypted, to_address_version, stream, ttl, ntpb=None, extra=None, rng=random, now=None,
+               default_ntpb=None, default_extra=None):
+    """A msg object (type 2, ``:1240-1256``) at the recipient's difficulty (``:1256-1264``)."""
+    n, e = msg_difficulty(to_address_version, ntpb, extra, default_ntpb, default_extra)
+    payload = pack('>Q', _embedded(ttl, now)) + b'\x00\x00\x00\x02' + _varint(1) + _varint(stream)
+    payload += bytes(encrypted)
+    return PowObject(payload, ttl, n, e)
+
+
+# ------------------------------------------------------------------------------------------
 # continuous batching across producer threads
 # ------------------------------------------------------------------------------------------
 class _Entry(object):

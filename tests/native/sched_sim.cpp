@@ -1,0 +1,403 @@
+// sched_sim.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// Drives the host-only half of libbmpow_hip.so's scheduler (pybitmessage_amd/csrc/bmpow_sched.cpp,
+// the code bmpow_host.hip runs between HIP calls) against a CPU stand-in for the gfx950 kernels,
+// whose trial function is the C oracle's (oracle/bmpow_oracle.c).  Built and run by
+// tests/test_native.py under ThreadSanitizer and under AddressSanitizer + UBSan, with the
+// concurrency the library has: one host thread per shard (device) per step, producer threads
+// feeding a shared session under one mutex (the library's g_mu) while a stepper thread steps it
+// and a consumer pops finished objects, and the multi-threaded payload padding of the verifier.
+//
+// Every answer is checked against the oracle's sequential _doSafePoW search
+// (src/proofofwork.py:100-111); exit status 0 = all scenarios passed.
+#include <stdint.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <array>
+#include <chrono>
+#include <atomic>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <random>
+#include <thread>
+#include <vector>
+
+#include "../../pybitmessage_amd/csrc/bmpow_sched.h"
+
+extern "C" {
+uint64_t bmo_trial(const uint8_t ih[64], uint64_t nonce);
+int bmo_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials, uint64_t* nonce_out,
+               uint64_t* trial_out);
+int bmo_min_trial(const uint8_t ih[64], uint64_t start, uint64_t count, uint64_t* min_out, uint64_t* argmin_out);
+}
+
+using namespace bmsched;
+
+static int g_fail = 0;
+#define CHECK(cond, ...)                            \
+  do {                                              \
+    if (!(cond)) {                                  \
+      fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+      fprintf(stderr, __VA_ARGS__);                 \
+      fprintf(stderr, "\n");                        \
+      ++g_fail;                                     \
+    }                                               \
+  } while (0)
+
+static void ih_of(const bm_obj& o, uint8_t ih[64]) {
+  for (int i = 0; i < 8; ++i)
+    for (int j = 0; j < 8; ++j) ih[8 * i + j] = (uint8_t)(o.w[i] >> (56 - 8 * j));
+}
+
+// ---- CPU stand-in for one shard's device state and kernels ----
+struct SimShard {
+  std::vector<uint64_t> best;
+  std::vector<uint32_t> found;
+  std::vector<bm_result> res;
+};
+
+// bm_search_kernel + bm_resolve_kernel for one shard: per item, nonces in order up to the first hit
+// (the device's early exit gives the same per-object minimum); res[k] = the object's shard minimum.
+static void sim_step_shard(const std::vector<bm_obj>& objs, const std::vector<bm_item>& items, SimShard& sh) {
+  if (sh.best.size() < objs.size()) {
+    sh.best.resize(objs.size(), kU64Max);
+    sh.found.resize(objs.size(), 0);
+  }
+  uint8_t ih[64];
+  for (const bm_item& it : items) {
+    ih_of(objs[it.obj], ih);
+    for (uint64_t j = 0; j < it.count; ++j) {
+      const uint64_t n = it.start + j;
+      if (bmo_trial(ih, n) <= objs[it.obj].target) {
+        if (!sh.found[it.obj] || n < sh.best[it.obj]) sh.best[it.obj] = n;
+        sh.found[it.obj] = 1;
+        break;
+      }
+    }
+  }
+  sh.res.resize(items.size());
+  for (size_t k = 0; k < items.size(); ++k) {
+    const uint32_t o = items[k].obj;
+    bm_result r;
+    r.nonce = sh.best[o];
+    r.found = sh.found[o];
+    r.pad = 0;
+    if (r.found) {
+      ih_of(objs[o], ih);
+      r.trial = bmo_trial(ih, r.nonce);
+    } else {
+      r.trial = 0;
+    }
+    sh.res[k] = r;
+  }
+}
+
+// One bounded step over S shards, one host thread per shard (as one stream per device).
+static bool sim_step(BatchState& b, std::vector<SimShard>& shards, uint64_t budget, uint64_t step_trials) {
+  StepPlan p;
+  if (!plan_step(b, budget, step_trials, shards.size(), p)) return false;
+  uint64_t chunks = 0;
+  for (size_t s = 0; s < shards.size(); ++s) chunks += p.nchunks[s];
+  CHECK(chunks == p.C, "shard chunks %llu != step chunks %llu", (unsigned long long)chunks, (unsigned long long)p.C);
+  for (size_t s = 0; s < shards.size(); ++s)
+    for (size_t k = 1; k < p.items[s].size(); ++k)
+      CHECK(p.items[s][k].chunk_base > p.items[s][k - 1].chunk_base, "chunk_base not ascending");
+  std::vector<std::thread> th;
+  for (size_t s = 0; s < shards.size(); ++s) th.emplace_back(sim_step_shard, std::cref(b.objs), std::cref(p.items[s]),
+                                                             std::ref(shards[s]));
+  for (auto& t : th) t.join();
+  std::vector<const bm_result*> res(shards.size());
+  for (size_t s = 0; s < shards.size(); ++s) res[s] = shards[s].res.data();
+  apply_step(b, p, res);
+  // a pending object's device state is (UINT64_MAX, 0) between steps (bmpow_host.hip relies on it)
+  for (size_t s = 0; s < shards.size(); ++s)
+    for (size_t i = 0; i < b.n && i < shards[s].found.size(); ++i)
+      if (b.done[i] == BMPOW_PENDING) CHECK(!shards[s].found[i], "pending object %zu has a hit on shard %zu", i, s);
+  return true;
+}
+
+struct Obj {
+  uint8_t ih[64];
+  uint64_t target, start;
+};
+
+static std::vector<Obj> random_objs(std::mt19937_64& rng, size_t n, uint64_t max_div) {
+  std::vector<Obj> v(n);
+  for (auto& o : v) {
+    for (auto& c : o.ih) c = (uint8_t)rng();
+    o.target = kU64Max / (1 + rng() % max_div);
+    o.start = 1;
+  }
+  return v;
+}
+
+static void expect_exact(const Obj& o, int done, uint64_t nonce, uint64_t trial, const char* what, size_t i) {
+  uint64_t n = 0, t = 0;
+  const uint64_t budget = kU64Max - o.start + 1 == 0 ? kU64Max : kU64Max - o.start + 1;
+  const int hit = bmo_search(o.ih, o.target, o.start, budget, &n, &t);
+  if (hit) {
+    CHECK(done == BMPOW_DONE_FOUND && nonce == n && trial == t, "%s: object %zu: got (%d, %llu) want %llu", what, i,
+          done, (unsigned long long)nonce, (unsigned long long)n);
+  } else {
+    CHECK(done == BMPOW_DONE_EXHAUSTED, "%s: object %zu: want EXHAUSTED, got %d", what, i, done);
+  }
+}
+
+// ---- scenario 1: whole batches, many shard layouts and step sizes ----
+static void scenario_batches() {
+  std::mt19937_64 rng(1);
+  struct Case { size_t n, S; uint64_t budget, max_div; };
+  const Case cases[] = {{40, 1, 0, 3000}, {300, 3, 3001, 2000}, {2500, 2, 1 << 20, 500}, {600, 8, 1 << 14, 5000},
+                        {5000, 1, 1 << 22, 200}, {17, 5, 1, 50000}};
+  for (const Case& c : cases) {
+    std::vector<Obj> objs = random_objs(rng, c.n, c.max_div);
+    std::vector<uint8_t> ihs(64 * c.n);
+    std::vector<uint64_t> tg(c.n), st(c.n);
+    for (size_t i = 0; i < c.n; ++i) {
+      memcpy(&ihs[64 * i], objs[i].ih, 64);
+      tg[i] = objs[i].target;
+      st[i] = objs[i].start;
+    }
+    BatchState b;
+    init(b, c.n, ihs.data(), tg.data(), st.data());
+    std::vector<SimShard> shards(c.S);
+    int steps = 0;
+    while (sim_step(b, shards, c.budget, 1 << 16)) ++steps;
+    CHECK(b.pending == 0, "batch n=%zu left %zu pending", c.n, b.pending);
+    for (size_t i = 0; i < c.n; ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "batch", i);
+    fprintf(stderr, "batches: n=%zu S=%zu budget=%llu: %d steps\n", c.n, c.S, (unsigned long long)c.budget, steps);
+  }
+}
+
+// ---- scenario 2: windows clipped at the top of the nonce space ----
+static void scenario_top_of_space() {
+  std::mt19937_64 rng(2);
+  std::vector<Obj> objs = random_objs(rng, 24, 1);
+  for (size_t i = 0; i < objs.size(); ++i) {
+    objs[i].start = kU64Max - (i % 6) * 700;
+    objs[i].target = i % 3 == 0 ? 0 : (i % 3 == 1 ? kU64Max : kU64Max / 900);
+  }
+  std::vector<uint8_t> ihs(64 * objs.size());
+  std::vector<uint64_t> tg(objs.size()), st(objs.size());
+  for (size_t i = 0; i < objs.size(); ++i) {
+    memcpy(&ihs[64 * i], objs[i].ih, 64);
+    tg[i] = objs[i].target;
+    st[i] = objs[i].start;
+  }
+  for (size_t S : {1, 3}) {
+    BatchState b;
+    init(b, objs.size(), ihs.data(), tg.data(), st.data());
+    std::vector<SimShard> shards(S);
+    while (sim_step(b, shards, 1000, 1 << 16)) {
+    }
+    for (size_t i = 0; i < objs.size(); ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "top", i);
+  }
+}
+
+// ---- scenario 3: a shared session fed by producer threads (PowService's use of the library) ----
+static void scenario_session() {
+  std::mutex mu;  // the library's g_mu: every entry point holds it
+  BatchState b;
+  init(b, 0, nullptr, nullptr, nullptr);
+  std::vector<SimShard> shards(2);
+  std::vector<Obj> all;
+  std::vector<int> slot_owner;                     // slot -> index into `all` (live objects)
+  std::vector<std::array<uint64_t, 3>> results;  // per `all` index: done, nonce, trial
+  std::atomic<int> producers_left{4};
+  std::atomic<bool> stop{false};
+  std::condition_variable cv;
+
+  auto producer = [&](int id) {
+    std::mt19937_64 rng(100 + id);
+    for (int burst = 0; burst < 25; ++burst) {
+      const size_t m = 1 + rng() % 40;
+      std::vector<Obj> objs = random_objs(rng, m, 4000);
+      std::vector<uint8_t> ihs(64 * m);
+      std::vector<uint64_t> tg(m);
+      for (size_t i = 0; i < m; ++i) {
+        memcpy(&ihs[64 * i], objs[i].ih, 64);
+        tg[i] = objs[i].target;
+      }
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        std::vector<uint32_t> slots;
+        add(b, m, ihs.data(), tg.data(), nullptr, slots);
+        b.cap = std::max(b.cap, b.n);  // the device side's reallocation
+        for (SimShard& sh : shards)      // ... and its reset of the added slots' best[] / found[]
+          for (uint32_t sl : slots)
+            if (sl < sh.best.size()) {
+              sh.best[sl] = kU64Max;
+              sh.found[sl] = 0;
+            }
+        for (size_t i = 0; i < m; ++i) {
+          if (slot_owner.size() <= slots[i]) slot_owner.resize(slots[i] + 1, -1);
+          CHECK(slot_owner[slots[i]] == -1, "slot %u handed out while live", slots[i]);
+          slot_owner[slots[i]] = (int)all.size();
+          all.push_back(objs[i]);
+          results.push_back({0, 0, 0});
+        }
+      }
+      cv.notify_all();
+      std::this_thread::sleep_for(std::chrono::microseconds(200 + rng() % 800));
+    }
+    producers_left--;
+    cv.notify_all();
+  };
+  auto consumer = [&]() {
+    uint32_t slot[64];
+    uint64_t nonce[64], trial[64];
+    uint8_t done[64];
+    for (;;) {
+      std::unique_lock<std::mutex> lk(mu);
+      // wait() (pthread_cond_wait), not wait_for: GCC 11's wait_for uses pthread_cond_clockwait,
+      // which its ThreadSanitizer does not intercept (false "double lock" reports)
+      cv.wait(lk, [&]() { return b.finished_head < b.finished.size() || stop.load(); });
+      const size_t k = take_done(b, 64, slot, nonce, trial, done);
+      for (size_t j = 0; j < k; ++j) {
+        const int a = slot_owner[slot[j]];
+        CHECK(a >= 0, "finished slot %u has no owner", slot[j]);
+        if (a < 0) continue;
+        results[a] = {done[j], nonce[j], trial[j]};
+        slot_owner[slot[j]] = -1;
+      }
+      if (stop.load() && k == 0 && b.finished_head == b.finished.size()) return;
+    }
+  };
+  auto stepper = [&]() {
+    for (;;) {
+      bool stepped;
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        stepped = sim_step(b, shards, 1 << 13, 1 << 16);
+      }
+      cv.notify_all();
+      if (!stepped) {
+        if (producers_left.load() == 0) {
+          std::lock_guard<std::mutex> lk(mu);
+          if (b.pending == 0) break;
+        }
+        std::this_thread::sleep_for(std::chrono::microseconds(300));
+      }
+    }
+    stop.store(true);
+    cv.notify_all();
+  };
+  std::vector<std::thread> th;
+  for (int i = 0; i < 4; ++i) th.emplace_back(producer, i);
+  th.emplace_back(stepper);
+  th.emplace_back(consumer);
+  for (auto& t : th) t.join();
+  for (size_t i = 0; i < all.size(); ++i)
+    expect_exact(all[i], (int)results[i][0], results[i][1], results[i][2], "session", i);
+  size_t live = 0;
+  for (int o : slot_owner) live += o >= 0;
+  CHECK(live == 0, "%zu slots still owned after the session drained", live);
+  CHECK(b.n < all.size(), "slots were not reused (%zu slots for %zu objects)", b.n, all.size());
+  fprintf(stderr, "session: %zu objects through %zu slots\n", all.size(), b.n);
+}
+
+// ---- scenario 4: min-trial planning and reduction ----
+static void scenario_min_trial() {
+  std::mt19937_64 rng(4);
+  const size_t n = 60;
+  std::vector<Obj> objs = random_objs(rng, n, 1);
+  std::vector<uint64_t> start(n), count(n), mn(n), arg(n);
+  for (size_t i = 0; i < n; ++i) {
+    start[i] = i % 7 == 0 ? kU64Max - rng() % 3000 : rng() % 100000;
+    count[i] = i % 11 == 0 ? 0 : rng() % 30000;
+  }
+  std::vector<bm_obj> ob(n);
+  for (size_t i = 0; i < n; ++i) pack_obj(objs[i].ih, 0, &ob[i]);
+  for (size_t S : {1, 4}) {
+    MinTrial mt;
+    mt.init(n, start.data(), count.data(), mn.data(), arg.data());
+    StepPlan p;
+    uint64_t C = 0;
+    while (mt.plan(9, p.wins, C)) {  // 9 chunks of BM_CHUNK per step: ranges span steps and shards
+      slice(p.wins, C, BM_CHUNK, S, p);
+      std::vector<std::thread> th;
+      std::vector<std::vector<bm_minpart>> parts(S);
+      for (size_t s = 0; s < S; ++s)
+        th.emplace_back([&, s]() {  // bm_mintrial_kernel: per chunk, the first minimum
+          parts[s].assign(p.nchunks[s], bm_minpart{kU64Max, kU64Max});
+          uint8_t ih[64];
+          for (const bm_item& it : p.items[s]) {
+            ih_of(ob[it.obj], ih);
+            for (uint64_t j = 0; j < it.count; ++j) {
+              bm_minpart& q = parts[s][it.chunk_base + j / BM_CHUNK];
+              const uint64_t t = bmo_trial(ih, it.start + j);
+              if (t < q.trial || (t == q.trial && it.start + j < q.nonce)) q = {t, it.start + j};
+            }
+          }
+        });
+      for (auto& t : th) t.join();
+      for (size_t s = 0; s < S; ++s) mt.reduce_parts(p.items[s], parts[s].data(), mn.data(), arg.data());
+      mt.advance(p.wins);
+    }
+    for (size_t i = 0; i < n; ++i) {
+      uint64_t wm = 0, wa = 0;
+      bmo_min_trial(objs[i].ih, start[i], count[i], &wm, &wa);
+      CHECK(mn[i] == wm && arg[i] == wa, "min-trial object %zu (S=%zu): got (%llu, %llu) want (%llu, %llu)", i, S,
+            (unsigned long long)mn[i], (unsigned long long)arg[i], (unsigned long long)wm, (unsigned long long)wa);
+    }
+  }
+}
+
+// ---- scenario 5: verification layout and multi-threaded padding ----
+static void scenario_verify() {
+  std::mt19937_64 rng(5);
+  std::vector<std::vector<uint8_t>> bufs;
+  const size_t lens[] = {8, 9, 16, 119, 120, 127, 128, 135, 136, 1000, 4096, 262144 + 8};
+  for (int r = 0; r < 900; ++r) {
+    const size_t len = r < 12 ? lens[r] : 8 + rng() % 20000;
+    std::vector<uint8_t> v(len);
+    for (auto& c : v) c = (uint8_t)rng();
+    bufs.push_back(std::move(v));
+  }
+  std::vector<Span> spans;
+  for (auto& v : bufs) spans.push_back({v.data(), v.size()});
+  for (size_t S : {1, 3}) {
+    std::vector<VPart> parts;
+    uint64_t total = 0;
+    CHECK(plan_verify(spans, S, parts, total) == 0, "plan_verify failed");
+    uint64_t seen = 0;
+    std::vector<int> hits(spans.size(), 0);
+    for (const VPart& pt : parts) {
+      seen += pt.blocks;
+      for (size_t j = 1; j < pt.ho.size(); ++j) CHECK(pt.ho[j].nblk <= pt.ho[j - 1].nblk, "not sorted by blocks");
+      std::vector<uint8_t> pool(pt.blocks * 128, 0xEE);
+      pad_range(spans, pt, 0, pt.orig.size(), 0, pool.data());
+      for (size_t j = 0; j < pt.orig.size(); ++j) {
+        const Span& sp = spans[pt.orig[j]];
+        hits[pt.orig[j]]++;
+        const uint64_t m = sp.len - 8, nb = padded_blocks(m);
+        CHECK(pt.ho[j].nblk == nb && pt.ho[j].nonce == load_be64(sp.p), "object descriptor");
+        std::vector<uint8_t> want(nb * 128, 0);
+        memcpy(want.data(), sp.p + 8, m);
+        want[m] = 0x80;
+        for (int k = 0; k < 8; ++k) want[nb * 128 - 1 - k] = (uint8_t)((m << 3) >> (8 * k));
+        want[nb * 128 - 9] = (uint8_t)(m >> 61);
+        CHECK(memcmp(want.data(), pool.data() + (uint64_t)pt.ho[j].blk * 128, nb * 128) == 0, "padding of object %u",
+              pt.orig[j]);
+      }
+    }
+    CHECK(seen == total, "blocks");
+    for (int h : hits) CHECK(h == 1, "object placed %d times", h);
+  }
+}
+
+int main() {
+  scenario_batches();
+  scenario_top_of_space();
+  scenario_session();
+  scenario_min_trial();
+  scenario_verify();
+  if (g_fail) {
+    fprintf(stderr, "%d check(s) failed\n", g_fail);
+    return 1;
+  }
+  fprintf(stderr, "sched_sim: all scenarios passed\n");
+  return 0;
+}

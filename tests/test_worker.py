@@ -7,6 +7,7 @@ import ctypes
 import hashlib
 import logging
 import random
+import struct
 import subprocess
 import threading
 import time
@@ -327,3 +328,89 @@ def test_gpu_hippow_shutdown(gpulib):
             hippow.do_opencl_pow('00' * 64, 0)
     finally:
         state.shutdown = 0
+
+
+# ------------------------------------------------------------------ every singleWorker object kind
+def _mixed_objects(rng, ntpb=None, extra=None, now=1700000000):
+    from pybitmessage_amd import worker as w
+    pub_s, pub_e = b'\x04' + rng.randbytes(64), b'\x04' + rng.randbytes(64)
+    sig = rng.randbytes(71)
+    objs = [
+        ('pubkey v2', w.pubkey_object(2, 1, w.pubkey_v2_body(pub_s, pub_e), rng, now, ntpb, extra)),
+        ('pubkey v3', w.pubkey_object(3, 1, w.pubkey_v3_body(pub_s, pub_e, 1000, 1000, sig), rng, now, ntpb, extra)),
+        ('pubkey v4', w.pubkey_object(4, 1, rng.randbytes(32) + rng.randbytes(300), rng, now, ntpb, extra)),
+        ('onionpeer v3', w.onionpeer_object('a' * 56 + '.onion', 8444, rng, now, ntpb, extra)),
+        ('onionpeer v2', w.onionpeer_object('b' * 16 + '.onion', 8444, rng, now, ntpb, extra)),
+        ('broadcast v4', w.broadcast_object(3, 1, rng.randbytes(400), 4 * 24 * 3600, b'', rng, now, ntpb, extra)),
+        ('broadcast v5', w.broadcast_object(4, 1, rng.randbytes(900), 60, rng.randbytes(32), rng, now, ntpb, extra)),
+        ('getpubkey v3', w.getpubkey_object(3, 1, rng.randbytes(20), 0, rng, now, ntpb, extra)),
+        ('getpubkey v4 retry 5', w.getpubkey_object(4, 1, rng.randbytes(32), 5, rng, now, ntpb, extra)),
+        ('msg to v4', w.msg_object(rng.randbytes(700), 4, 1, w.msg_ttl(4 * 24 * 3600, 0, rng),
+                                   *((2000, 1500) if ntpb is None else (20, 15)), rng=rng, now=now,
+                                   default_ntpb=ntpb, default_extra=extra)),
+        ('ack', w.ack_object(rng.randbytes(32), 4 * 24 * 3600, rng, now)),
+    ]
+    if ntpb is not None:  # the ack builder always uses the network default: give it the same one
+        objs[-1] = ('ack', w.PowObject(objs[-1][1].payload, objs[-1][1].ttl, ntpb, extra))
+    return objs
+
+
+def test_object_builders_follow_the_reference_layout():
+    """TTL rules and unencrypted headers of class_singleWorker.py:252-715, 1375-1493."""
+    from pybitmessage_amd import worker as w
+    rng = random.Random(1)
+    now = 1700000000
+    for _ in range(50):
+        assert 28 * 86400 - 300 <= w.pubkey_ttl(rng) < 28 * 86400 + 300
+        assert 7 * 86400 - 300 <= w.onionpeer_ttl(rng) < 7 * 86400 + 300
+        assert 3600 - 300 <= w.broadcast_ttl(10, rng) < 3600 + 300
+        assert 28 * 86400 - 300 <= w.broadcast_ttl(10 ** 9, rng) < 28 * 86400 + 300
+        t = w.getpubkey_ttl(2, rng)
+        assert isinstance(t, float) and 10 * 86400 - 300 <= t < 10 * 86400 + 300
+        assert 28 * 86400 - 300 <= w.getpubkey_ttl(7, rng) < 28 * 86400 + 300
+        assert 28 * 86400 - 300 <= w.msg_ttl(4 * 86400, 3, rng) < 28 * 86400 + 300
+    assert w.msg_difficulty(2, 5000, 5000) == (1000, 1000)      # v2: network defaults
+    assert w.msg_difficulty(4, 10, 20) == (1000, 1000)          # v3+: at least the defaults
+    assert w.msg_difficulty(4, 3000, 1500) == (3000, 1500)
+    objs = dict(_mixed_objects(random.Random(2), now=now))
+    for name, o in objs.items():
+        expires = struct.unpack('>Q', o.payload[:8])[0]
+        assert expires == int(now + o.ttl), name
+        assert o.target == targets.object_target(len(o.payload), o.ttl, o.ntpb, o.extra)
+    assert objs['pubkey v2'].payload[8:12] == b'\x00\x00\x00\x01' and objs['pubkey v2'].payload[12:14] == b'\x02\x01'
+    assert len(objs['pubkey v2'].payload) == 8 + 4 + 2 + 4 + 128
+    assert objs['onionpeer v3'].payload[8:12] == struct.pack('>I', 0x746f72)
+    assert objs['onionpeer v3'].payload[12:14] == b'\x03\x01' and objs['onionpeer v2'].payload[12:14] == b'\x02\x01'
+    assert objs['onionpeer v3'].payload[14:17] == b'\xfd\x20\xfc'  # varint(8444)
+    assert objs['broadcast v4'].payload[8:14] == b'\x00\x00\x00\x03\x04\x01'
+    assert objs['broadcast v5'].payload[8:14] == b'\x00\x00\x00\x03\x05\x01'
+    assert objs['getpubkey v3'].payload[8:14] == b'\x00\x00\x00\x00\x03\x01'
+    assert objs['msg to v4'].payload[8:14] == b'\x00\x00\x00\x02\x01\x01'
+    assert (objs['msg to v4'].ntpb, objs['msg to v4'].extra) == (2000, 1500)
+    assert w.encode_host('127.0.0.1') == b'\x00' * 10 + b'\xff\xff\x7f\x00\x00\x01'
+
+
+def test_mixed_kinds_in_one_batch_cpu(oracle_batch, coracle):
+    """Every object kind in one pow_objects batch (test-mode difficulty), each answer the
+    sequential _doSafePoW nonce."""
+    objs = [o for _, o in _mixed_objects(random.Random(3), ntpb=10, extra=10)]
+    done = worker.pow_objects(objs)
+    for o, d in zip(objs, done):
+        nonce = struct.unpack('>Q', d[:8])[0]
+        assert d[8:] == o.payload
+        assert coracle.search(o.initial_hash, int(o.target))[1] == nonce
+
+
+@pytest.mark.gpu
+def test_gpu_mixed_kinds_in_one_batch(gpulib, coracle):
+    """Every singleWorker object kind (pubkey v2/v3/v4, onionpeer, broadcast v4/v5, getpubkey,
+    msg, ack) in one device batch at test-mode difficulty, vs the C oracle."""
+    rng = random.Random(4)
+    objs = []
+    for _ in range(20):
+        objs += [o for _, o in _mixed_objects(rng, ntpb=10, extra=10)]
+    done = worker.pow_objects(objs)
+    for o, d in zip(objs, done):
+        assert d[8:] == o.payload
+        assert (coracle.trial(struct.unpack('>Q', d[:8])[0], o.initial_hash), struct.unpack('>Q', d[:8])[0]) == \
+            coracle.search(o.initial_hash, int(o.target))

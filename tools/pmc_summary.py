@@ -6,7 +6,12 @@
 Derived (MI355X_MICROARCH.md conventions):
   * issued VALU instructions per trial = SQ_INSTS_VALU x 64 / trials
   * effective clock = GRBM_GUI_ACTIVE / 8 XCDs / kernel time (sum over XCDs)
-  * VALU busy = SQ_ACTIVE_INST_VALU x 4 (quad-cycles) / (256 CUs x GRBM_GUI_ACTIVE / 8)  [per-CU share]
+  * VALU issue utilisation = (SQ_ACTIVE_INST_VALU - SQ_ACTIVE_INST_VALU2) / SIMD quad-cycles, with
+    SIMD quad-cycles = 1,024 SIMDs x (GRBM_GUI_ACTIVE / 8) / 4: the share of every SIMD's quad-cycles
+    in which it issued at least one VALU instruction (SQ_ACTIVE_INST_VALU counts one quad-cycle per
+    wave-instruction -- it equals SQ_INSTS_VALU here -- and SQ_ACTIVE_INST_VALU2 the quad-cycles in
+    which a SIMD issued two); dual-issue share = VALU2 / ACTIVE_INST_VALU.  rocprof's own VALUBusy
+    (100 x ACTIVE_INST_VALU / CUs / GRBM, its gfx94x formula) is reported beside it.
   * HBM bytes = (2 x FETCH_SIZE + WRITE_SIZE) x 1024: FETCH_SIZE reads half the bytes of wide streams
     on gfx950 (guide §HBM); this kernel's reads are scalar/64-bit, so the doubled figure is an upper bound.
 """
@@ -40,7 +45,7 @@ def main():
     root = sys.argv[1]
     trials = float(sys.argv[2]) if len(sys.argv) > 2 else float(1 << 28)
     out = {'trials_per_launch': trials}
-    for p in ['instr', 'busy', 'valu', 'fetch', 'write']:
+    for p in ['instr', 'busy', 'issue', 'valu', 'fetch', 'write']:
         path = os.path.join(root, p, 'run_counter_collection.csv')
         if not os.path.exists(path):
             continue
@@ -52,14 +57,25 @@ def main():
     res = {}
     if out.get('SQ_INSTS_VALU'):
         res['valu_instr_per_trial'] = out['SQ_INSTS_VALU'] * 64 / trials
-        res['salu_instr_per_trial'] = out['SQ_INSTS_SALU'] * 64 / trials
-        res['waves_per_launch'] = out['SQ_WAVES']
+        if out.get('SQ_INSTS_SALU') is not None:
+            res['salu_instr_per_trial'] = out['SQ_INSTS_SALU'] * 64 / trials
+            res['waves_per_launch'] = out['SQ_WAVES']
     if out.get('GRBM_GUI_ACTIVE') and out.get('instr_ns'):
         res['eff_clock_ghz'] = out['GRBM_GUI_ACTIVE'] / 8 / out['instr_ns']
-    if out.get('SQ_ACTIVE_INST_VALU') and out.get('busy_ns'):
-        cyc = out['busy_ns'] * res.get('eff_clock_ghz', 2.4)
-        res['valu_busy_frac'] = out['SQ_ACTIVE_INST_VALU'] * 4 / 256 / cyc / 4  # 4 SIMDs per CU
-        res['wave_cycles_per_trial'] = out['SQ_WAVE_CYCLES'] * 4 * 64 / trials
+    if out.get('SQ_ACTIVE_INST_VALU2') is not None and out.get('GRBM_GUI_ACTIVE'):
+        quad = 1024 * out['GRBM_GUI_ACTIVE'] / 8 / 4  # SIMD quad-cycles per launch
+        res['valu_issue_util'] = (out['SQ_ACTIVE_INST_VALU'] - out['SQ_ACTIVE_INST_VALU2']) / quad
+        res['valu_instr_per_simd_quad_cycle'] = out['SQ_ACTIVE_INST_VALU'] / quad
+        res['dual_issue_share'] = out['SQ_ACTIVE_INST_VALU2'] / out['SQ_ACTIVE_INST_VALU']
+        res['rocprof_VALUBusy_pct'] = 100 * out['SQ_ACTIVE_INST_VALU'] / 256 / out['GRBM_GUI_ACTIVE'] * 8
+        if out.get('SQ_BUSY_CU_CYCLES'):
+            res['simd_busy_frac'] = out['SQ_BUSY_CU_CYCLES'] / quad
+        if out.get('SQ_WAVE_CYCLES'):
+            res['wave_issue_stall_share'] = out['SQ_WAIT_INST_ANY'] / out['SQ_WAVE_CYCLES']
+            if out.get('SQ_WAIT_ANY') is not None:
+                res['wave_wait_share'] = out['SQ_WAIT_ANY'] / out['SQ_WAVE_CYCLES']
+        if out.get('issue_ns'):
+            res['eff_clock_ghz_issue_pass'] = out['GRBM_GUI_ACTIVE'] / 8 / out['issue_ns']
     if out.get('SQ_INSTS_VALU_INT32') is not None:
         res['int32_per_trial'] = out['SQ_INSTS_VALU_INT32'] * 64 / trials
         res['int64_per_trial'] = out['SQ_INSTS_VALU_INT64'] * 64 / trials

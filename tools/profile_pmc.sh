@@ -9,13 +9,15 @@ LOG2=${2:-33}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 CMD=(python3 bench.py --config c3 --c3-log2 "$LOG2" --steps 1 --warmup 0 --no-cpu-baseline)
+if [ -n "${PMC_DEFAULT_BENCH:-}" ]; then CMD=(python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline); fi
 pass() {
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- "${CMD[@]}" \
     > "$OUT/$name.bench.json" 2> "$OUT/$name.err"
 }
 pass instr SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM GRBM_GUI_ACTIVE
-pass busy SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE
+pass issue SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
+  SQ_WAIT_ANY GRBM_GUI_ACTIVE
 pass valu SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE
 pass fetch FETCH_SIZE
 pass write WRITE_SIZE
