@@ -23,6 +23,7 @@ kernels actually hashed (incl. the work past a hit that the early exit did not c
 reported beside it.
 """
 import argparse
+import ctypes
 import hashlib
 import json
 import os
@@ -43,17 +44,11 @@ OPS_PER_TRIAL = 8288
 PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
 #: BASELINE.md section 3 priced the roofline at 64 lanes/clk/CU (39.32 T); kept for comparison
 BASELINE_MD_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
-#: issued instructions per trial of bm_search_kernel (tools/isa_census.py on the gfx950 ISA) and
-#: their measured issue rates, lane-ops/clk/CU (tools/ubench_valu.hip, profiles/r01_ubench_valu.json).
-#: v_alignbit_b32, v_lshl_add_u64, v_lshrrev_b64 and v_bitop3_b32 have no full-rate encoding, so the
-#: trial's instruction mix, not PEAK_TOPS, is the ceiling this kernel can reach.  (SHR64 is one
-#: v_lshrrev_b64 since r01's last kernel revision; it was v_alignbit_b32 + v_lshrrev_b32 before.)
-#: v_bitop3_b32 at 81.0: its effective rate between half-rate VOP3 ops, from the alternating
-#: alignbit/bitop3 stream of tools/ubench_banks (71.0 lane-ops/clk/CU per instruction,
-#: profiles/r01_ubench_coissue.json: 2 / 71.0 - 1 / 63.2 = 1 / 81.0); alone it co-issues at ~122.
-ISA_MIX = {'v_alignbit_b32': (2788, 63.2), 'v_bitop3_b32': (1716, 81.0), 'v_lshl_add_u64': (1420, 63.1),
-           'v_lshrrev_b64': (226, 63.6), 'other': (46, 117.8)}
-ISSUE_CLK_PER_TRIAL_PER_CU = sum(c / r for c, r in ISA_MIX.values())
+#: The VALU issue model behind the roofline (profiles/r02): a wave64 VALU
+#: instruction occupies its SIMD for one quad-cycle (4 clocks) unless two waves' full-rate 32-bit ops
+#: pair in it (SQ_ACTIVE_INST_VALU2); bm_search_kernel's mix is 73 % half-rate VOP3 (v_alignbit_b32,
+#: v_lshl_add_u64, v_lshrrev_b64), so its ceiling is one instruction per SIMD per quad-cycle.
+SIMDS = 256 * 4
 
 
 def object_target(L, ttl, ntpb=1000, extra=1000):
@@ -209,7 +204,10 @@ def run_batch_bench(args, dist):
 
     from pybitmessage_amd import _lib, proofofwork
     per_gpu = args.objects or {'c2': 1024, 'c4': 64, 'c5': 100000}[args.config]
-    objs, desc = make_objects(args.config, 0, per_gpu * dist.world)
+    units = dist.world * max(1, args.devices)
+    if args.config == 'c4' and args.devices and not args.objects:
+        units = 1  # BASELINE C4: 64 objects in all, nonce-sharded over the in-process devices
+    objs, desc = make_objects(args.config, 0, per_gpu * units)
     lib = _lib.get()
     n = len(objs)
     ihs = b''.join(ih for _, ih in objs)
@@ -251,6 +249,38 @@ def run_batch_bench(args, dist):
         desc += ' (global batch of %d, pieces of %d claimed on demand)' % (n, chunk)
     return {'desc': desc, 'objects': len(idx) * args.steps, 'useful': useful, 'elapsed': elapsed, 'stats': st,
             'nonces_sum': int(sum(int(nonce[i]) for i in idx))}
+
+
+def run_service_bench(args, dist):
+    """C2/C5 through worker.PowService: every object submitted to the service (producers joining a
+    resident device session, bmpow_batch_add / bmpow_batch_take_done), all futures awaited; the
+    same objects and answers as the batch leg, so the two objects/s figures compare directly."""
+    from pybitmessage_amd import _lib, worker
+    per_gpu = args.objects or {'c2': 1024, 'c5': 4096}[args.config]
+    objs, desc = make_objects(args.config, dist.rank, per_gpu)
+    lib = _lib.get()
+
+    def once():
+        svc = worker.PowService().start()
+        try:
+            futs = [svc.submit(t, ih) for t, ih in objs]
+            return [f.result() for f in futs]
+        finally:
+            svc.stop(30)
+    for _ in range(args.warmup):
+        once()
+    dist.barrier()
+    lib.bmpow_reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = once()
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = _lib.BmpowStats()
+    lib.bmpow_get_stats(ctypes.byref(st))
+    useful = float(sum(n for _, n in res)) * args.steps
+    return {'desc': desc + ' via worker.PowService (resident session)', 'objects': len(objs) * args.steps,
+            'useful': useful, 'elapsed': elapsed, 'stats': st}
 
 
 def run_c3_bench(args, dist):
@@ -647,6 +677,12 @@ def main():
     ap.add_argument('--cpu-mode', default='c', choices=['c', 'fast'], help=argparse.SUPPRESS)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--share-device', action='store_true', help=argparse.SUPPRESS)
+    ap.add_argument('--devices', type=int, default=0,
+                    help='one process driving this many GPUs in-process (bmpow_set_devices: one object\'s '
+                         'nonce space sharded over them, host min-reduction); 0 = one GPU per rank')
+    ap.add_argument('--service', action='store_true',
+                    help='c2/c5: feed the objects through worker.PowService (resident session, '
+                         'bmpow_batch_add/take_done) instead of one batch')
     ap.add_argument('--cpu-baseline-worker', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_baseline_worker:
@@ -656,7 +692,12 @@ def main():
     dist = Dist()
     # one process per GPU; --share-device puts every rank on GPU 0 (rehearsing the multi-rank
     # path on a one-GPU box: the ranks then split one GPU, so the value is not a scaling number)
-    os.environ['BMPOW_DEVICES'] = '0' if args.share_device else str(dist.local_rank)
+    if args.devices:
+        if dist.world > 1:
+            raise SystemExit('--devices drives several GPUs from one process: run it without torch.distributed')
+        os.environ['BMPOW_DEVICES'] = ','.join(str(i) for i in range(args.devices))
+    else:
+        os.environ['BMPOW_DEVICES'] = '0' if args.share_device else str(dist.local_rank)
     from pybitmessage_amd import _lib
     lib = _lib.get()
     if args.step_trials:
@@ -682,7 +723,16 @@ def main():
         return
     runner = {'c1': run_c1_bench, 'c2': run_batch_bench, 'c3': run_c3_bench, 'c4': run_batch_bench,
               'c5': run_batch_bench}[args.config]
+    if args.service:
+        if args.config not in ('c2', 'c5'):
+            raise SystemExit('--service applies to c2 and c5')
+        runner = run_service_bench
+    if args.devices:
+        n = lib.bmpow_get_devices((ctypes.c_int * 64)(), 64)
+        if n != args.devices:
+            raise SystemExit('asked for %d devices, the library selected %d' % (args.devices, n))
     r = runner(args, dist)
+    r['devices'] = args.devices
     line = summarize(args, dist, r, lib.bmpow_version().decode())
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_threads or None)
@@ -733,31 +783,42 @@ def summarize(args, dist, r, lib_version):
             'kernel_busy_frac': round(kernel_ms * 1e-3 / r['elapsed'], 4),
             'frac_vs_baseline_md_peak': round(achieved / BASELINE_MD_PEAK_TOPS, 4),
         }
-        pmc = pmc_traffic()
+        pmc = pmc_counters()
         if pmc:
-            line['roofline'].update(pmc)
-        clk = (pmc or {}).get('eff_clock_ghz_pmc') or 2.4
-        ceiling = 256 * clk * 1e9 / ISSUE_CLK_PER_TRIAL_PER_CU / 1e9
-        line['roofline']['issue_ceiling'] = {
-            'ghs': round(ceiling, 4), 'clock_ghz': clk, 'frac': round(kernel_ghs / ceiling, 4),
-            'basis': 'per-trial instruction mix of the gfx950 ISA x measured issue rates (bench.ISA_MIX)'}
+            line['roofline']['traffic'] = pmc.pop('traffic')
+            line['roofline']['counters'] = pmc
+            if pmc.get('valu_instr_per_trial') and pmc.get('eff_clock_ghz'):
+                # one wave64 VALU instruction per SIMD per quad-cycle, at the PMC run's clock
+                ceil = SIMDS * pmc['eff_clock_ghz'] * 1e9 / 4 * 64 / pmc['valu_instr_per_trial'] / 1e9
+                line['roofline']['single_issue_ceiling'] = {
+                    'ghs': round(ceil, 4), 'frac': round(kernel_ghs / ceil, 4),
+                    'basis': '1,024 SIMDs x one VALU instruction per quad-cycle x 64 lanes / VALU instructions '
+                             'per trial (SQ_INSTS_VALU), at the PMC run clock (GRBM_GUI_ACTIVE / 8 / kernel time)'}
+    if r.get('devices'):
+        line['config']['parallelism'] = ('in-process nonce/object sharding over %d devices (bmpow_set_devices, '
+                                         'host min-reduction, no collective)' % r['devices'])
+        line['n_gpus'] = r['devices']
     return line
 
 
-def pmc_traffic():
-    """HBM bytes per bm_search_kernel launch from the committed rocprofv3 PMC passes
-    (tools/profile_pmc.sh -> tools/pmc_summary.py -> profiles/pmc_latest.json): FETCH_SIZE
-    doubled (gfx950 under-count, MI355X_MICROARCH.md §HBM) + WRITE_SIZE, KB -> bytes.  The
-    algorithmic traffic is ~0 (9 words per workgroup); the counters bound the real traffic."""
+def pmc_counters():
+    """bm_search_kernel's hardware counters from the committed rocprofv3 PMC passes
+    (tools/profile_pmc.sh -> tools/pmc_summary.py -> profiles/pmc_latest.json; C3 launches of 2^28
+    trials, one counter group per pass): HBM bytes per launch = FETCH_SIZE doubled (gfx950
+    under-count, MI355X_MICROARCH.md section HBM) + WRITE_SIZE -- the algorithmic traffic is ~0 (9
+    words per workgroup) --, and the VALU issue figures (SQ_ACTIVE_INST_VALU / _VALU2 per SIMD
+    quad-cycle)."""
     path = os.path.join(ROOT, 'profiles', 'pmc_latest.json')
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)['derived']
-    return {'traffic': d.get('hbm_bytes_per_launch_upper'),
-            'traffic_source': 'profiles/pmc_latest.json (C3 launches of 2^28 trials)',
-            'valu_instr_per_trial_pmc': round(d.get('valu_instr_per_trial', 0), 1),
-            'eff_clock_ghz_pmc': round(d.get('eff_clock_ghz', 0), 3)}
+    out = {'traffic': d.get('hbm_bytes_per_launch_upper'), 'source': 'profiles/pmc_latest.json (C3, 2^28-trial launches)'}
+    for k in ('valu_instr_per_trial', 'valu_issue_util', 'valu_instr_per_simd_quad_cycle', 'dual_issue_share',
+              'simd_busy_frac', 'wave_issue_stall_share', 'wave_wait_share', 'eff_clock_ghz'):
+        if d.get(k) is not None:
+            out[k] = round(d[k], 4)
+    return out
 
 
 if __name__ == '__main__':

@@ -214,8 +214,7 @@ __host__ __device__ inline uint32_t ar_tries_per_lane(uint32_t mode) { return mo
 // The first of the lane's ntries tries (k0, k0 + 1, ...) whose ripe has the prefix; 4 if none.
 template <int W>
 BM_DEV uint32_t try_quad(const ar_params* __restrict__ prm, const ge* __restrict__ table, uint64_t k0, uint32_t ntries,
-                         uint32_t* st, uint32_t lane) {
-  const bool fixed_sign = prm->mode != 0;
+                         uint32_t* st, uint32_t lane, bool fixed_sign) {
   fe z0, z1, z2;
   uint32_t bad = 0;  // bit t: a key of try t is 0 mod n
   gej r;             // after the loop: key 3 (no copy of it is kept live across the loop)
@@ -244,7 +243,9 @@ BM_DEV uint32_t try_quad(const ar_params* __restrict__ prm, const ge* __restrict
   ec::fe_mul(ia, inv, zb);
   ec::fe_mul(ib, inv, za);
   uint32_t hit = 4;
-  ge saved;  // mode 0: the encryption key (odd key) of the try being assembled
+  ge saved;  // mode 0: the encryption key (odd key) of the try being assembled; never read in mode 1
+  ec::fe_set(saved.x, 0);  // (only through a select), but defined there too
+  ec::fe_set(saved.y, 0);
 #pragma unroll 1
   for (int q = 3; q >= 0; --q) {  // one affine + hash body for every key (key 3 first: it is live)
     fe it, zp, zi, x, y;
@@ -335,18 +336,18 @@ template <bool kResolve, int W>
 __global__ __launch_bounds__(64) AR_OCC void ar_search_kernel(const ar_params* __restrict__ prm, const ge* __restrict__ table,
                                                        uint64_t start, uint32_t count,
                                                        unsigned long long* __restrict__ best,
-                                                       ar_result* __restrict__ out) {
+                                                       ar_result* __restrict__ out, uint32_t mode) {
   const uint32_t g = blockIdx.x * 64 + threadIdx.x;
 #ifndef AR_SINGLE
   if (!kResolve) {  // lane g: tries start + T g .. start + T g + T - 1 below start + count (T = 2 or 4)
     __shared__ uint32_t stash[3 * 16 * kPairLanes];
-    const uint32_t T = ar_tries_per_lane(prm->mode);
+    const uint32_t T = ar_tries_per_lane(mode);  // the host sized the grid with this same argument
     const uint64_t first = (uint64_t)T * g;
     if (first >= count) return;
     const uint64_t k0 = start + first;
     if (__hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < k0) return;
     const uint32_t ntries = (uint32_t)min((uint64_t)T, count - first);
-    const uint32_t hit = try_quad<W>(prm, table, k0, ntries, stash, threadIdx.x);
+    const uint32_t hit = try_quad<W>(prm, table, k0, ntries, stash, threadIdx.x, mode != 0);
     if (hit < ntries) atomicMin(best, (unsigned long long)(k0 + hit));
     return;
   }
@@ -453,7 +454,7 @@ hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, uint32_t mode,
                             uint64_t start, uint32_t count, unsigned long long* best) {
   if (count == 0) return hipSuccess;
 #ifndef AR_SINGLE
-  const uint32_t tpl = ar_tries_per_lane(mode);  // must match what the kernel reads from prm->mode
+  const uint32_t tpl = ar_tries_per_lane(mode);  // the kernel takes the same mode argument
 #else
   const uint32_t tpl = 1;
   (void)mode;
@@ -461,10 +462,10 @@ hipError_t ar_launch_search(hipStream_t st, const ar_params* prm, uint32_t mode,
   const uint32_t lanes = (uint32_t)(((uint64_t)count + tpl - 1) / tpl);
   if (wbits == ec::kCombLarge)
     hipLaunchKernelGGL((ar_search_kernel<false, ec::kCombLarge>), dim3((lanes + 63) / 64), dim3(64), 0, st, prm, table,
-                       start, count, best, (ar_result*)nullptr);
+                       start, count, best, (ar_result*)nullptr, mode);
   else
     hipLaunchKernelGGL((ar_search_kernel<false, ec::kCombSmall>), dim3((lanes + 63) / 64), dim3(64), 0, st, prm, table,
-                       start, count, best, (ar_result*)nullptr);
+                       start, count, best, (ar_result*)nullptr, mode);
   return hipGetLastError();
 }
 
@@ -474,10 +475,10 @@ hipError_t ar_launch_resolve(hipStream_t st, const ar_params* prm, const ge* tab
                              ar_result* out) {
   if (wbits == ec::kCombLarge)
     hipLaunchKernelGGL((ar_search_kernel<true, ec::kCombLarge>), dim3(1), dim3(64), 0, st, prm, table, k, 1u,
-                       (unsigned long long*)nullptr, out);
+                       (unsigned long long*)nullptr, out, 0u /* the resolve path (try_keys) reads prm->mode */);
   else
     hipLaunchKernelGGL((ar_search_kernel<true, ec::kCombSmall>), dim3(1), dim3(64), 0, st, prm, table, k, 1u,
-                       (unsigned long long*)nullptr, out);
+                       (unsigned long long*)nullptr, out, 0u /* the resolve path (try_keys) reads prm->mode */);
   return hipGetLastError();
 }
 

@@ -12,6 +12,12 @@
 // multiples of p added to make a matrix product divisible by 2^30 touch three limbs only.
 // Invariants: f = d x (mod p), g = e x (mod p); at the end g = 0, f = +-1, so x^-1 = +-d.
 //
+// The structure follows libsecp256k1's 32-bit safegcd implementation (src/modinv32_impl.h, MIT
+// licence; the reference uses secp256k1 through OpenSSL, not libsecp256k1): zeta-form 30-divstep
+// batches on the low words, and the update of d, e with the multiple of p chosen from
+// p^-1 mod 2^30 so each product is exactly divisible by 2^30.  Rewritten here for a wave of 64
+// lanes (branch-free selects, the 9-limb representation and p's three nonzero limbs).
+//
 // Plain C++ (int32/int64 only): the same source compiles for gfx950 and for the host, where
 // tests/test_modinv.py checks it against Python's pow(x, -1, p).
 #pragma once

@@ -17,8 +17,10 @@ Differences from the reference, each a fix of an Appendix-B quirk:
 """
 import ctypes
 import logging
+import time
 
 from . import _lib
+from . import proofofwork
 from . import state
 from ._lib import BmpowUnavailable
 
@@ -92,13 +94,18 @@ def do_opencl_pow(hash_, target):
         return 0
     ih = bytes.fromhex(hash_) if isinstance(hash_, str) else bytes(hash_)
     ih = ih + b'\x00' * (64 - len(ih))
-    target = min(int(target), _lib.U64_MAX)
+    # a negative target is unsatisfiable (never wrapped into a u64, which would accept nonce 1):
+    # wait, interruptibly, as the reference's kernel loop would spin
+    target, satisfiable = proofofwork._clamp_target(target)
     lib = _lib.get()
     n, tv = ctypes.c_uint64(), ctypes.c_uint64()
     start = 1
     while True:
         if state.shutdown != 0:
             raise Exception('Interrupted')
+        if not satisfiable:
+            time.sleep(0.05)
+            continue
         rc = _lib.check(lib, lib.bmpow_search(ih, target, start, CALL_TRIALS, ctypes.byref(n), ctypes.byref(tv)),
                         'bmpow_search')
         if rc == _lib.FOUND:

@@ -253,6 +253,28 @@ def test_hippow_without_device(monkeypatch):
     assert hippow.do_opencl_pow('00' * 64, 2 ** 60) == 0  # reference: 0 when no GPU is enabled
 
 
+def test_hippow_negative_target_never_searches(monkeypatch):
+    """A negative target is unsatisfiable: do_opencl_pow must not wrap it into a u64 (which would
+    accept nonce 1) -- it waits, interruptibly, and never calls the search."""
+    calls = []
+
+    class Lib(object):
+        def bmpow_search(self, *a):
+            calls.append(a)
+            return _lib.FOUND
+    monkeypatch.setattr(_lib, 'get', lambda: Lib())
+    monkeypatch.setattr(hippow, 'enabledGpus', [0])
+    timer = threading.Timer(0.2, lambda: setattr(state, 'shutdown', 1))
+    timer.start()
+    try:
+        with pytest.raises(Exception, match='Interrupted'):
+            hippow.do_opencl_pow('00' * 64, -5)
+    finally:
+        timer.join()
+        state.shutdown = 0
+    assert calls == []
+
+
 # ------------------------------------------------------------------ GPU
 gpu = pytest.mark.gpu
 
