@@ -189,3 +189,16 @@ def test_verify_rejects_wrong_gpu_answer():
         proofofwork._verify(2 ** 64 // 1000, ih, 2417842470843602, 1315)
     with pytest.raises(_lib.BmpowError):
         proofofwork._verify(10, ih, 2417842470843601, 1315)
+
+
+def test_sender_targets_match_the_reference_expressions(golden):
+    """targets.object_target against the reference's own _doPOWDefaults and sendMsg target
+    statements (class_singleWorker.py:222-230, 1256-1264), evaluated by
+    tests/golden/make_target_golden.py: bit-exact floats, at network-default and test-mode
+    difficulty, int and float (requestPubKey) TTLs, recipient difficulties."""
+    d = golden('sender_targets_ref.json')
+    assert len(d['cases']) > 700
+    for c in d['cases']:
+        t = targets.object_target(c['L'], c['ttl'], c['ntpb'], c['extra'])
+        assert t == float.fromhex(c['target_float']), c
+        assert int(t) == c['target']
