@@ -375,13 +375,22 @@ def run_verify_bench(args, dist):
     # end to end, the way a caller uses it: host buffers in, verdicts out (padding and sorting on
     # the host, PCIe upload, kernel, IEEE-double verdicts) -- reported beside, never as `value`
     # (first call: allocates the library's staging and device buffers; later floods reuse them)
-    e2e = []
+    e2e, parts = [], []
     for _ in range(3):
+        lib.bmpow_reset_stats()
         t1 = time.perf_counter()
         ok = verify.isProofOfWorkSufficient_batch(objs, recvTime=1700000000)
         e2e.append(time.perf_counter() - t1)
+        s2 = _lib.BmpowStats()
+        lib.bmpow_get_stats(ctypes.byref(s2))
+        parts.append({'build_ms': round(s2.verify_host_build_ms, 2), 'run_ms': round(s2.verify_host_run_ms, 2),
+                      'verdict_ms': round(s2.verify_host_verdict_ms, 2), 'kernel_ms': round(s2.verify_kernel_ms, 3),
+                      'marshal_ms': round(e2e[-1] * 1e3 - s2.verify_host_build_ms - s2.verify_host_run_ms
+                                          - s2.verify_host_verdict_ms, 2)})
         assert len(ok) == n
-    return {'e2e_objects_per_s': n / min(e2e[1:]), 'e2e_s': min(e2e[1:]), 'e2e_first_s': e2e[0],
+    best = 1 + min(range(2), key=lambda i: e2e[1 + i])
+    return {'e2e_objects_per_s': n / e2e[best], 'e2e_s': e2e[best], 'e2e_first_s': e2e[0], 'e2e_parts': parts[best],
+            'e2e_fast_marshalling': verify._fast() is not None,
             'desc': 'verify: %d received objects (50%% acks, 25%% pubkeys, 25%% msgs 0.5-16 KB), POW of each '
                     '(protocol.isProofOfWorkSufficient hashing) resident in HBM' % n,
             'objects': n * args.steps, 'elapsed': elapsed, 'stats': st, 'payload_bytes': payload_bytes * args.steps}
@@ -400,7 +409,8 @@ def summarize_verify(args, dist, r, lib_version):
         'config': {'workload': r['desc'], 'parallelism': 'object-sharded dp%d' % dist.world, 'lib': lib_version},
         'payload_GBps': round(nbytes / el_max / 1e9, 3),
         'e2e_host_buffers': {'objects_per_s': round(r['e2e_objects_per_s'], 1), 'seconds': round(r['e2e_s'], 3),
-                             'first_call_seconds': round(r['e2e_first_s'], 3),
+                             'first_call_seconds': round(r['e2e_first_s'], 3), 'parts': r['e2e_parts'],
+                             'c_marshalling': r['e2e_fast_marshalling'],
                              'what': 'bmpow_verify_batch_ptrs from host buffers: sort + pad into pinned staging '
                                      'overlapped with the PCIe upload + kernel + verdicts (rank 0; best of 2 '
                                      'calls after the first, which allocates the reused buffers)'},

@@ -269,6 +269,10 @@ typedef struct bmpow_stats {
     /* min-trial probe (bmpow_min_trial*) */
     uint64_t probe_trials;    /* nonces hashed by the probe */
     double probe_kernel_ms;   /* sum over launches of probe-kernel time (HIP events) */
+    /* host-side wall time of bmpow_verify_batch* (steady clock), summed over calls */
+    double verify_host_build_ms;    /* sort, layout, padding into pinned staging, PCIe upload issued */
+    double verify_host_run_ms;      /* kernel + results back (waits for the uploads) */
+    double verify_host_verdict_ms;  /* IEEE-double verdicts */
 } bmpow_stats;
 
 BMPOW_API int bmpow_get_stats(bmpow_stats *out);

@@ -48,7 +48,9 @@ class BmpowStats(ctypes.Structure):
                 ('verify_objects', ctypes.c_uint64), ('verify_blocks', ctypes.c_uint64),
                 ('verify_kernel_ms', ctypes.c_double), ('addr_launches', ctypes.c_uint64),
                 ('addr_tries', ctypes.c_uint64), ('addr_kernel_ms', ctypes.c_double),
-                ('probe_trials', ctypes.c_uint64), ('probe_kernel_ms', ctypes.c_double)]
+                ('probe_trials', ctypes.c_uint64), ('probe_kernel_ms', ctypes.c_double),
+                ('verify_host_build_ms', ctypes.c_double), ('verify_host_run_ms', ctypes.c_double),
+                ('verify_host_verdict_ms', ctypes.c_double)]
 
 
 class BmpowAddress(ctypes.Structure):

@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1255,14 +1256,21 @@ static int verify_spans_locked(size_t n, const uint8_t* const* ptrs, const uint6
     spans.push_back({ptrs[i], lens[i]});
     idx.push_back(i);
   }
+  using clk = std::chrono::steady_clock;
+  auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+  const clk::time_point t0 = clk::now();
   std::vector<uint64_t> pow(spans.size());
   if (!spans.empty()) {
     bmpow_vbatch vb;
     int rc = vbatch_build(&vb, spans, true);
+    const clk::time_point t1 = clk::now();
     if (rc == 0) rc = vbatch_run_locked(&vb, pow.data());
+    g_stats.verify_host_build_ms += ms(t0, t1);
+    g_stats.verify_host_run_ms += ms(t1, clk::now());
     vbatch_free(&vb);
     if (rc < 0) return rc;
   }
+  const clk::time_point t2 = clk::now();
   const int64_t now = (int64_t)std::time(nullptr);
   for (size_t j = 0; j < spans.size(); ++j) {
     const size_t i = idx[j];
@@ -1270,6 +1278,7 @@ static int verify_spans_locked(size_t n, const uint8_t* const* ptrs, const uint6
     ok_out[i] = (uint8_t)pow_sufficient(pow[j], spans[j].len, ntpb ? ntpb[i] : 0, extra ? extra[i] : 0, recv,
                                         load_be64(spans[j].p + 8));
   }
+  g_stats.verify_host_verdict_ms += ms(t2, clk::now());
   return 0;
 }
 

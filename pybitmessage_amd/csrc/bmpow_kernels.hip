@@ -54,9 +54,10 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __res
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     ihw[i] = o->w[i];
-#ifdef BM_IHW_VGPR
-    asm volatile("" : "+v"(ihw[i]));  // A/B variant: per-object words (and what is hoisted from them) in VGPRs
-#endif
+    // The per-object words, and the terms hoisted from them, live in VGPRs: left in SGPRs they
+    // overflow the SGPR budget and every trial pays v_readlane reloads of the spilled ones (32 per
+    // trial -> 18).  Same-box A/B, C3: 6.345 vs 6.302 GH/s (profiles/r02/search_kernel_ab*.txt).
+    asm volatile("" : "+v"(ihw[i]));
   }
   const uint64_t target = o->target;
 

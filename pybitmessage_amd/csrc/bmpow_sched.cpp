@@ -322,9 +322,24 @@ int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& par
   }
   if (total > 0xffffffffULL) return BMPOW_E_ARG;  // payload pool above 2^32 blocks (512 GiB)
   total_blocks = total;
+  // stable counting sort by block count, descending (block counts are small: <= 2,049 for the
+  // protocol's 256 KiB objects, larger ones fall into one overflow bucket sorted on their own)
+  constexpr uint32_t kBuckets = 4096;
   std::vector<uint32_t> order(n);
-  for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)i;
-  std::stable_sort(order.begin(), order.end(), [&](uint32_t a, uint32_t b) { return nblk[a] > nblk[b]; });
+  {
+    std::vector<size_t> cnt(kBuckets + 1, 0);
+    for (size_t i = 0; i < n; ++i) cnt[std::min(nblk[i], kBuckets)]++;
+    std::vector<size_t> pos(kBuckets + 1, 0);
+    size_t acc = 0;
+    for (size_t b = kBuckets + 1; b-- > 0;) {  // descending
+      pos[b] = acc;
+      acc += cnt[b];
+    }
+    for (size_t i = 0; i < n; ++i) order[pos[std::min(nblk[i], kBuckets)]++] = (uint32_t)i;
+    if (cnt[kBuckets] > 1)
+      std::stable_sort(order.begin(), order.begin() + (ptrdiff_t)cnt[kBuckets],
+                       [&](uint32_t a, uint32_t b) { return nblk[a] > nblk[b]; });
+  }
   size_t k = 0;
   uint64_t acc = 0;
   for (size_t s = 0; s < S && k < n; ++s) {

@@ -10,6 +10,7 @@ target arithmetic (host side of the C ABI).  No CPU fallback: without the HIP li
 calls raise :class:`BmpowUnavailable`.
 """
 import ctypes
+import os
 import struct
 
 import numpy as np
@@ -78,6 +79,34 @@ def _pointers(objs):
     return np.frombuffer(arr, dtype=np.uint64).copy()
 
 
+def _load_fast():
+    """The CPython marshalling module built beside the library (csrc/bmpow_pyext.c): walks a list of
+    bytes in C and calls bmpow_verify_batch_ptrs with the GIL released.  None when not built (the
+    numpy marshalling below is then used; the hashing is on the GPU either way)."""
+    import glob
+    import importlib.util
+    for path in glob.glob(os.path.join(os.path.dirname(_lib.lib_path()), '_bmpow_fast*.so')):
+        try:
+            spec = importlib.util.spec_from_file_location('_bmpow_fast', path)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            return mod
+        except (ImportError, OSError):
+            continue
+    return None
+
+
+_FAST = None
+_FAST_TRIED = False
+
+
+def _fast():
+    global _FAST, _FAST_TRIED
+    if not _FAST_TRIED:
+        _FAST, _FAST_TRIED = _load_fast(), True
+    return _FAST
+
+
 def isProofOfWorkSufficient_batch(objects, nonceTrialsPerByte=0, payloadLengthExtraBytes=0, recvTime=0):
     """``[protocol.isProofOfWorkSufficient(o, nonceTrialsPerByte, payloadLengthExtraBytes,
     recvTime) for o in objects]`` with one GPU launch.  Each difficulty argument and
@@ -91,6 +120,17 @@ def isProofOfWorkSufficient_batch(objects, nonceTrialsPerByte=0, payloadLengthEx
     n = len(objs)
     if n == 0:
         return []
+    fast = _fast()
+    if fast is not None and not (np.ndim(nonceTrialsPerByte) or np.ndim(payloadLengthExtraBytes) or np.ndim(recvTime)):
+        lib = _lib.get()
+        if type(objs) is not list:
+            objs = list(objs)
+        addr = ctypes.cast(lib.bmpow_verify_batch_ptrs, ctypes.c_void_p).value
+        rc, ok = fast.verify_list(addr, objs, int(nonceTrialsPerByte), int(payloadLengthExtraBytes), int(recvTime))
+        _lib.check(lib, rc, 'bmpow_verify_batch_ptrs')
+        if 2 in ok:
+            raise struct.error('unpack requires a buffer of 8 bytes')
+        return np.frombuffer(ok, dtype=np.uint8).view(np.bool_).tolist()
     ptrs = _pointers(objs)
     lens = np.fromiter(map(len, objs), dtype=np.uint64, count=n)
     ntpb = _per_object(nonceTrialsPerByte, n, np.uint64)

@@ -170,3 +170,35 @@ def test_gpu_offsets_and_pointer_entry_points_agree(gpulib, kats):
                                                       ok2.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))), 'ptrs')
     assert ok1.tolist() == ok2.tolist()
     assert ok1.tolist() == [1] * (n - 2) + [2, 0]
+
+
+def test_fast_marshalling_passes_every_object_in_place():
+    """csrc/bmpow_pyext.c (the CPython walk of the object list) hands bmpow_verify_batch_ptrs each
+    bytes object's own buffer and length, the scalar difficulty and recvTime, and returns its flags
+    -- checked with a ctypes stand-in for the entry point (no device)."""
+    import ctypes
+
+    from pybitmessage_amd import verify
+    fast = verify._load_fast()
+    if fast is None:
+        pytest.skip('_bmpow_fast not built')
+    objs = [bytes([i % 251]) * (16 + i) for i in range(3000)]
+    seen = {}
+    proto = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
+                             ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                             ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
+                             ctypes.POINTER(ctypes.c_uint8))
+
+    def fake(n, ptrs, lens, ntpb, extra, recv, ok):
+        seen['n'] = n
+        for i in range(n):
+            assert ctypes.string_at(ptrs[i], lens[i]) == objs[i]
+            assert (ntpb[i], extra[i], recv[i]) == (1234, 5678, 1700000000)
+            ok[i] = lens[i] & 1
+        return 0
+    cb = proto(fake)
+    rc, ok = fast.verify_list(ctypes.cast(cb, ctypes.c_void_p).value, objs, 1234, 5678, 1700000000)
+    assert rc == 0 and seen['n'] == len(objs)
+    assert list(ok) == [len(o) & 1 for o in objs]
+    with pytest.raises(TypeError):
+        fast.verify_list(ctypes.cast(cb, ctypes.c_void_p).value, [b'x' * 20, bytearray(20)], 0, 0, 0)
