@@ -585,7 +585,6 @@ int vbatch_upload_transient(bmpow_vbatch::Part& pt, const std::vector<Span>& obj
   pt.d_pow = sh.d_vpow;
   pt.h_pow = sh.h_vpow;
   pt.borrowed = true;
-  HIPTRY(hipMemcpy(pt.d_obj, ho.data(), m * sizeof(bv_obj), hipMemcpyHostToDevice));
   // chunks of whole objects; an object larger than a chunk is padded in pageable memory on its own
   size_t j = 0;
   int c = 0;
@@ -619,6 +618,9 @@ int vbatch_upload_transient(bmpow_vbatch::Part& pt, const std::vector<Span>& obj
     }
     j = j1;
   }
+  // the descriptors last: the padding pass filled their nonces (one pass over the objects' memory)
+  HIPTRY(hipMemcpyAsync(pt.d_obj, ho.data(), m * sizeof(bv_obj), hipMemcpyHostToDevice, sh.stream));
+  HIPTRY(hipStreamSynchronize(sh.stream));
   return 0;
 }
 
@@ -1259,7 +1261,7 @@ static int verify_spans_locked(size_t n, const uint8_t* const* ptrs, const uint6
   using clk = std::chrono::steady_clock;
   auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   const clk::time_point t0 = clk::now();
-  std::vector<uint64_t> pow(spans.size());
+  std::vector<uint64_t> pow(spans.size()), eol(spans.size());
   if (!spans.empty()) {
     bmpow_vbatch vb;
     int rc = vbatch_build(&vb, spans, true);
@@ -1267,17 +1269,20 @@ static int verify_spans_locked(size_t n, const uint8_t* const* ptrs, const uint6
     if (rc == 0) rc = vbatch_run_locked(&vb, pow.data());
     g_stats.verify_host_build_ms += ms(t0, t1);
     g_stats.verify_host_run_ms += ms(t1, clk::now());
+    for (const auto& pt : vb.parts)  // expiresTime, read by the padding pass
+      for (size_t j = 0; j < pt.orig.size(); ++j) eol[pt.orig[j]] = pt.eol[j];
     vbatch_free(&vb);
     if (rc < 0) return rc;
   }
   const clk::time_point t2 = clk::now();
   const int64_t now = (int64_t)std::time(nullptr);
-  for (size_t j = 0; j < spans.size(); ++j) {
-    const size_t i = idx[j];
-    const int64_t recv = (recv_time && recv_time[i]) ? recv_time[i] : now;
-    ok_out[i] = (uint8_t)pow_sufficient(pow[j], spans[j].len, ntpb ? ntpb[i] : 0, extra ? extra[i] : 0, recv,
-                                        load_be64(spans[j].p + 8));
-  }
+  bmsched::parallel_for(spans.size(), 32768, [&](size_t a, size_t b) {
+    for (size_t j = a; j < b; ++j) {
+      const size_t i = idx[j];
+      const int64_t recv = (recv_time && recv_time[i]) ? recv_time[i] : now;
+      ok_out[i] = (uint8_t)pow_sufficient(pow[j], spans[j].len, ntpb ? ntpb[i] : 0, extra ? extra[i] : 0, recv, eol[j]);
+    }
+  });
   g_stats.verify_host_verdict_ms += ms(t2, clk::now());
   return 0;
 }

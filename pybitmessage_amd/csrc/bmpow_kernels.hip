@@ -26,7 +26,10 @@ using namespace bm;
 // ---------------------------------------------------------------------------------------
 // Search kernel.
 // ---------------------------------------------------------------------------------------
-__global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __restrict__ objs,
+#ifndef BM_SEARCH_WAVES
+#define BM_SEARCH_WAVES 1  // minimum waves per SIMD the register allocation must allow (A/B knob)
+#endif
+__global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(const bm_obj* __restrict__ objs,
                                                              const bm_item* __restrict__ items,
                                                              uint32_t nitems,
                                                              unsigned long long* __restrict__ best,
@@ -57,7 +60,9 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_kernel(const bm_obj* __res
     // The per-object words, and the terms hoisted from them, live in VGPRs: left in SGPRs they
     // overflow the SGPR budget and every trial pays v_readlane reloads of the spilled ones (32 per
     // trial -> 18).  Same-box A/B, C3: 6.345 vs 6.302 GH/s (profiles/r02/search_kernel_ab*.txt).
+#ifndef BM_IHW_SGPR
     asm volatile("" : "+v"(ihw[i]));
+#endif
   }
   const uint64_t target = o->target;
 

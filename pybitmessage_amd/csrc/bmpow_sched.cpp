@@ -353,37 +353,44 @@ int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& par
       bv_obj o;
       o.blk = (uint32_t)blk;
       o.nblk = nblk[i];
-      o.nonce = load_be64(objs[i].p);
+      o.nonce = 0;  // pad_range reads it with the payload
       pt.ho.push_back(o);
       blk += nblk[i];
       acc += nblk[i];
       ++k;
     }
     pt.blocks = blk;
+    pt.eol.assign(pt.orig.size(), 0);
     if (!pt.orig.empty()) parts.push_back(std::move(pt));
   }
   return 0;
 }
 
-void pad_range(const std::vector<Span>& objs, const VPart& pt, size_t j0, size_t j1, uint64_t blk0, uint8_t* dst) {
+void parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)>& body) {
+  const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency());
+  const size_t nth = std::max<size_t>(1, std::min<size_t>({16, hw, n / std::max<size_t>(grain, 1) + 1}));
+  if (nth == 1) return body(0, n);
+  std::vector<std::thread> th;
+  for (size_t t = 1; t < nth; ++t) th.emplace_back(body, n * t / nth, n * (t + 1) / nth);
+  body(0, n / nth);
+  for (auto& x : th) x.join();
+}
+
+void pad_range(const std::vector<Span>& objs, VPart& pt, size_t j0, size_t j1, uint64_t blk0, uint8_t* dst) {
   if (j1 <= j0) return;
-  const std::vector<bv_obj>& ho = pt.ho;
+  std::vector<bv_obj>& ho = pt.ho;
   const size_t m = j1 - j0;
   const uint64_t bytes = (uint64_t)(ho[j1 - 1].blk + ho[j1 - 1].nblk - ho[j0].blk) * 128;
   // a thread per ~2 MB (and per >= 64 objects), at most 16
-  const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency());
-  const size_t nth = std::max<size_t>(1, std::min<size_t>({16, hw, bytes / (2u << 20) + 1, m / 64 + 1}));
-  auto work = [&](size_t t) {
-    for (size_t j = j0 + m * t / nth; j < j0 + m * (t + 1) / nth; ++j) {
+  const size_t grain = std::max<size_t>(64, (size_t)(m / (bytes / (2u << 20) + 1)));
+  parallel_for(m, grain, [&](size_t a, size_t b) {
+    for (size_t j = j0 + a; j < j0 + b; ++j) {
       const Span& sp = objs[pt.orig[j]];
+      ho[j].nonce = load_be64(sp.p);
+      pt.eol[j] = sp.len >= 16 ? load_be64(sp.p + 8) : 0;
       pad_into(sp.p + 8, sp.len - 8, dst + (uint64_t)(ho[j].blk - blk0) * 128, ho[j].nblk);
     }
-  };
-  if (nth == 1) return work(0);
-  std::vector<std::thread> th;
-  for (size_t t = 1; t < nth; ++t) th.emplace_back(work, t);
-  work(0);
-  for (auto& x : th) x.join();
+  });
 }
 
 // Python ints until the true division by 2**16 (correctly rounded: the exact 128-bit product
@@ -396,7 +403,8 @@ int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, in
   if (ttl < 300) ttl = 300;
   const unsigned __int128 le = (unsigned __int128)len + extra;
   const unsigned __int128 prod = (unsigned __int128)ttl * le;
-  const double q = (double)prod / 65536.0;
+  // int -> double correctly rounded either way; the int64 conversion is the hardware one
+  const double q = (prod >> 63) ? (double)prod / 65536.0 : (double)(int64_t)prod / 65536.0;
   const double x = (double)le + q;
   const double y = (double)ntpb * x;
   const double t = 18446744073709551616.0 / y;

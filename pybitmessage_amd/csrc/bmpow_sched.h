@@ -14,6 +14,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <functional>
 #include <vector>
 
 #include "../../include/bmpow.h"
@@ -113,16 +114,22 @@ struct VPart {
   size_t shard = 0;
   std::vector<uint32_t> orig;  // sorted position -> input index
   std::vector<bv_obj> ho;      // per sorted position: first block (part-relative), blocks, nonce
+  std::vector<uint64_t> eol;   // per sorted position: expiresTime (object[8:16]; 0 if shorter), set by pad_range
   uint64_t blocks = 0;
 };
 
 // Sort objects by padded block count (descending, stable) and cut them into per-shard parts of
-// equal block totals.  Returns BMPOW_E_ARG on size limits, else 0.
+// equal block totals.  Reads only the lengths: the objects' bytes are first touched by pad_range,
+// which also fills each descriptor's nonce and expiresTime (one pass over memory, in parallel).
+// Returns BMPOW_E_ARG on size limits, else 0.
 int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& parts, uint64_t& total_blocks);
 
-// Pad objects [j0, j1) of a part (sorted order) into dst (their blocks from blk0 on), over up to 16
-// host threads: a memory-bound copy of every payload.
-void pad_range(const std::vector<Span>& objs, const VPart& pt, size_t j0, size_t j1, uint64_t blk0, uint8_t* dst);
+// Pad objects [j0, j1) of a part (sorted order) into dst (their blocks from blk0 on) and fill their
+// nonce / expiresTime, over up to 16 host threads: a memory-bound copy of every payload.
+void pad_range(const std::vector<Span>& objs, VPart& pt, size_t j0, size_t j1, uint64_t blk0, uint8_t* dst);
+
+// The same thread fan-out for an index range (a thread per >= `grain` indices, at most 16).
+void parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)>& body);
 
 // protocol.isProofOfWorkSufficient's comparison (src/protocol.py:272-286) in the reference's
 // arithmetic.  1 sufficient, 0 not.

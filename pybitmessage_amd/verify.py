@@ -115,22 +115,25 @@ def isProofOfWorkSufficient_batch(objects, nonceTrialsPerByte=0, payloadLengthEx
     ``unpack('>Q', data[8:16])`` does.  The objects are read where they lie
     (``bmpow_verify_batch_ptrs``): no concatenation on the host."""
     objs = objects if type(objects) is list else list(objects)
-    if set(map(type, objs)) - {bytes}:  # bytearray / memoryview: one bytes copy each
-        objs = [o if type(o) is bytes else bytes(o) for o in objs]
     n = len(objs)
     if n == 0:
         return []
     fast = _fast()
     if fast is not None and not (np.ndim(nonceTrialsPerByte) or np.ndim(payloadLengthExtraBytes) or np.ndim(recvTime)):
         lib = _lib.get()
-        if type(objs) is not list:
-            objs = list(objs)
         addr = ctypes.cast(lib.bmpow_verify_batch_ptrs, ctypes.c_void_p).value
-        rc, ok = fast.verify_list(addr, objs, int(nonceTrialsPerByte), int(payloadLengthExtraBytes), int(recvTime))
+        args = (int(nonceTrialsPerByte), int(payloadLengthExtraBytes), int(recvTime))
+        try:
+            rc, ok = fast.verify_list(addr, objs, *args)
+        except TypeError:  # bytearray / memoryview items: one bytes copy each
+            objs = [o if type(o) is bytes else bytes(o) for o in objs]
+            rc, ok = fast.verify_list(addr, objs, *args)
         _lib.check(lib, rc, 'bmpow_verify_batch_ptrs')
         if 2 in ok:
             raise struct.error('unpack requires a buffer of 8 bytes')
         return np.frombuffer(ok, dtype=np.uint8).view(np.bool_).tolist()
+    if set(map(type, objs)) - {bytes}:  # bytearray / memoryview: one bytes copy each
+        objs = [o if type(o) is bytes else bytes(o) for o in objs]
     ptrs = _pointers(objs)
     lens = np.fromiter(map(len, objs), dtype=np.uint64, count=n)
     ntpb = _per_object(nonceTrialsPerByte, n, np.uint64)

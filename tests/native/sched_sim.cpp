@@ -364,7 +364,7 @@ static void scenario_verify() {
     CHECK(plan_verify(spans, S, parts, total) == 0, "plan_verify failed");
     uint64_t seen = 0;
     std::vector<int> hits(spans.size(), 0);
-    for (const VPart& pt : parts) {
+    for (VPart& pt : parts) {
       seen += pt.blocks;
       for (size_t j = 1; j < pt.ho.size(); ++j) CHECK(pt.ho[j].nblk <= pt.ho[j - 1].nblk, "not sorted by blocks");
       std::vector<uint8_t> pool(pt.blocks * 128, 0xEE);
@@ -374,6 +374,7 @@ static void scenario_verify() {
         hits[pt.orig[j]]++;
         const uint64_t m = sp.len - 8, nb = padded_blocks(m);
         CHECK(pt.ho[j].nblk == nb && pt.ho[j].nonce == load_be64(sp.p), "object descriptor");
+        CHECK(pt.eol[j] == (sp.len >= 16 ? load_be64(sp.p + 8) : 0), "expiresTime of object %u", pt.orig[j]);
         std::vector<uint8_t> want(nb * 128, 0);
         memcpy(want.data(), sp.p + 8, m);
         want[m] = 0x80;
