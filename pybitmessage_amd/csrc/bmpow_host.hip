@@ -486,7 +486,25 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
 // Library-owned scratch batch reused by the stateless entry points.
 bmpow_batch* g_scratch = nullptr;
 
+// Reused while it is large enough and the device set is unchanged: a run() call (one object per
+// bounded bmpow_search) then pays one upload of its 128-B record, not three hipMalloc/hipFree pairs.
 int scratch_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
+  if (g_scratch && g_scratch->dev.size() == g_shards.size() && g_scratch->cap >= n) {
+    const size_t cap = g_scratch->cap;
+    bmsched::init(*g_scratch, n, ihs, targets, start);
+    g_scratch->cap = cap;
+    for (size_t s = 0; s < g_shards.size(); ++s) {
+      Shard& sh = g_shards[s];
+      HIPTRY(hipSetDevice(sh.dev));
+      if (!n) continue;
+      HIPTRY(hipMemcpyAsync(g_scratch->dev[s].d_obj, g_scratch->objs.data(), n * sizeof(bm_obj), hipMemcpyHostToDevice,
+                            sh.stream));
+      HIPTRY(hipMemsetAsync(g_scratch->dev[s].d_best, 0xFF, n * sizeof(unsigned long long), sh.stream));
+      HIPTRY(hipMemsetAsync(g_scratch->dev[s].d_found, 0, n * sizeof(uint32_t), sh.stream));
+    }
+    // no host sync needed: the step's launches follow on the same streams
+    return 0;
+  }
   if (g_scratch) {
     batch_free_dev(g_scratch);
     delete g_scratch;

@@ -26,8 +26,13 @@ using namespace bm;
 // ---------------------------------------------------------------------------------------
 // Search kernel.
 // ---------------------------------------------------------------------------------------
+// Register budget for 5 waves per SIMD (<= 96 VGPRs; the allocator keeps 12 dwords of loop-invariant
+// per-object terms in scratch, 6 scratch_load_dwordx2 per iteration, L1-resident).  Same-box A/B, C3
+// 2^35 nonces, on three boxes: 6.53-6.59 GH/s against 6.30-6.39 at the 4 waves of 120 VGPRs
+// (profiles/r02/search_kernel_ab_waves*.txt).  The gain needs the per-object words in VGPRs too: with
+// them in SGPRs (BM_IHW_SGPR) 5 waves fit without scratch but run no faster than 4.
 #ifndef BM_SEARCH_WAVES
-#define BM_SEARCH_WAVES 1  // minimum waves per SIMD the register allocation must allow (A/B knob)
+#define BM_SEARCH_WAVES 5
 #endif
 __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(const bm_obj* __restrict__ objs,
                                                              const bm_item* __restrict__ items,
