@@ -207,7 +207,7 @@ def run_batch_bench(args, dist):
     units = dist.world * max(1, args.devices)
     if args.config == 'c4' and args.devices and not args.objects:
         units = 1  # BASELINE C4: 64 objects in all, nonce-sharded over the in-process devices
-    objs, desc = make_objects(args.config, 0, per_gpu * units)
+    objs, desc = make_objects(args.config, 0, per_gpu * units, test_mode=args.test_mode)
     lib = _lib.get()
     n = len(objs)
     ihs = b''.join(ih for _, ih in objs)
@@ -257,13 +257,13 @@ def run_service_bench(args, dist):
     same objects and answers as the batch leg, so the two objects/s figures compare directly."""
     from pybitmessage_amd import _lib, worker
     per_gpu = args.objects or {'c2': 1024, 'c5': 4096}[args.config]
-    objs, desc = make_objects(args.config, dist.rank, per_gpu)
+    objs, desc = make_objects(args.config, dist.rank, per_gpu, test_mode=args.test_mode)
     lib = _lib.get()
 
     def once():
         svc = worker.PowService().start()
         try:
-            futs = [svc.submit(t, ih) for t, ih in objs]
+            futs = svc.submit_many(objs)
             return [f.result() for f in futs]
         finally:
             svc.stop(30)
@@ -690,6 +690,9 @@ def main():
     ap.add_argument('--devices', type=int, default=0,
                     help='one process driving this many GPUs in-process (bmpow_set_devices: one object\'s '
                          'nonce space sharded over them, host min-reduction); 0 = one GPU per rank')
+    ap.add_argument('--test-mode', action='store_true',
+                    help='c5: the reference\'s test-mode difficulty (ntpb and extra / 100): 100k objects of '
+                         '~2e4 trials each, so per-object host and launch costs dominate')
     ap.add_argument('--service', action='store_true',
                     help='c2/c5: feed the objects through worker.PowService (resident session, '
                          'bmpow_batch_add/take_done) instead of one batch')

@@ -343,7 +343,10 @@ class PowService(object):
     (``bmpow_batch_add``, only their 64-byte hashes and targets cross PCIe), each
     ``bmpow_batch_step`` is one bounded launch per device over every pending object, and
     finished objects are popped with ``bmpow_batch_take_done`` -- the per-step host work is
-    O(new + finished), never a walk over the whole table.  An object submitted mid-flight joins
+    O(new + finished), never a walk over the whole table.  A second thread completes the finished
+    objects (hashlib re-check, as ``_doGPUPoW`` does, then the future) while the service thread's
+    next step runs on the device with the GIL released, so the per-object Python work overlaps the
+    kernels instead of idling the GPU between steps.  An object submitted mid-flight joins
     the next step (~40 ms on one MI355X) instead of waiting for the objects ahead of it, and
     producers never contend for the device.  Replaces concurrent blocking ``run`` calls from the
     worker and API threads (``class_singleWorker.py:236,1276``, ``api.py:1304,1350``)."""
@@ -356,14 +359,22 @@ class PowService(object):
         self._incoming = []
         self._stopping = False
         self._thread = None
+        self._completer = None
+        self._done_q = None
         self.calls = 0
         self.solved = 0
 
     def start(self):
         with self._cv:
             if self._thread is None:
+                import queue
                 self._stopping = False
-                self._thread = threading.Thread(target=self._loop, name='PowService')
+                self._done_q = queue.Queue()
+                self._completer = threading.Thread(target=self._complete, args=(self._done_q,),
+                                                   name='PowService-complete')
+                self._completer.daemon = True
+                self._completer.start()
+                self._thread = threading.Thread(target=self._loop, args=(self._done_q,), name='PowService')
                 self._thread.daemon = True
                 self._thread.start()
         return self
@@ -375,7 +386,10 @@ class PowService(object):
             th = self._thread
         if th is not None:
             th.join(timeout)
+        if self._completer is not None:
+            self._completer.join(timeout)
         self._thread = None
+        self._completer = None
 
     def submit(self, target, initialHash):
         fut = Future()
@@ -391,6 +405,25 @@ class PowService(object):
             self._cv.notify_all()
         return fut
 
+    def submit_many(self, objects):
+        """``[submit(t, ih) for t, ih in objects]`` under one lock and one wake-up: a producer with
+        many objects at once (a flood of acks, every pending pubkey) joins the next step together."""
+        futs, entries = [], []
+        for target, initialHash in objects:
+            fut = Future()
+            futs.append(fut)
+            t, ok = proofofwork._clamp_target(target)
+            if not ok:
+                fut.set_exception(ValueError('negative target: no nonce can satisfy it'))
+                continue
+            entries.append(_Entry(proofofwork._ih_bytes(initialHash), t, fut))
+        with self._cv:
+            if self._stopping or self._thread is None:
+                raise RuntimeError('PowService is not running')
+            self._incoming.extend(entries)
+            self._cv.notify_all()
+        return futs
+
     def run(self, target, initialHash):
         """Blocking ``proofofwork.run`` through the shared batch."""
         if state.shutdown != 0:
@@ -403,7 +436,25 @@ class PowService(object):
             if not e.future.done():
                 e.future.set_exception(exc)
 
-    def _loop(self):
+    def _complete(self, q):
+        """Completion thread: re-check each found nonce with hashlib and resolve its future."""
+        while True:
+            batch = q.get()
+            if batch is None:
+                return
+            for e, done, tv, nn in batch:
+                if done == _lib.DONE_FOUND:
+                    try:
+                        proofofwork._verify(e.target, e.ih, tv, nn)
+                    except Exception as err:  # noqa: BLE001
+                        e.future.set_exception(err)
+                        continue
+                    self.solved += 1
+                    e.future.set_result([tv, nn])
+                else:
+                    e.future.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
+
+    def _loop(self, done_q):
         import numpy as np
         p64 = ctypes.POINTER(ctypes.c_uint64)
         pu32 = ctypes.POINTER(ctypes.c_uint32)
@@ -466,19 +517,10 @@ class PowService(object):
                             h, self.TAKE, slot_buf.ctypes.data_as(pu32), nonce_buf.ctypes.data_as(p64),
                             trial_buf.ctypes.data_as(p64), done_buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
                             'bmpow_batch_take_done')
-                        for j in range(k):
-                            e = live.pop(int(slot_buf[j]))
-                            if done_buf[j] == _lib.DONE_FOUND:
-                                tv, nn = int(trial_buf[j]), int(nonce_buf[j])
-                                try:
-                                    proofofwork._verify(e.target, e.ih, tv, nn)
-                                except Exception as err:  # noqa: BLE001
-                                    e.future.set_exception(err)
-                                    continue
-                                self.solved += 1
-                                e.future.set_result([tv, nn])
-                            else:
-                                e.future.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
+                        if k:
+                            done_q.put([(live.pop(sl), d, tv, nn) for sl, d, tv, nn in
+                                        zip(slot_buf[:k].tolist(), done_buf[:k].tolist(), trial_buf[:k].tolist(),
+                                            nonce_buf[:k].tolist())])
                         if k < self.TAKE:
                             break
                 except Exception as e:  # noqa: BLE001
@@ -487,3 +529,4 @@ class PowService(object):
         finally:
             if h is not None and lib is not None:
                 lib.bmpow_batch_destroy(h)
+            done_q.put(None)  # the completion thread drains what is queued, then exits

@@ -218,6 +218,21 @@ def test_powservice_concurrent_producers(batchlib, coracle):
         svc.stop(5)
 
 
+def test_powservice_submit_many(batchlib, coracle):
+    svc = worker.PowService().start()
+    try:
+        rng = random.Random(12)
+        jobs = [(U64 // rng.choice([50, 2000, 9000]), rng.randbytes(64)) for _ in range(40)] + [(-1, bytes(64))]
+        futs = svc.submit_many(jobs)
+        for (t, ih), f in zip(jobs[:-1], futs[:-1]):
+            assert f.result(60) == list(coracle.search(ih, t))
+        with pytest.raises(ValueError):
+            futs[-1].result(1)
+        assert svc.solved == 40
+    finally:
+        svc.stop(5)
+
+
 def test_powservice_shutdown_and_errors(batchlib):
     svc = worker.PowService().start()
     try:
