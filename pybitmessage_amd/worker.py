@@ -324,6 +324,63 @@ def msg_object(encrypted, to_address_version, stream, ttl, ntpb=None, extra=None
 # ------------------------------------------------------------------------------------------
 # continuous batching across producer threads
 # ------------------------------------------------------------------------------------------
+class _Group(object):
+    """One condition shared by the results of one ``submit_many`` call."""
+    __slots__ = ('cv',)
+
+    def __init__(self):
+        self.cv = threading.Condition()
+
+
+class BatchResult(object):
+    """The result of one object of a ``PowService.submit_many`` call: ``result(timeout)``,
+    ``exception(timeout)`` and ``done()`` as on a ``concurrent.futures.Future``, without its
+    per-object lock and condition (a Future costs more to create than the object's whole host-side
+    handling; the results of one call share one condition, notified once per completed batch)."""
+    __slots__ = ('_group', '_value', '_exc', '_done')
+
+    def __init__(self, group):
+        self._group = group
+        self._value = None
+        self._exc = None
+        self._done = False
+
+    def done(self):
+        return self._done
+
+    def _wait(self, timeout):
+        if not self._done:
+            with self._group.cv:
+                if not self._group.cv.wait_for(lambda: self._done, timeout):
+                    raise TimeoutError('PoW result not ready')
+
+    def result(self, timeout=None):
+        self._wait(timeout)
+        if self._exc is not None:
+            raise self._exc
+        return self._value
+
+    def exception(self, timeout=None):
+        self._wait(timeout)
+        return self._exc
+
+    # completion side (the service's completion thread; waiters are woken by _notify)
+    def set_result(self, value):
+        self._value = value
+        self._done = True
+
+    def set_exception(self, exc):
+        self._exc = exc
+        self._done = True
+
+
+def _notify(entries):
+    groups = {id(e.future._group): e.future._group for e in entries if type(e.future) is BatchResult}
+    for g in groups.values():
+        with g.cv:
+            g.cv.notify_all()
+
+
 class _Entry(object):
     __slots__ = ('ih', 'target', 'future')
 
@@ -407,10 +464,12 @@ class PowService(object):
 
     def submit_many(self, objects):
         """``[submit(t, ih) for t, ih in objects]`` under one lock and one wake-up: a producer with
-        many objects at once (a flood of acks, every pending pubkey) joins the next step together."""
+        many objects at once (a flood of acks, every pending pubkey) joins the next step together.
+        Returns one :class:`BatchResult` per object (``result()`` gives ``[trialValue, nonce]``)."""
         futs, entries = [], []
+        group = _Group()
         for target, initialHash in objects:
-            fut = Future()
+            fut = BatchResult(group)
             futs.append(fut)
             t, ok = proofofwork._clamp_target(target)
             if not ok:
@@ -435,6 +494,7 @@ class PowService(object):
         for e in entries:
             if not e.future.done():
                 e.future.set_exception(exc)
+        _notify(entries)
 
     def _complete(self, q):
         """Completion thread: re-check each found nonce with hashlib and resolve its future."""
@@ -453,6 +513,7 @@ class PowService(object):
                     e.future.set_result([tv, nn])
                 else:
                     e.future.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
+            _notify([b[0] for b in batch])
 
     def _loop(self, done_q):
         import numpy as np
