@@ -283,6 +283,29 @@ def run_service_bench(args, dist):
             'useful': useful, 'elapsed': elapsed, 'stats': st}
 
 
+def run_runbatch_bench(args, dist):
+    """C2/C5 through the product entry point proofofwork.run_batch (session + stepping thread +
+    per-object hashlib re-check, each answer the _doSafePoW nonce)."""
+    from pybitmessage_amd import _lib, proofofwork
+    per_gpu = args.objects or {'c2': 1024, 'c5': 4096}[args.config]
+    objs, desc = make_objects(args.config, dist.rank, per_gpu, test_mode=args.test_mode)
+    lib = _lib.get()
+    for _ in range(args.warmup):
+        proofofwork.run_batch(objs)
+    dist.barrier()
+    lib.bmpow_reset_stats()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = proofofwork.run_batch(objs)
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = _lib.BmpowStats()
+    lib.bmpow_get_stats(ctypes.byref(st))
+    useful = float(sum(n for _, n in res)) * args.steps
+    return {'desc': desc + ' via proofofwork.run_batch', 'objects': len(objs) * args.steps,
+            'useful': useful, 'elapsed': elapsed, 'stats': st}
+
+
 def run_c3_bench(args, dist):
     """C3: fixed initialHash, target 0 (no hit), 2^log2 nonces split contiguously over ranks."""
     import ctypes
@@ -693,6 +716,8 @@ def main():
     ap.add_argument('--test-mode', action='store_true',
                     help='c5: the reference\'s test-mode difficulty (ntpb and extra / 100): 100k objects of '
                          '~2e4 trials each, so per-object host and launch costs dominate')
+    ap.add_argument('--run-batch', action='store_true',
+                    help='c2/c5: through proofofwork.run_batch (the product entry point, host re-check included)')
     ap.add_argument('--service', action='store_true',
                     help='c2/c5: feed the objects through worker.PowService (resident session, '
                          'bmpow_batch_add/take_done) instead of one batch')
@@ -736,10 +761,10 @@ def main():
         return
     runner = {'c1': run_c1_bench, 'c2': run_batch_bench, 'c3': run_c3_bench, 'c4': run_batch_bench,
               'c5': run_batch_bench}[args.config]
-    if args.service:
+    if args.service or args.run_batch:
         if args.config not in ('c2', 'c5'):
-            raise SystemExit('--service applies to c2 and c5')
-        runner = run_service_bench
+            raise SystemExit('--service / --run-batch apply to c2 and c5')
+        runner = run_service_bench if args.service else run_runbatch_bench
     if args.devices:
         n = lib.bmpow_get_devices((ctypes.c_int * 64)(), 64)
         if n != args.devices:

@@ -129,8 +129,15 @@ def iter_batch(objects, step_trials=0):
     ``(index, trialValue, nonce)`` as each finishes (ascending index within a step).
 
     The object table stays in HBM (``bmpow_batch_create``); each ``bmpow_batch_step`` is one
-    bounded launch per device over the pending objects, so large objects are nonce-sharded
-    and small ones packed many per launch.  Raises :class:`PowInterrupted` on shutdown."""
+    bounded launch per device over the pending objects, so large objects are nonce-sharded and
+    small ones packed many per launch.  A stepping thread drives the device and pops the finished
+    objects (``bmpow_batch_take_done``: O(finished) per step); this generator re-checks each with
+    hashlib and yields it meanwhile, so the per-object host work overlaps the next step's kernels
+    (the stepping thread holds no GIL inside the library).  ``state.shutdown`` is polled between
+    steps and raises :class:`PowInterrupted`."""
+    import queue
+    import threading
+
     import numpy as np
     lib = _lib.get()
     objs = list(objects)
@@ -150,27 +157,56 @@ def iter_batch(objects, step_trials=0):
     h = lib.bmpow_batch_create(n, ihs, targets.ctypes.data_as(p64), None)
     if not h:
         raise BmpowError(_lib.E_HIP, 'bmpow_batch_create: %s' % lib.bmpow_last_error().decode())
+    out = queue.Queue()
+    stop = threading.Event()
+    cap = min(n, 65536)
+
+    def stepper():
+        slots = np.zeros(cap, dtype=np.uint32)
+        nonce = np.zeros(cap, dtype=np.uint64)
+        trial = np.zeros(cap, dtype=np.uint64)
+        done = np.zeros(cap, dtype=np.uint8)
+        try:
+            pending = n
+            while pending > 0 and not stop.is_set():
+                if _interrupted():
+                    out.put(('interrupted',))
+                    return
+                pending = _lib.check(lib, lib.bmpow_batch_step(h, step_trials), 'bmpow_batch_step')
+                while True:
+                    k = _lib.check(lib, lib.bmpow_batch_take_done(
+                        h, cap, slots.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), nonce.ctypes.data_as(p64),
+                        trial.ctypes.data_as(p64), done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
+                        'bmpow_batch_take_done')
+                    if k:
+                        out.put(('done', slots[:k].tolist(), trial[:k].tolist(), nonce[:k].tolist(), done[:k].tolist()))
+                    if k < cap:
+                        break
+            out.put(('end',))
+        except Exception as e:  # noqa: BLE001 -- re-raised by the generator
+            out.put(('error', e))
+
+    th = threading.Thread(target=stepper, name='bmpow-iter_batch')
+    th.daemon = True
+    th.start()
     try:
-        nonce = np.zeros(n, dtype=np.uint64)
-        trial = np.zeros(n, dtype=np.uint64)
-        done = np.zeros(n, dtype=np.uint8)
-        reported = np.zeros(n, dtype=bool)
-        pending = n
-        while pending > 0:
-            if _interrupted():
+        while True:
+            msg = out.get()
+            if msg[0] == 'end':
+                return
+            if msg[0] == 'interrupted':
                 raise PowInterrupted('Interrupted')
-            pending = _lib.check(lib, lib.bmpow_batch_step(h, step_trials), 'bmpow_batch_step')
-            lib.bmpow_batch_results(h, nonce.ctypes.data_as(p64), trial.ctypes.data_as(p64),
-                                    done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), None)
-            fresh = np.flatnonzero((done != _lib.PENDING) & ~reported)
-            reported[fresh] = True
-            for i in fresh.tolist():
-                if done[i] != _lib.DONE_FOUND:
+            if msg[0] == 'error':
+                raise msg[1]
+            _, idx, tvs, nonces, dones = msg
+            for i, tv, nn, d in zip(idx, tvs, nonces, dones):
+                if d != _lib.DONE_FOUND:
                     raise BmpowError(_lib.E_ARG, 'object %d: nonce space exhausted' % i)
-                tv, nn = int(trial[i]), int(nonce[i])
                 _verify(int(targets[i]), ihs[64 * i:64 * i + 64], tv, nn)
                 yield i, tv, nn
     finally:
+        stop.set()
+        th.join()
         lib.bmpow_batch_destroy(h)
 
 

@@ -409,6 +409,7 @@ class PowService(object):
     worker and API threads (``class_singleWorker.py:236,1276``, ``api.py:1304,1350``)."""
 
     TAKE = 4096  # finished objects popped per bmpow_batch_take_done call
+    ADD_PER_STEP = 32768  # new objects appended to the device session per step
 
     def __init__(self, step_trials=0):
         self.step_trials = step_trials
@@ -548,7 +549,9 @@ class PowService(object):
                         self._incoming = []
                         drop(RuntimeError('PowService stopped'))
                         return
-                    new, self._incoming = self._incoming, []
+                    # at most ADD_PER_STEP join per step: a flood starts on the device while the rest
+                    # of it is still being appended, one step behind
+                    new, self._incoming = self._incoming[:self.ADD_PER_STEP], self._incoming[self.ADD_PER_STEP:]
                 if lib is None:
                     self._fail(new, lib_err)
                     continue

@@ -54,10 +54,12 @@ class BatchLib(object):
         self.next_handle = 1
 
     def bmpow_batch_create(self, n, ihs, tg, start):
-        assert n == 0
         h = self.next_handle
         self.next_handle += 1
         self.sessions[h] = {'objs': [], 'queue': [], 'free': []}
+        if n:
+            assert start is None
+            self.bmpow_batch_add(h, n, ihs, tg, None, (ctypes.c_uint32 * n)())
         return h
 
     def bmpow_batch_add(self, h, n, ihs, tg, start, slot_out):
@@ -216,6 +218,30 @@ def test_powservice_concurrent_producers(batchlib, coracle):
         assert not batchlib.sessions or all(not ses['queue'] for ses in batchlib.sessions.values())
     finally:
         svc.stop(5)
+
+
+def test_iter_batch_stepping_thread(batchlib, coracle):
+    """proofofwork.run_batch / iter_batch over the session ABI (stepping thread + take_done):
+    exact answers in input order, objects yielded as they finish, interrupt and early close."""
+    rng = random.Random(21)
+    objs = [(U64 // rng.choice([3, 400, 7000]), rng.randbytes(64)) for _ in range(60)]
+    assert proofofwork.run_batch(objs) == [list(coracle.search(ih, t)) for t, ih in objs]
+    seen = [i for i, _, _ in proofofwork.iter_batch(objs)]
+    assert sorted(seen) == list(range(len(objs))) and seen != list(range(len(objs)))  # finishing order
+    gen = proofofwork.iter_batch(objs)
+    next(gen)
+    gen.close()  # the stepping thread stops and the session is destroyed
+    assert not batchlib.sessions
+    hard = [(0, rng.randbytes(64))]  # never found
+    timer = threading.Timer(0.2, lambda: setattr(state, 'shutdown', 1))
+    timer.start()
+    try:
+        with pytest.raises(StopIteration):
+            proofofwork.run_batch(hard)
+    finally:
+        timer.join()
+        state.shutdown = 0
+    assert not batchlib.sessions
 
 
 def test_powservice_submit_many(batchlib, coracle):
