@@ -261,7 +261,10 @@ def run_service_bench(args, dist):
     lib = _lib.get()
 
     def once():
-        svc = worker.PowService().start()
+        svc = worker.PowService()
+        if args.service_add_per_step:
+            svc.ADD_PER_STEP = args.service_add_per_step
+        svc.start()
         try:
             futs = svc.submit_many(objs)
             return [f.result() for f in futs]
@@ -716,6 +719,7 @@ def main():
     ap.add_argument('--test-mode', action='store_true',
                     help='c5: the reference\'s test-mode difficulty (ntpb and extra / 100): 100k objects of '
                          '~2e4 trials each, so per-object host and launch costs dominate')
+    ap.add_argument('--service-add-per-step', type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument('--run-batch', action='store_true',
                     help='c2/c5: through proofofwork.run_batch (the product entry point, host re-check included)')
     ap.add_argument('--service', action='store_true',
