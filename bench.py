@@ -252,19 +252,17 @@ def run_batch_bench(args, dist):
 
 
 def run_service_bench(args, dist):
-    """C2/C5 through worker.PowService: every object submitted to the service (producers joining a
-    resident device session, bmpow_batch_add / bmpow_batch_take_done), all futures awaited; the
-    same objects and answers as the batch leg, so the two objects/s figures compare directly."""
+    """C2/C5 through worker.PowService: every object submitted to the service (the library's stepping
+    thread over a resident device session, bmpow_service_submit / bmpow_service_poll), all futures
+    awaited; the same objects and answers as the batch leg, so the two objects/s figures compare
+    directly."""
     from pybitmessage_amd import _lib, worker
     per_gpu = args.objects or {'c2': 1024, 'c5': 4096}[args.config]
     objs, desc = make_objects(args.config, dist.rank, per_gpu, test_mode=args.test_mode)
     lib = _lib.get()
 
     def once():
-        svc = worker.PowService()
-        if args.service_add_per_step:
-            svc.ADD_PER_STEP = args.service_add_per_step
-        svc.start()
+        svc = worker.PowService().start()
         try:
             futs = svc.submit_many(objs)
             return [f.result() for f in futs]
@@ -282,7 +280,7 @@ def run_service_bench(args, dist):
     st = _lib.BmpowStats()
     lib.bmpow_get_stats(ctypes.byref(st))
     useful = float(sum(n for _, n in res)) * args.steps
-    return {'desc': desc + ' via worker.PowService (resident session)', 'objects': len(objs) * args.steps,
+    return {'desc': desc + ' via worker.PowService (native stepping thread)', 'objects': len(objs) * args.steps,
             'useful': useful, 'elapsed': elapsed, 'stats': st}
 
 
@@ -719,7 +717,6 @@ def main():
     ap.add_argument('--test-mode', action='store_true',
                     help='c5: the reference\'s test-mode difficulty (ntpb and extra / 100): 100k objects of '
                          '~2e4 trials each, so per-object host and launch costs dominate')
-    ap.add_argument('--service-add-per-step', type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument('--run-batch', action='store_true',
                     help='c2/c5: through proofofwork.run_batch (the product entry point, host re-check included)')
     ap.add_argument('--service', action='store_true',

@@ -159,6 +159,36 @@ BMPOW_API int bmpow_batch_take_done(bmpow_batch *b, size_t cap, uint32_t *slot_o
 
 BMPOW_API void bmpow_batch_destroy(bmpow_batch *b);
 
+/* ---- continuous-batching service: a library thread steps one resident session while producers
+ *      submit and a consumer polls (worker.PowService; replaces concurrent blocking run() calls of
+ *      the worker and API threads, src/class_singleWorker.py:236,1276, src/api.py:1304,1350) ---- */
+typedef struct bmpow_service bmpow_service;
+
+/* Start the service thread.  step_budget: trials per step (0 = library default).  NULL on error. */
+BMPOW_API bmpow_service *bmpow_service_create(uint64_t step_budget);
+
+/* Queue n objects (ihs: n x 64 bytes, targets: n; every search starts at nonce 1); they join the
+ * session at the next step.  tickets_out[i] (may be NULL) = object i's ticket (ascending over the
+ * service's life).  Returns 0 or < 0. */
+BMPOW_API int bmpow_service_submit(bmpow_service *s, size_t n, const uint8_t *ihs, const uint64_t *targets,
+                                   uint64_t *tickets_out);
+
+/* Pop up to cap finished objects (ticket, nonce, trial, BMPOW_DONE_FOUND or BMPOW_DONE_EXHAUSTED),
+ * waiting up to timeout_ms (< 0: forever) for the first.  Returns the count (0 on timeout), or the
+ * error a step hit (< 0, bmpow_last_error() in this thread) once everything before it was popped;
+ * the service then steps nothing until bmpow_service_cancel. */
+BMPOW_API int bmpow_service_poll(bmpow_service *s, size_t cap, int timeout_ms, uint64_t *tickets, uint64_t *nonce_out,
+                                 uint64_t *trial_out, uint8_t *done_out);
+
+/* Drop every queued, live and unpolled object (and a pending error); the service keeps running. */
+BMPOW_API int bmpow_service_cancel(bmpow_service *s);
+
+/* Objects submitted and not yet popped by bmpow_service_poll. */
+BMPOW_API int bmpow_service_outstanding(bmpow_service *s);
+
+/* Stop the thread (after its current step) and free the session. */
+BMPOW_API void bmpow_service_destroy(bmpow_service *s);
+
 /* ---- receive-side verification (replaces protocol.isProofOfWorkSufficient,
  *      src/protocol.py:258-286, called once per received object from
  *      src/network/bmobject.py:71-76) ----

@@ -88,6 +88,12 @@ SIGNATURES = [
     ('bmpow_batch_add', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _pu32]),
     ('bmpow_batch_take_done', ctypes.c_int, [_vp, ctypes.c_size_t, _pu32, _p64, _p64, _pu8]),
     ('bmpow_batch_destroy', None, [_vp]),
+    ('bmpow_service_create', _vp, [_u64]),
+    ('bmpow_service_submit', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_char_p, _p64, _p64]),
+    ('bmpow_service_poll', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_int, _p64, _p64, _p64, _pu8]),
+    ('bmpow_service_cancel', ctypes.c_int, [_vp]),
+    ('bmpow_service_outstanding', ctypes.c_int, [_vp]),
+    ('bmpow_service_destroy', None, [_vp]),
     ('bmpow_get_stats', ctypes.c_int, [ctypes.POINTER(BmpowStats)]),
     ('bmpow_reset_stats', None, []),
     ('bmpow_get_step_trials', _u64, []),

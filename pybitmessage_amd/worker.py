@@ -395,77 +395,71 @@ class PowService(object):
 
     ``submit(target, initialHash)`` returns a ``concurrent.futures.Future`` that resolves to
     ``[trialValue, nonce]`` (the ``run`` answer) or raises ``StopIteration('Interrupted')``
-    when ``state.shutdown`` is set.  One service thread owns a resident device session
-    (``bmpow_batch_create``): new objects are appended to it between steps
-    (``bmpow_batch_add``, only their 64-byte hashes and targets cross PCIe), each
-    ``bmpow_batch_step`` is one bounded launch per device over every pending object, and
-    finished objects are popped with ``bmpow_batch_take_done`` -- the per-step host work is
-    O(new + finished), never a walk over the whole table.  A second thread completes the finished
-    objects (hashlib re-check, as ``_doGPUPoW`` does, then the future) while the service thread's
-    next step runs on the device with the GIL released, so the per-object Python work overlaps the
-    kernels instead of idling the GPU between steps.  An object submitted mid-flight joins
+    when ``state.shutdown`` is set.  The stepping runs inside the library
+    (``bmpow_service_create``): a native thread owns a resident device session, appends what
+    producers submitted between two steps (only 64-byte hashes and targets cross PCIe), launches
+    each bounded step over every pending object and queues the finished ones -- the per-step host
+    work is O(new + finished) and no Python thread (so no GIL) sits between two steps.  This
+    object's completion thread pops finished objects (``bmpow_service_poll``, GIL released while
+    it waits), re-checks each nonce with hashlib as ``_doGPUPoW`` does and resolves its future,
+    overlapping the Python work with the device's next step.  An object submitted mid-flight joins
     the next step (~40 ms on one MI355X) instead of waiting for the objects ahead of it, and
     producers never contend for the device.  Replaces concurrent blocking ``run`` calls from the
     worker and API threads (``class_singleWorker.py:236,1276``, ``api.py:1304,1350``)."""
 
-    TAKE = 4096  # finished objects popped per bmpow_batch_take_done call
-    ADD_PER_STEP = 32768  # new objects appended to the device session per step
+    TAKE = 4096  # finished objects popped per bmpow_service_poll call
+    POLL_MS = 100  # longest wait in one poll: bounds the reaction time to state.shutdown / stop()
 
     def __init__(self, step_trials=0):
         self.step_trials = step_trials
-        self._cv = threading.Condition()
-        self._incoming = []
+        self._lock = threading.Lock()  # guards _live and the service handle
+        self._live = {}  # ticket -> _Entry
+        self._lib = None
+        self._lib_err = None
+        self._h = None
         self._stopping = False
-        self._thread = None
         self._completer = None
-        self._done_q = None
-        self.calls = 0
         self.solved = 0
 
     def start(self):
-        with self._cv:
-            if self._thread is None:
-                import queue
+        with self._lock:
+            if self._completer is None:
                 self._stopping = False
-                self._done_q = queue.Queue()
-                self._completer = threading.Thread(target=self._complete, args=(self._done_q,),
-                                                   name='PowService-complete')
+                self._lib_err = None
+                try:
+                    self._lib = _lib.get()
+                    h = self._lib.bmpow_service_create(self.step_trials)
+                    if not h:
+                        raise _lib.BmpowError(_lib.E_HIP, 'bmpow_service_create: %s'
+                                              % self._lib.bmpow_last_error().decode())
+                    self._h = h
+                except Exception as e:  # noqa: BLE001 -- no device: every submitter sees why
+                    self._lib_err = e
+                self._completer = threading.Thread(target=self._complete, name='PowService-complete')
                 self._completer.daemon = True
                 self._completer.start()
-                self._thread = threading.Thread(target=self._loop, args=(self._done_q,), name='PowService')
-                self._thread.daemon = True
-                self._thread.start()
         return self
 
     def stop(self, timeout=None):
-        with self._cv:
+        with self._lock:
             self._stopping = True
-            self._cv.notify_all()
-            th = self._thread
+            th = self._completer
         if th is not None:
             th.join(timeout)
-        if self._completer is not None:
-            self._completer.join(timeout)
-        self._thread = None
         self._completer = None
 
     def submit(self, target, initialHash):
         fut = Future()
-        ih = proofofwork._ih_bytes(initialHash)
         t, ok = proofofwork._clamp_target(target)
         if not ok:
             fut.set_exception(ValueError('negative target: no nonce can satisfy it'))
             return fut
-        with self._cv:
-            if self._stopping or self._thread is None:
-                raise RuntimeError('PowService is not running')
-            self._incoming.append(_Entry(ih, t, fut))
-            self._cv.notify_all()
+        self._enqueue([_Entry(proofofwork._ih_bytes(initialHash), t, fut)])
         return fut
 
     def submit_many(self, objects):
-        """``[submit(t, ih) for t, ih in objects]`` under one lock and one wake-up: a producer with
-        many objects at once (a flood of acks, every pending pubkey) joins the next step together.
+        """``[submit(t, ih) for t, ih in objects]`` in one library call: a producer with many
+        objects at once (a flood of acks, every pending pubkey) joins the next step together.
         Returns one :class:`BatchResult` per object (``result()`` gives ``[trialValue, nonce]``)."""
         futs, entries = [], []
         group = _Group()
@@ -477,12 +471,33 @@ class PowService(object):
                 fut.set_exception(ValueError('negative target: no nonce can satisfy it'))
                 continue
             entries.append(_Entry(proofofwork._ih_bytes(initialHash), t, fut))
-        with self._cv:
-            if self._stopping or self._thread is None:
-                raise RuntimeError('PowService is not running')
-            self._incoming.extend(entries)
-            self._cv.notify_all()
+        self._enqueue(entries)
         return futs
+
+    def _enqueue(self, entries):
+        import numpy as np
+        with self._lock:
+            if self._stopping or self._completer is None:
+                raise RuntimeError('PowService is not running')
+            if not entries:
+                return
+            if self._h is None:
+                self._fail(entries, self._lib_err)
+                return
+            if state.shutdown != 0:
+                self._fail(entries, StopIteration('Interrupted'))
+                return
+            p64 = ctypes.POINTER(ctypes.c_uint64)
+            n = len(entries)
+            tg = np.fromiter((e.target for e in entries), dtype=np.uint64, count=n)
+            tickets = np.empty(n, dtype=np.uint64)
+            rc = self._lib.bmpow_service_submit(self._h, n, b''.join(e.ih for e in entries),
+                                                tg.ctypes.data_as(p64), tickets.ctypes.data_as(p64))
+            if rc < 0:
+                self._fail(entries, _lib.BmpowError(rc, 'bmpow_service_submit: %s'
+                                                    % self._lib.bmpow_last_error().decode()))
+                return
+            self._live.update(zip(tickets.tolist(), entries))
 
     def run(self, target, initialHash):
         """Blocking ``proofofwork.run`` through the shared batch."""
@@ -497,100 +512,63 @@ class PowService(object):
                 e.future.set_exception(exc)
         _notify(entries)
 
-    def _complete(self, q):
-        """Completion thread: re-check each found nonce with hashlib and resolve its future."""
-        while True:
-            batch = q.get()
-            if batch is None:
-                return
-            for e, done, tv, nn in batch:
-                if done == _lib.DONE_FOUND:
-                    try:
-                        proofofwork._verify(e.target, e.ih, tv, nn)
-                    except Exception as err:  # noqa: BLE001
-                        e.future.set_exception(err)
-                        continue
-                    self.solved += 1
-                    e.future.set_result([tv, nn])
-                else:
-                    e.future.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
-            _notify([b[0] for b in batch])
+    def _drop_live(self, exc):
+        """Cancel everything in the library and fail its futures (caller holds the lock)."""
+        dead = list(self._live.values())
+        self._live.clear()
+        self._lib.bmpow_service_cancel(self._h)
+        self._fail(dead, exc)
 
-    def _loop(self, done_q):
+    def _complete(self):
+        """Completion thread: pop finished objects, re-check each found nonce with hashlib and
+        resolve its future; cancels on state.shutdown; destroys the library service on stop()."""
         import numpy as np
+        lib, h = self._lib, self._h
         p64 = ctypes.POINTER(ctypes.c_uint64)
-        pu32 = ctypes.POINTER(ctypes.c_uint32)
-        slot_buf = np.zeros(self.TAKE, dtype=np.uint32)
-        nonce_buf = np.zeros(self.TAKE, dtype=np.uint64)
-        trial_buf = np.zeros(self.TAKE, dtype=np.uint64)
-        done_buf = np.zeros(self.TAKE, dtype=np.uint8)
+        tick = np.zeros(self.TAKE, dtype=np.uint64)
+        nonce = np.zeros(self.TAKE, dtype=np.uint64)
+        trial = np.zeros(self.TAKE, dtype=np.uint64)
+        done = np.zeros(self.TAKE, dtype=np.uint8)
         try:
-            lib = _lib.get()
-        except Exception as e:  # noqa: BLE001 -- no device: every submitter sees why
-            lib, lib_err = None, e
-        h = None
-        live = {}  # slot -> _Entry
-
-        def drop(exc):
-            nonlocal h
-            self._fail(list(live.values()), exc)
-            live.clear()
-            if h is not None:
-                lib.bmpow_batch_destroy(h)
-                h = None
-
-        try:
-            while True:
-                with self._cv:
-                    while not self._incoming and not live and not self._stopping:
-                        self._cv.wait(0.5)
-                    if self._stopping:
-                        self._fail(self._incoming, RuntimeError('PowService stopped'))
-                        self._incoming = []
-                        drop(RuntimeError('PowService stopped'))
-                        return
-                    # at most ADD_PER_STEP join per step: a flood starts on the device while the rest
-                    # of it is still being appended, one step behind
-                    new, self._incoming = self._incoming[:self.ADD_PER_STEP], self._incoming[self.ADD_PER_STEP:]
-                if lib is None:
-                    self._fail(new, lib_err)
+            while not self._stopping:
+                if h is None:
+                    time.sleep(self.POLL_MS / 1000.0)
                     continue
-                if state.shutdown != 0:
-                    self._fail(new, StopIteration('Interrupted'))
-                    drop(StopIteration('Interrupted'))
+                if state.shutdown != 0 and self._live:
+                    with self._lock:
+                        self._drop_live(StopIteration('Interrupted'))
                     continue
-                try:
-                    if new:
-                        if h is None:
-                            h = lib.bmpow_batch_create(0, None, None, None)
-                            if not h:
-                                raise _lib.BmpowError(_lib.E_HIP, 'bmpow_batch_create: %s'
-                                                      % lib.bmpow_last_error().decode())
-                        tg = np.array([e.target for e in new], dtype=np.uint64)
-                        slots = np.zeros(len(new), dtype=np.uint32)
-                        _lib.check(lib, lib.bmpow_batch_add(h, len(new), b''.join(e.ih for e in new),
-                                                            tg.ctypes.data_as(p64), None, slots.ctypes.data_as(pu32)),
-                                   'bmpow_batch_add')
-                        for e, sl in zip(new, slots.tolist()):
-                            live[sl] = e
-                        new = []
-                    _lib.check(lib, lib.bmpow_batch_step(h, self.step_trials), 'bmpow_batch_step')
-                    self.calls += 1
-                    while True:
-                        k = _lib.check(lib, lib.bmpow_batch_take_done(
-                            h, self.TAKE, slot_buf.ctypes.data_as(pu32), nonce_buf.ctypes.data_as(p64),
-                            trial_buf.ctypes.data_as(p64), done_buf.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
-                            'bmpow_batch_take_done')
-                        if k:
-                            done_q.put([(live.pop(sl), d, tv, nn) for sl, d, tv, nn in
-                                        zip(slot_buf[:k].tolist(), done_buf[:k].tolist(), trial_buf[:k].tolist(),
-                                            nonce_buf[:k].tolist())])
-                        if k < self.TAKE:
-                            break
-                except Exception as e:  # noqa: BLE001
-                    self._fail(new, e)
-                    drop(e)
+                k = lib.bmpow_service_poll(h, self.TAKE, self.POLL_MS, tick.ctypes.data_as(p64),
+                                           nonce.ctypes.data_as(p64), trial.ctypes.data_as(p64),
+                                           done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
+                if k < 0:
+                    err = _lib.BmpowError(k, 'bmpow service step: %s' % lib.bmpow_last_error().decode())
+                    with self._lock:
+                        self._drop_live(err)
+                    continue
+                if not k:
+                    continue
+                with self._lock:
+                    batch = [self._live.pop(t, None) for t in tick[:k].tolist()]
+                for e, d, tv, nn in zip(batch, done[:k].tolist(), trial[:k].tolist(), nonce[:k].tolist()):
+                    if e is None:  # dropped by a cancel that raced this poll
+                        continue
+                    if d == _lib.DONE_FOUND:
+                        try:
+                            proofofwork._verify(e.target, e.ih, tv, nn)
+                        except Exception as err:  # noqa: BLE001
+                            e.future.set_exception(err)
+                            continue
+                        self.solved += 1
+                        e.future.set_result([tv, nn])
+                    else:
+                        e.future.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
+                _notify([e for e in batch if e is not None])
         finally:
-            if h is not None and lib is not None:
-                lib.bmpow_batch_destroy(h)
-            done_q.put(None)  # the completion thread drains what is queued, then exits
+            with self._lock:
+                dead = list(self._live.values())
+                self._live.clear()
+                if h is not None:
+                    lib.bmpow_service_destroy(h)
+                self._h = None
+            self._fail(dead, RuntimeError('PowService stopped'))

@@ -404,3 +404,82 @@ def test_session_add_and_take_done(gpulib, coracle):
     assert len(got) == serial
     for (t, ih), res in got.values():
         assert res == coracle.search(ih, t)
+
+
+def test_native_service_producers_cancel_abort(gpulib, coracle):
+    """bmpow_service_*: the library's stepping thread.  Four producers submit concurrently while
+    one consumer polls; tickets are unique and every answer exact.  A cancel drops everything in
+    flight and the service keeps going; an abort surfaces as the poll's error, and a cancel
+    recovers from it."""
+    gpulib.bmpow_set_step_trials(1 << 22)
+    s = gpulib.bmpow_service_create(0)
+    assert s
+    cap = 512
+    tk, nn = np.zeros(cap, dtype=np.uint64), np.zeros(cap, dtype=np.uint64)
+    tv, dn = np.zeros(cap, dtype=np.uint64), np.zeros(cap, dtype=np.uint8)
+    pu8 = ctypes.POINTER(ctypes.c_uint8)
+
+    def poll(timeout_ms=2000):
+        k = gpulib.bmpow_service_poll(s, cap, timeout_ms, tk.ctypes.data_as(P64), nn.ctypes.data_as(P64),
+                                      tv.ctypes.data_as(P64), dn.ctypes.data_as(pu8))
+        if k < 0:
+            return k
+        return [(int(tk[j]), int(tv[j]), int(nn[j]), int(dn[j])) for j in range(k)]
+
+    def submit(objs):
+        tg = np.array([t for t, _ in objs], dtype=np.uint64)
+        out = np.zeros(len(objs), dtype=np.uint64)
+        assert gpulib.bmpow_service_submit(s, len(objs), b''.join(ih for _, ih in objs), tg.ctypes.data_as(P64),
+                                           out.ctypes.data_as(P64)) == 0
+        return out.tolist()
+    try:
+        jobs, lock = {}, threading.Lock()
+
+        def producer(seed):
+            rng = random.Random(seed)
+            for _ in range(10):
+                objs = [(U64 // rng.choice([3, 500, 20000, 300000]), rng.randbytes(64))
+                        for _ in range(rng.randrange(1, 60))]
+                with lock:  # the ticket map must hold a ticket before a poll can return it
+                    for t, o in zip(submit(objs), objs):
+                        assert t not in jobs
+                        jobs[t] = o
+                time.sleep(rng.random() * 0.02)
+        ths = [threading.Thread(target=producer, args=(k,)) for k in range(4)]
+        for t in ths:
+            t.start()
+        got = {}
+        deadline = time.time() + 120
+        while (any(t.is_alive() for t in ths) or len(got) < len(jobs)) and time.time() < deadline:
+            r = poll(200)
+            assert not isinstance(r, int), r
+            for t, trial, nonce, d in r:
+                assert d == _lib.DONE_FOUND and t not in got
+                got[t] = (trial, nonce)
+        for t in ths:
+            t.join()
+        assert len(got) == len(jobs) and gpulib.bmpow_service_outstanding(s) == 0
+        for t, (target, ih) in jobs.items():
+            assert got[t] == coracle.search(ih, target)
+        # cancel drops in-flight work (a target-0 object never finishes) and the service goes on
+        submit([(0, bytes(64))] * 3)
+        time.sleep(0.2)
+        assert gpulib.bmpow_service_cancel(s) == 0 and gpulib.bmpow_service_outstanding(s) == 0
+        ih = hashlib.sha512(b'after-cancel').digest()
+        (t1,) = submit([(U64 // 1000, ih)])
+        r = poll(10000)
+        assert [(t, tr, n) for t, tr, n, _ in r] == [(t1,) + coracle.search(ih, U64 // 1000)]
+        # abort: the step fails, the poll reports it, a cancel clears it
+        submit([(0, bytes(64))])
+        time.sleep(0.1)
+        gpulib.bmpow_abort()
+        assert poll(10000) == _lib.E_ABORTED
+        gpulib.bmpow_clear_abort()
+        gpulib.bmpow_service_cancel(s)
+        (t2,) = submit([(U64 // 1000, ih)])
+        r = poll(10000)
+        assert [(t, tr, n) for t, tr, n, _ in r] == [(t2,) + coracle.search(ih, U64 // 1000)]
+    finally:
+        gpulib.bmpow_clear_abort()
+        gpulib.bmpow_service_destroy(s)
+        gpulib.bmpow_set_step_trials(1 << 28)

@@ -43,7 +43,8 @@ def oracle_batch(monkeypatch, coracle):
 class BatchLib(object):
     """Test double of the resident-session ABI (bmpow_batch_create/add/step/take_done/destroy,
     include/bmpow.h): each step advances every pending object by WINDOW nonces, searched with the
-    C oracle; finished slots are queued for take_done and freed for reuse, as the library does."""
+    C oracle; finished slots are queued for take_done and freed for reuse, as the library does.
+    The bmpow_service_* calls run the library's stepping thread over those sessions."""
     WINDOW = 3000
 
     def __init__(self, coracle):
@@ -52,6 +53,8 @@ class BatchLib(object):
         self.sizes = []
         self.sessions = {}
         self.next_handle = 1
+        self.services = []
+        self.fail_step = False
 
     def bmpow_batch_create(self, n, ihs, tg, start):
         h = self.next_handle
@@ -113,8 +116,97 @@ class BatchLib(object):
     def bmpow_batch_destroy(self, h):
         del self.sessions[h]
 
+    # bmpow_service_*: the library's stepping thread, emulated over the session double above
+    def bmpow_service_create(self, budget):
+        svc = {'h': self.bmpow_batch_create(0, None, None, None), 'cv': threading.Condition(), 'in': [],
+               'out': [], 'ticket': 0, 'stop': False, 'cancel': False, 'error': 0, 'live': {}}
+        svc['th'] = threading.Thread(target=self._service_loop, args=(svc,), daemon=True)
+        svc['th'].start()
+        self.services.append(svc)
+        return len(self.services)
+
+    def _service_loop(self, svc):
+        slots = (ctypes.c_uint32 * 64)()
+        nonce, trial, done = (ctypes.c_uint64 * 64)(), (ctypes.c_uint64 * 64)(), (ctypes.c_uint8 * 64)()
+        while True:
+            with svc['cv']:
+                svc['cv'].wait_for(lambda: svc['stop'] or svc['cancel'] or svc['in'] or
+                                   (svc['live'] and not svc['error']))
+                if svc['stop']:
+                    return
+                if svc['cancel']:
+                    self.bmpow_batch_destroy(svc['h'])
+                    svc['h'] = self.bmpow_batch_create(0, None, None, None)
+                    svc['live'], svc['cancel'] = {}, False
+                new, svc['in'] = svc['in'], []
+            h = svc['h']
+            if new:
+                tg = (ctypes.c_uint64 * len(new))(*[t for _, _, t in new])
+                sl = (ctypes.c_uint32 * len(new))()
+                self.bmpow_batch_add(h, len(new), b''.join(ih for _, ih, _ in new), tg, None, sl)
+                for (tk, _, _), k in zip(new, sl):
+                    svc['live'][k] = tk
+            fin, rc = [], 0
+            if self.fail_step:
+                rc = -3
+            else:
+                self.bmpow_batch_step(h, 0)
+                while True:
+                    k = self.bmpow_batch_take_done(h, 64, slots, nonce, trial, done)
+                    fin += [(svc['live'].pop(slots[j]), nonce[j], trial[j], done[j]) for j in range(k)]
+                    if k < 64:
+                        break
+            with svc['cv']:
+                if not svc['cancel']:
+                    svc['out'] += fin
+                    svc['error'] = rc
+                svc['cv'].notify_all()
+
+    def bmpow_service_submit(self, sh, n, ihs, tg, tickets_out):
+        svc = self.services[sh - 1]
+        tg = np.ctypeslib.as_array(ctypes.cast(tg, ctypes.POINTER(ctypes.c_uint64)), shape=(n,))
+        tk = np.ctypeslib.as_array(ctypes.cast(tickets_out, ctypes.POINTER(ctypes.c_uint64)), shape=(n,))
+        with svc['cv']:
+            for i in range(n):
+                tk[i] = svc['ticket']
+                svc['in'].append((svc['ticket'], ihs[64 * i:64 * i + 64], int(tg[i])))
+                svc['ticket'] += 1
+            svc['cv'].notify_all()
+        return 0
+
+    def bmpow_service_poll(self, sh, cap, timeout_ms, tickets, nonce_out, trial_out, done_out):
+        svc = self.services[sh - 1]
+        view = lambda p, t: np.ctypeslib.as_array(ctypes.cast(p, ctypes.POINTER(t)), shape=(cap,))  # noqa: E731
+        tk, nonce = view(tickets, ctypes.c_uint64), view(nonce_out, ctypes.c_uint64)
+        trial, done = view(trial_out, ctypes.c_uint64), view(done_out, ctypes.c_uint8)
+        with svc['cv']:
+            if not svc['cv'].wait_for(lambda: svc['out'] or svc['error'] or svc['stop'], timeout_ms / 1000.0):
+                return 0
+            if not svc['out'] and svc['error']:
+                return svc['error']
+            k = min(cap, len(svc['out']))
+            for j in range(k):
+                tk[j], nonce[j], trial[j], done[j] = svc['out'][j]
+            del svc['out'][:k]
+            return k
+
+    def bmpow_service_cancel(self, sh):
+        svc = self.services[sh - 1]
+        with svc['cv']:
+            svc['cancel'], svc['error'], svc['in'], svc['out'] = True, 0, [], []
+            svc['cv'].notify_all()
+        return 0
+
+    def bmpow_service_destroy(self, sh):
+        svc = self.services[sh - 1]
+        with svc['cv']:
+            svc['stop'] = True
+            svc['cv'].notify_all()
+        svc['th'].join()
+        self.bmpow_batch_destroy(svc['h'])
+
     def bmpow_last_error(self):
-        return b''
+        return b'injected step failure' if self.fail_step else b''
 
 
 @pytest.fixture
@@ -259,7 +351,7 @@ def test_powservice_submit_many(batchlib, coracle):
         svc.stop(5)
 
 
-def test_powservice_shutdown_and_errors(batchlib):
+def test_powservice_shutdown_and_errors(batchlib, coracle):
     svc = worker.PowService().start()
     try:
         fut = svc.submit(0, bytes(64))  # target 0: never found
@@ -270,11 +362,22 @@ def test_powservice_shutdown_and_errors(batchlib):
         state.shutdown = 0
         with pytest.raises(ValueError):
             svc.submit(-1, bytes(64)).result(1)
+        # a failing step fails what is live with the library's error; the service then recovers
+        batchlib.fail_step = True
+        with pytest.raises(_lib.BmpowError, match='injected'):
+            svc.submit(U64 // 10, bytes(64)).result(10)
+        batchlib.fail_step = False
+        ih = bytes(range(64))
+        assert svc.submit(U64 // 10, ih).result(10) == list(coracle.search(ih, U64 // 10))
+        pending = svc.submit(0, bytes(64))
     finally:
         state.shutdown = 0
         svc.stop(5)
+    with pytest.raises(RuntimeError, match='stopped'):
+        pending.result(1)
     with pytest.raises(RuntimeError):
         svc.submit(1, bytes(64))
+    assert not batchlib.sessions  # the service's session was destroyed
 
 
 def test_logoutput_captures_native_stdout(caplog):
