@@ -126,18 +126,16 @@ class PowInterrupted(Exception):
 
 def iter_batch(objects, step_trials=0):
     """Solve many ``(target, initialHash)`` objects at once on the GPU, yielding
-    ``(index, trialValue, nonce)`` as each finishes (ascending index within a step).
+    ``(index, trialValue, nonce)`` as each finishes.
 
-    The object table stays in HBM (``bmpow_batch_create``); each ``bmpow_batch_step`` is one
-    bounded launch per device over the pending objects, so large objects are nonce-sharded and
-    small ones packed many per launch.  A stepping thread drives the device and pops the finished
-    objects (``bmpow_batch_take_done``: O(finished) per step); this generator re-checks each with
-    hashlib and yields it meanwhile, so the per-object host work overlaps the next step's kernels
-    (the stepping thread holds no GIL inside the library).  ``state.shutdown`` is polled between
-    steps and raises :class:`PowInterrupted`."""
-    import queue
-    import threading
-
+    The objects go to the library's continuous-batching service (``bmpow_service_create`` /
+    ``bmpow_service_submit``): its native thread keeps the object table in HBM and steps it --
+    each step one bounded launch per device over the pending objects, large objects nonce-sharded
+    and small ones packed many per launch -- without ever waiting on this interpreter's GIL.  This
+    generator pops the finished objects (``bmpow_service_poll``, GIL released while it waits),
+    re-checks each with hashlib and yields it while the next step runs.  ``state.shutdown`` is
+    polled at least every 100 ms and raises :class:`PowInterrupted`; closing the generator stops
+    the service after its current step."""
     import numpy as np
     lib = _lib.get()
     objs = list(objects)
@@ -154,60 +152,35 @@ def iter_batch(objects, step_trials=0):
         targets[i] = t
     ihs = bytes(ihs)
     p64 = ctypes.POINTER(ctypes.c_uint64)
-    h = lib.bmpow_batch_create(n, ihs, targets.ctypes.data_as(p64), None)
-    if not h:
-        raise BmpowError(_lib.E_HIP, 'bmpow_batch_create: %s' % lib.bmpow_last_error().decode())
-    out = queue.Queue()
-    stop = threading.Event()
-    cap = min(n, 65536)
-
-    def stepper():
-        slots = np.zeros(cap, dtype=np.uint32)
+    s = lib.bmpow_service_create(step_trials)
+    if not s:
+        raise BmpowError(_lib.E_HIP, 'bmpow_service_create: %s' % lib.bmpow_last_error().decode())
+    try:
+        cap = min(n, 65536)
+        tick = np.zeros(max(n, cap), dtype=np.uint64)
+        _lib.check(lib, lib.bmpow_service_submit(s, n, ihs, targets.ctypes.data_as(p64), tick.ctypes.data_as(p64)),
+                   'bmpow_service_submit')
+        base = int(tick[0])  # tickets are consecutive from the first
         nonce = np.zeros(cap, dtype=np.uint64)
         trial = np.zeros(cap, dtype=np.uint64)
         done = np.zeros(cap, dtype=np.uint8)
-        try:
-            pending = n
-            while pending > 0 and not stop.is_set():
-                if _interrupted():
-                    out.put(('interrupted',))
-                    return
-                pending = _lib.check(lib, lib.bmpow_batch_step(h, step_trials), 'bmpow_batch_step')
-                while True:
-                    k = _lib.check(lib, lib.bmpow_batch_take_done(
-                        h, cap, slots.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), nonce.ctypes.data_as(p64),
-                        trial.ctypes.data_as(p64), done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
-                        'bmpow_batch_take_done')
-                    if k:
-                        out.put(('done', slots[:k].tolist(), trial[:k].tolist(), nonce[:k].tolist(), done[:k].tolist()))
-                    if k < cap:
-                        break
-            out.put(('end',))
-        except Exception as e:  # noqa: BLE001 -- re-raised by the generator
-            out.put(('error', e))
-
-    th = threading.Thread(target=stepper, name='bmpow-iter_batch')
-    th.daemon = True
-    th.start()
-    try:
-        while True:
-            msg = out.get()
-            if msg[0] == 'end':
-                return
-            if msg[0] == 'interrupted':
+        remaining = n
+        while remaining:
+            if _interrupted():
                 raise PowInterrupted('Interrupted')
-            if msg[0] == 'error':
-                raise msg[1]
-            _, idx, tvs, nonces, dones = msg
-            for i, tv, nn, d in zip(idx, tvs, nonces, dones):
+            k = _lib.check(lib, lib.bmpow_service_poll(s, cap, 100, tick.ctypes.data_as(p64), nonce.ctypes.data_as(p64),
+                                                       trial.ctypes.data_as(p64),
+                                                       done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8))),
+                           'bmpow_service_poll')
+            for t, tv, nn, d in zip(tick[:k].tolist(), trial[:k].tolist(), nonce[:k].tolist(), done[:k].tolist()):
+                i = t - base
                 if d != _lib.DONE_FOUND:
                     raise BmpowError(_lib.E_ARG, 'object %d: nonce space exhausted' % i)
                 _verify(int(targets[i]), ihs[64 * i:64 * i + 64], tv, nn)
                 yield i, tv, nn
+            remaining -= k
     finally:
-        stop.set()
-        th.join()
-        lib.bmpow_batch_destroy(h)
+        lib.bmpow_service_destroy(s)
 
 
 def run_batch(objects, step_trials=0):
