@@ -20,8 +20,6 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
-#include <condition_variable>
-#include <deque>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -941,108 +939,46 @@ int addr_search_locked(uint32_t mode, const uint8_t* seed, size_t len, const uin
 }  // namespace
 
 // ---------------------------------------------------------------------------------------
-// Continuous-batching service (bmpow_service_*).  A library thread owns a resident session and steps
-// it while producers submit and a consumer polls finished objects, so no caller thread -- and no
-// Python GIL -- sits between two steps: the device goes from one step to the next as soon as the
-// previous one's results are folded in.  Lock order: the service's own mutex and the library's g_mu
-// are never held together.
+// Continuous-batching service (bmpow_service_*): bmsched::Service's stepper thread over a resident
+// session, so no caller thread -- and no Python GIL -- sits between two steps.  Its ops take g_mu
+// one at a time; the service's own mutex is never held with it.
 // ---------------------------------------------------------------------------------------
 struct bmpow_service {
-  bmpow_batch* b = nullptr;  // resident session (stepper thread, under g_mu)
+  bmpow_batch* b = nullptr;  // resident session (ops run on the stepper thread, under g_mu)
   uint64_t budget = 0;       // trials per step (0 = library default)
-  std::thread th;
-  std::mutex mu;             // guards everything below
-  std::condition_variable cv_in, cv_out;
-  std::vector<uint8_t> in_ih;  // submitted, not yet in the session (64 B each)
-  std::vector<uint64_t> in_target, in_ticket;
-  struct Done {
-    uint64_t ticket, nonce, trial;
-    uint8_t done;
-  };
-  std::deque<Done> out;        // finished, not yet polled
-  uint64_t next_ticket = 0;
-  size_t outstanding = 0;      // submitted and not yet polled
-  bool stopping = false, cancel = false;
-  int error = 0;
-  std::string err;
-  std::vector<uint64_t> slot_ticket;  // stepper thread only
+  std::unique_ptr<bmsched::Service> svc;
 };
 
 namespace {
 
-void service_loop(bmpow_service* s) {
-  std::vector<uint8_t> ih;
-  std::vector<uint64_t> tg, tk;
-  std::vector<uint32_t> slots;
-  constexpr size_t kTake = 4096;
-  std::vector<uint32_t> fs(kTake);
-  std::vector<uint64_t> fn(kTake), ft(kTake);
-  std::vector<uint8_t> fd(kTake);
-  size_t live = 0;
-  for (;;) {
-    bool cancel = false;
-    {
-      std::unique_lock<std::mutex> lk(s->mu);
-      s->cv_in.wait(lk, [&] { return s->stopping || s->cancel || !s->in_ticket.empty() || (live > 0 && !s->error); });
-      if (s->stopping) return;
-      cancel = s->cancel;
-      s->cancel = false;
-      ih.swap(s->in_ih);
-      tg.swap(s->in_target);
-      tk.swap(s->in_ticket);
-    }
-    std::vector<bmpow_service::Done> fin;
-    int rc = 0;
-    std::string msg;
-    {
-      std::lock_guard<std::mutex> g(g_mu);
-      if (cancel) {  // drop every object of the session: a fresh, empty one
-        batch_free_dev(s->b);
-        delete s->b;
-        s->b = new bmpow_batch();
-        rc = batch_init(s->b, 0, nullptr, nullptr, nullptr);
-        s->slot_ticket.clear();
-        live = 0;
-      }
-      if (rc == 0 && !tk.empty()) {
-        slots.resize(tk.size());
-        rc = batch_add_locked(s->b, tk.size(), ih.data(), tg.data(), nullptr, slots.data());
-        if (rc == 0) {
-          for (size_t i = 0; i < tk.size(); ++i) {
-            if (s->slot_ticket.size() <= slots[i]) s->slot_ticket.resize(slots[i] + 1);
-            s->slot_ticket[slots[i]] = tk[i];
-          }
-          live += tk.size();
-        }
-      }
-      if (rc == 0 && live) rc = batch_step_locked(s->b, s->budget, nullptr);
-      if (rc >= 0) {
-        rc = 0;
-        for (;;) {
-          const size_t k = bmsched::take_done(*s->b, kTake, fs.data(), fn.data(), ft.data(), fd.data());
-          for (size_t j = 0; j < k; ++j) fin.push_back({s->slot_ticket[fs[j]], fn[j], ft[j], fd[j]});
-          live -= k;
-          if (k < kTake) break;
-        }
-      } else {
-        msg = g_err;  // this thread's error text
-      }
-    }
-    {
-      std::lock_guard<std::mutex> lk(s->mu);
-      if (!s->cancel) {  // a cancel since the step started drops its results too
-        for (const auto& d : fin) s->out.push_back(d);
-        if (rc < 0) {
-          s->error = rc;
-          s->err = msg;
-        }
-      }
-    }
-    s->cv_out.notify_all();
-    ih.clear();
-    tg.clear();
-    tk.clear();
-  }
+bmsched::ServiceOps service_ops(bmpow_service* s) {
+  bmsched::ServiceOps ops;
+  ops.add = [s](size_t n, const uint8_t* ihs, const uint64_t* tg, uint32_t* slots, std::string& err) {
+    std::lock_guard<std::mutex> g(g_mu);
+    const int rc = batch_add_locked(s->b, n, ihs, tg, nullptr, slots);
+    if (rc < 0) err = g_err;
+    return rc;
+  };
+  ops.step = [s](std::string& err) {
+    std::lock_guard<std::mutex> g(g_mu);
+    const int rc = batch_step_locked(s->b, s->budget, nullptr);
+    if (rc < 0) err = g_err;
+    return rc;
+  };
+  ops.take = [s](size_t cap, uint32_t* slot, uint64_t* nonce, uint64_t* trial, uint8_t* done) {
+    std::lock_guard<std::mutex> g(g_mu);
+    return bmsched::take_done(*s->b, cap, slot, nonce, trial, done);
+  };
+  ops.reset = [s](std::string& err) {
+    std::lock_guard<std::mutex> g(g_mu);
+    batch_free_dev(s->b);
+    delete s->b;
+    s->b = new bmpow_batch();
+    const int rc = batch_init(s->b, 0, nullptr, nullptr, nullptr);
+    if (rc < 0) err = g_err;
+    return rc;
+  };
+  return ops;
 }
 
 }  // namespace
@@ -1323,101 +1259,54 @@ void bmpow_batch_destroy(bmpow_batch* b) {
 }
 
 bmpow_service* bmpow_service_create(uint64_t step_budget) {
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (init_locked() < 0) return nullptr;
   bmpow_service* s = new bmpow_service();
-  s->b = new bmpow_batch();
-  if (batch_init(s->b, 0, nullptr, nullptr, nullptr) < 0) {
-    batch_free_dev(s->b);
-    delete s->b;
-    delete s;
-    return nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    s->b = new bmpow_batch();
+    if (init_locked() < 0 || batch_init(s->b, 0, nullptr, nullptr, nullptr) < 0) {
+      batch_free_dev(s->b);
+      delete s->b;
+      delete s;
+      return nullptr;
+    }
+    s->budget = step_budget;
   }
-  s->budget = step_budget;
-  s->th = std::thread(service_loop, s);
+  s->svc.reset(new bmsched::Service(service_ops(s)));
   return s;
 }
 
 int bmpow_service_submit(bmpow_service* s, size_t n, const uint8_t* ihs, const uint64_t* targets,
                          uint64_t* tickets_out) {
   if (!s) return set_err(BMPOW_E_STATE, "null service");
-  if (n == 0) return 0;
-  if (!ihs || !targets) return set_err(BMPOW_E_ARG, "null pointer");
-  {
-    std::lock_guard<std::mutex> lk(s->mu);
-    if (s->stopping) return set_err(BMPOW_E_STATE, "service stopping");
-    s->in_ih.insert(s->in_ih.end(), ihs, ihs + 64 * n);
-    s->in_target.insert(s->in_target.end(), targets, targets + n);
-    for (size_t i = 0; i < n; ++i) {
-      const uint64_t t = s->next_ticket++;
-      s->in_ticket.push_back(t);
-      if (tickets_out) tickets_out[i] = t;
-    }
-    s->outstanding += n;
-  }
-  s->cv_in.notify_all();
-  return 0;
+  if (n && (!ihs || !targets)) return set_err(BMPOW_E_ARG, "null pointer");
+  const int rc = s->svc->submit(n, ihs, targets, tickets_out);
+  return rc < 0 ? set_err(rc, "service stopping") : rc;
 }
 
 int bmpow_service_poll(bmpow_service* s, size_t cap, int timeout_ms, uint64_t* tickets, uint64_t* nonce_out,
                        uint64_t* trial_out, uint8_t* done_out) {
   if (!s) return set_err(BMPOW_E_STATE, "null service");
   if (cap && !tickets) return set_err(BMPOW_E_ARG, "null pointer");
-  std::unique_lock<std::mutex> lk(s->mu);
-  auto ready = [&] { return !s->out.empty() || s->error || s->stopping; };
-  if (timeout_ms < 0) s->cv_out.wait(lk, ready);
-  else if (!s->cv_out.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready)) return 0;
-  if (s->out.empty() && s->error) {
-    g_err = s->err;
-    return s->error;
-  }
-  size_t k = 0;
-  cap = std::min<size_t>(cap, 0x7fffffff);
-  while (k < cap && !s->out.empty()) {
-    const bmpow_service::Done& d = s->out.front();
-    tickets[k] = d.ticket;
-    if (nonce_out) nonce_out[k] = d.nonce;
-    if (trial_out) trial_out[k] = d.trial;
-    if (done_out) done_out[k] = d.done;
-    s->out.pop_front();
-    ++k;
-  }
-  s->outstanding -= k;
-  return (int)k;
+  std::string err;
+  const int rc = s->svc->poll(cap, timeout_ms, tickets, nonce_out, trial_out, done_out, err);
+  if (rc < 0) g_err = err;
+  return rc;
 }
 
 int bmpow_service_cancel(bmpow_service* s) {
   if (!s) return set_err(BMPOW_E_STATE, "null service");
-  {
-    std::lock_guard<std::mutex> lk(s->mu);
-    s->cancel = true;
-    s->error = 0;
-    s->err.clear();
-    s->in_ih.clear();
-    s->in_target.clear();
-    s->in_ticket.clear();
-    s->out.clear();
-    s->outstanding = 0;
-  }
-  s->cv_in.notify_all();
+  s->svc->cancel();
   return 0;
 }
 
 int bmpow_service_outstanding(bmpow_service* s) {
   if (!s) return set_err(BMPOW_E_STATE, "null service");
-  std::lock_guard<std::mutex> lk(s->mu);
-  return (int)std::min<size_t>(s->outstanding, 0x7fffffff);
+  return (int)std::min<size_t>(s->svc->outstanding(), 0x7fffffff);
 }
 
 void bmpow_service_destroy(bmpow_service* s) {
   if (!s) return;
-  {
-    std::lock_guard<std::mutex> lk(s->mu);
-    s->stopping = true;
-  }
-  s->cv_in.notify_all();
-  s->cv_out.notify_all();
-  if (s->th.joinable()) s->th.join();
+  s->svc.reset();  // joins the stepper thread after its current step
   std::lock_guard<std::mutex> lk(g_mu);
   batch_free_dev(s->b);
   delete s->b;

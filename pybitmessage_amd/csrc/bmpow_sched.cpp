@@ -3,6 +3,7 @@
 #include "bmpow_sched.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <thread>
 
@@ -410,6 +411,152 @@ int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, in
   const double t = 18446744073709551616.0 / y;
   if (t >= 18446744073709551616.0) return 1;
   return pow <= (uint64_t)t ? 1 : 0;
+}
+
+// ---------------------------------------------------------------------------------------
+// Service
+// ---------------------------------------------------------------------------------------
+Service::Service(ServiceOps ops) : ops_(std::move(ops)) { th_ = std::thread(&Service::loop, this); }
+
+Service::~Service() { stop(); }
+
+void Service::stop() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    stopping_ = true;
+  }
+  cv_in_.notify_all();
+  cv_out_.notify_all();
+  if (th_.joinable()) th_.join();
+}
+
+int Service::submit(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* tickets_out) {
+  if (n == 0) return 0;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (stopping_) return BMPOW_E_STATE;
+    in_ih_.insert(in_ih_.end(), ihs, ihs + 64 * n);
+    in_target_.insert(in_target_.end(), targets, targets + n);
+    for (size_t i = 0; i < n; ++i) {
+      const uint64_t t = next_ticket_++;
+      in_ticket_.push_back(t);
+      if (tickets_out) tickets_out[i] = t;
+    }
+    outstanding_ += n;
+  }
+  cv_in_.notify_all();
+  return 0;
+}
+
+int Service::poll(size_t cap, int timeout_ms, uint64_t* tickets, uint64_t* nonce, uint64_t* trial, uint8_t* done,
+                  std::string& err) {
+  std::unique_lock<std::mutex> lk(mu_);
+  auto ready = [&] { return !out_.empty() || error_ || stopping_; };
+  // (a plain wait is used for < 0: GCC 11's ThreadSanitizer mis-reports timed waits)
+  if (timeout_ms < 0) cv_out_.wait(lk, ready);
+  else if (!cv_out_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready)) return 0;
+  if (out_.empty() && error_) {
+    err = err_;
+    return error_;
+  }
+  size_t k = 0;
+  cap = std::min<size_t>(cap, 0x7fffffff);
+  for (; k < cap && !out_.empty(); ++k) {
+    const Done& d = out_.front();
+    tickets[k] = d.ticket;
+    if (nonce) nonce[k] = d.nonce;
+    if (trial) trial[k] = d.trial;
+    if (done) done[k] = d.done;
+    out_.pop_front();
+  }
+  outstanding_ -= k;
+  return (int)k;
+}
+
+void Service::cancel() {
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    cancel_ = true;
+    error_ = 0;
+    err_.clear();
+    in_ih_.clear();
+    in_target_.clear();
+    in_ticket_.clear();
+    out_.clear();
+    outstanding_ = 0;
+  }
+  cv_in_.notify_all();
+}
+
+size_t Service::outstanding() {
+  std::lock_guard<std::mutex> lk(mu_);
+  return outstanding_;
+}
+
+void Service::loop() {
+  std::vector<uint8_t> ih;
+  std::vector<uint64_t> tg, tk, slot_ticket;
+  std::vector<uint32_t> slots;
+  constexpr size_t kTake = 4096;
+  std::vector<uint32_t> fs(kTake);
+  std::vector<uint64_t> fn(kTake), ft(kTake);
+  std::vector<uint8_t> fd(kTake);
+  std::vector<Done> fin;
+  size_t live = 0;  // objects in the session
+  for (;;) {
+    bool cancel = false;
+    {
+      std::unique_lock<std::mutex> lk(mu_);
+      cv_in_.wait(lk, [&] { return stopping_ || cancel_ || (!error_ && (live > 0 || !in_ticket_.empty())); });
+      if (stopping_) return;
+      cancel = cancel_;
+      cancel_ = false;
+      ih.swap(in_ih_);
+      tg.swap(in_target_);
+      tk.swap(in_ticket_);
+    }
+    fin.clear();
+    std::string err;
+    int rc = 0;
+    if (cancel) {
+      rc = ops_.reset(err);
+      live = 0;
+    }
+    if (rc >= 0 && !tk.empty()) {
+      slots.resize(tk.size());
+      rc = ops_.add(tk.size(), ih.data(), tg.data(), slots.data(), err);
+      if (rc >= 0) {
+        for (size_t i = 0; i < tk.size(); ++i) {
+          if (slot_ticket.size() <= slots[i]) slot_ticket.resize((size_t)slots[i] + 1);
+          slot_ticket[slots[i]] = tk[i];
+        }
+        live += tk.size();
+      }
+    }
+    if (rc >= 0 && live) rc = ops_.step(err);
+    if (rc >= 0) {
+      for (;;) {
+        const size_t k = ops_.take(kTake, fs.data(), fn.data(), ft.data(), fd.data());
+        for (size_t j = 0; j < k; ++j) fin.push_back({slot_ticket[fs[j]], fn[j], ft[j], fd[j]});
+        live -= k;
+        if (k < kTake) break;
+      }
+    }
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      if (!cancel_) {  // a cancel since this step started drops its results too
+        out_.insert(out_.end(), fin.begin(), fin.end());
+        if (rc < 0) {
+          error_ = rc;
+          err_ = err;
+        }
+      }
+    }
+    cv_out_.notify_all();
+    ih.clear();
+    tg.clear();
+    tk.clear();
+  }
 }
 
 }  // namespace bmsched

@@ -7,6 +7,7 @@
 //   sessions       init / add / take_done / reset / set_pending          (bmpow_batch_*)
 //   min-trial      MinTrial::plan -> (launch) -> reduce_parts -> advance (bmpow_min_trial*)
 //   verification   plan_verify, pad_range, pow_sufficient                (bmpow_verify*, bmpow_pow_values)
+//   service        Service: stepper thread, submit / poll / cancel         (bmpow_service_*)
 //
 // Semantics reproduced: the reference's _doSafePoW first nonce (src/proofofwork.py:100-111) over
 // contiguous windows per object, and protocol.isProofOfWorkSufficient (src/protocol.py:258-286).
@@ -14,7 +15,12 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <condition_variable>
+#include <deque>
 #include <functional>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/bmpow.h"
@@ -134,5 +140,54 @@ void parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_
 // protocol.isProofOfWorkSufficient's comparison (src/protocol.py:272-286) in the reference's
 // arithmetic.  1 sufficient, 0 not.
 int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, int64_t recv, uint64_t eol);
+
+// ---- continuous-batching service (bmpow_service_*) ----
+// The service's threading, independent of the device: one stepper thread folds what producers
+// submitted into the session (ops.add), steps it (ops.step) and queues the finished objects
+// (ops.take) for poll().  The ops run on the stepper thread only and never under the service's
+// mutex, so a caller of submit/poll/cancel waits at most for a queue operation, never for a step.
+struct ServiceOps {
+  // append n objects (64-byte hashes, targets; searches start at nonce 1); slots[i] = object i's slot
+  std::function<int(size_t n, const uint8_t* ihs, const uint64_t* targets, uint32_t* slots, std::string& err)> add;
+  std::function<int(std::string& err)> step;  // one step over the pending objects
+  std::function<size_t(size_t cap, uint32_t* slot, uint64_t* nonce, uint64_t* trial, uint8_t* done)> take;
+  std::function<int(std::string& err)> reset;  // drop every object of the session
+};
+
+class Service {
+ public:
+  struct Done {
+    uint64_t ticket, nonce, trial;
+    uint8_t done;
+  };
+  explicit Service(ServiceOps ops);
+  ~Service();  // stop()
+  // Queue n objects; tickets_out[i] (may be null) = object i's ticket, ascending over the service's
+  // life.  BMPOW_E_STATE once stopping.
+  int submit(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* tickets_out);
+  // Pop up to cap finished objects, waiting up to timeout_ms (< 0: forever) for the first.  Returns
+  // the count, 0 on timeout, or the error a step hit (err = its text) once everything before it was
+  // popped; nothing is stepped after an error until cancel().
+  int poll(size_t cap, int timeout_ms, uint64_t* tickets, uint64_t* nonce, uint64_t* trial, uint8_t* done,
+           std::string& err);
+  void cancel();  // drop queued, live and unpolled objects and a pending error
+  size_t outstanding();  // submitted and not yet popped
+  void stop();  // after the current step; idempotent
+
+ private:
+  void loop();
+  ServiceOps ops_;
+  std::mutex mu_;  // guards every member below
+  std::condition_variable cv_in_, cv_out_;
+  std::vector<uint8_t> in_ih_;
+  std::vector<uint64_t> in_target_, in_ticket_;
+  std::deque<Done> out_;
+  uint64_t next_ticket_ = 0;
+  size_t outstanding_ = 0;
+  bool stopping_ = false, cancel_ = false;
+  int error_ = 0;
+  std::string err_;
+  std::thread th_;
+};
 
 }  // namespace bmsched

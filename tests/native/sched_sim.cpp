@@ -389,12 +389,139 @@ static void scenario_verify() {
   }
 }
 
+// ---- scenario 6: the library's continuous-batching service (bmpow_service_*) over the stand-in ----
+static void scenario_service() {
+  std::mutex gmu;  // the library's g_mu: every op takes it
+  BatchState b;
+  init(b, 0, nullptr, nullptr, nullptr);
+  std::vector<SimShard> shards(2);
+  std::atomic<int> fail_step{0};
+  ServiceOps ops;
+  ops.add = [&](size_t n, const uint8_t* ihs, const uint64_t* tg, uint32_t* slots, std::string&) {
+    std::lock_guard<std::mutex> lk(gmu);
+    std::vector<uint32_t> sl;
+    add(b, n, ihs, tg, nullptr, sl);
+    b.cap = std::max(b.cap, b.n);
+    for (SimShard& sh : shards)
+      for (uint32_t x : sl)
+        if (x < sh.best.size()) {
+          sh.best[x] = kU64Max;
+          sh.found[x] = 0;
+        }
+    std::copy(sl.begin(), sl.end(), slots);
+    return 0;
+  };
+  ops.step = [&](std::string& err) {
+    std::lock_guard<std::mutex> lk(gmu);
+    if (fail_step.load()) {
+      err = "injected step failure";
+      return (int)BMPOW_E_HIP;
+    }
+    sim_step(b, shards, 1 << 13, 1 << 16);
+    return 0;
+  };
+  ops.take = [&](size_t cap, uint32_t* slot, uint64_t* nonce, uint64_t* trial, uint8_t* done) {
+    std::lock_guard<std::mutex> lk(gmu);
+    return take_done(b, cap, slot, nonce, trial, done);
+  };
+  ops.reset = [&](std::string&) {
+    std::lock_guard<std::mutex> lk(gmu);
+    b = BatchState();
+    init(b, 0, nullptr, nullptr, nullptr);
+    shards.assign(2, SimShard());
+    return 0;
+  };
+  Service svc(ops);
+  auto submit_objs = [&](const std::vector<Obj>& objs, std::vector<uint64_t>& tk) {
+    std::vector<uint8_t> ihs(64 * objs.size());
+    std::vector<uint64_t> tg(objs.size());
+    for (size_t i = 0; i < objs.size(); ++i) {
+      memcpy(&ihs[64 * i], objs[i].ih, 64);
+      tg[i] = objs[i].target;
+    }
+    tk.resize(objs.size());
+    return svc.submit(objs.size(), ihs.data(), tg.data(), tk.data());
+  };
+  uint64_t tk[64], nn[64], tv[64];
+  uint8_t dn[64];
+  std::string err;
+
+  // producers and one consumer: tickets unique, every answer exact
+  std::mutex tmu;
+  std::vector<std::pair<uint64_t, Obj>> sent;
+  size_t total = 0;
+  for (int id = 0; id < 4; ++id)
+    for (int burst = 0; burst < 20; ++burst) total += 1 + (id * 7 + burst * 13) % 40;
+  std::vector<std::array<uint64_t, 4>> got;  // ticket, done, nonce, trial
+  std::thread consumer([&] {
+    while (got.size() < total) {
+      const int k = svc.poll(64, -1, tk, nn, tv, dn, err);
+      CHECK(k > 0, "poll returned %d (%s)", k, err.c_str());
+      if (k <= 0) return;
+      for (int j = 0; j < k; ++j) got.push_back({tk[j], dn[j], nn[j], tv[j]});
+    }
+  });
+  std::vector<std::thread> prod;
+  for (int id = 0; id < 4; ++id)
+    prod.emplace_back([&, id] {
+      std::mt19937_64 rng(300 + id);
+      for (int burst = 0; burst < 20; ++burst) {
+        std::vector<Obj> objs = random_objs(rng, 1 + (id * 7 + burst * 13) % 40, 4000);
+        std::vector<uint64_t> t;
+        std::lock_guard<std::mutex> lk(tmu);  // tickets recorded before a poll can return them
+        CHECK(submit_objs(objs, t) == 0, "submit failed");
+        for (size_t i = 0; i < objs.size(); ++i) sent.emplace_back(t[i], objs[i]);
+      }
+    });
+  for (auto& t : prod) t.join();
+  consumer.join();
+  std::sort(sent.begin(), sent.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+  std::sort(got.begin(), got.end());
+  CHECK(sent.size() == total && got.size() == total, "sent %zu got %zu of %zu", sent.size(), got.size(), total);
+  for (size_t i = 0; i < std::min(sent.size(), got.size()); ++i) {
+    CHECK(sent[i].first == i && got[i][0] == i, "ticket %zu: sent %llu got %llu", i,
+          (unsigned long long)sent[i].first, (unsigned long long)got[i][0]);
+    expect_exact(sent[i].second, (int)got[i][1], got[i][2], got[i][3], "service", i);
+  }
+  CHECK(svc.outstanding() == 0, "outstanding %zu after draining", svc.outstanding());
+
+  // cancel drops in-flight objects that never finish; the service goes on
+  std::mt19937_64 rng(77);
+  std::vector<Obj> never = random_objs(rng, 3, 1), easy = random_objs(rng, 1, 100);
+  for (Obj& o : never) o.target = 0;
+  std::vector<uint64_t> t;
+  submit_objs(never, t);
+  std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  svc.cancel();
+  CHECK(svc.outstanding() == 0, "outstanding after cancel");
+  submit_objs(easy, t);
+  int k = svc.poll(64, -1, tk, nn, tv, dn, err);
+  CHECK(k == 1 && tk[0] == t[0], "after cancel: k=%d", k);
+  if (k == 1) expect_exact(easy[0], dn[0], nn[0], tv[0], "after cancel", 0);
+
+  // a failing step surfaces as the poll's error; nothing steps until cancel; then it recovers
+  submit_objs(never, t);
+  fail_step = 1;
+  k = svc.poll(64, -1, tk, nn, tv, dn, err);
+  CHECK(k == BMPOW_E_HIP && err == "injected step failure", "error poll: k=%d err=%s", k, err.c_str());
+  fail_step = 0;
+  svc.cancel();
+  submit_objs(easy, t);
+  k = svc.poll(64, -1, tk, nn, tv, dn, err);
+  CHECK(k == 1 && tk[0] == t[0], "after error: k=%d", k);
+  if (k == 1) expect_exact(easy[0], dn[0], nn[0], tv[0], "after error", 0);
+  svc.stop();
+  CHECK(submit_objs(easy, t) == BMPOW_E_STATE, "submit after stop");
+  fprintf(stderr, "service: %zu objects from 4 producers, cancel and error recovery\n", total);
+}
+
 int main() {
   scenario_batches();
   scenario_top_of_space();
   scenario_session();
   scenario_min_trial();
   scenario_verify();
+  scenario_service();
   if (g_fail) {
     fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;
