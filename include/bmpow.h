@@ -51,6 +51,7 @@ extern "C" {
 #define BMPOW_DONE_EXHAUSTED 2 /* reached nonce 2^64-1 without a hit */
 #define BMPOW_PARKED 3         /* in the table but not scheduled (bmpow_batch_set_pending) */
 #define BMPOW_FREE 4           /* released slot (bmpow_batch_take_done), reused by bmpow_batch_add */
+#define BMPOW_DONE_BADHASH 5   /* service with BMPOW_SERVICE_VERIFY: the device's answer failed the host re-check */
 
 /* ---- lifecycle (replaces proofofwork.init / bmpow global, src/proofofwork.py:336-394) ---- */
 
@@ -164,8 +165,13 @@ BMPOW_API void bmpow_batch_destroy(bmpow_batch *b);
  *      the worker and API threads, src/class_singleWorker.py:236,1276, src/api.py:1304,1350) ---- */
 typedef struct bmpow_service bmpow_service;
 
-/* Start the service thread.  step_budget: trials per step (0 = library default).  NULL on error. */
-BMPOW_API bmpow_service *bmpow_service_create(uint64_t step_budget);
+/* Start the service thread.  step_budget: trials per step (0 = library default).  flags:
+ * BMPOW_SERVICE_VERIFY re-hashes every found nonce on the host (OpenSSL SHA-512) inside
+ * bmpow_service_poll, on the polling thread, and reports a mismatch or a trial above the target as
+ * BMPOW_DONE_BADHASH -- the check _doGPUPoW makes with hashlib (src/proofofwork.py:176-190).
+ * NULL on error. */
+#define BMPOW_SERVICE_VERIFY 1u
+BMPOW_API bmpow_service *bmpow_service_create(uint64_t step_budget, uint32_t flags);
 
 /* Queue n objects (ihs: n x 64 bytes, targets: n; every search starts at nonce 1); they join the
  * session at the next step.  tickets_out[i] (may be NULL) = object i's ticket (ascending over the

@@ -25,6 +25,8 @@ DONE_FOUND = 1
 DONE_EXHAUSTED = 2
 PARKED = 3
 FREE = 4
+DONE_BADHASH = 5
+SERVICE_VERIFY = 1
 
 U64_MAX = (1 << 64) - 1
 
@@ -88,7 +90,7 @@ SIGNATURES = [
     ('bmpow_batch_add', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _pu32]),
     ('bmpow_batch_take_done', ctypes.c_int, [_vp, ctypes.c_size_t, _pu32, _p64, _p64, _pu8]),
     ('bmpow_batch_destroy', None, [_vp]),
-    ('bmpow_service_create', _vp, [_u64]),
+    ('bmpow_service_create', _vp, [_u64, ctypes.c_uint32]),
     ('bmpow_service_submit', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_char_p, _p64, _p64]),
     ('bmpow_service_poll', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_int, _p64, _p64, _p64, _pu8]),
     ('bmpow_service_cancel', ctypes.c_int, [_vp]),

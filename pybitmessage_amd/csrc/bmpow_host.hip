@@ -1258,7 +1258,7 @@ void bmpow_batch_destroy(bmpow_batch* b) {
   delete b;
 }
 
-bmpow_service* bmpow_service_create(uint64_t step_budget) {
+bmpow_service* bmpow_service_create(uint64_t step_budget, uint32_t flags) {
   bmpow_service* s = new bmpow_service();
   {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -1271,7 +1271,7 @@ bmpow_service* bmpow_service_create(uint64_t step_budget) {
     }
     s->budget = step_budget;
   }
-  s->svc.reset(new bmsched::Service(service_ops(s)));
+  s->svc.reset(new bmsched::Service(service_ops(s), (flags & BMPOW_SERVICE_VERIFY) != 0));
   return s;
 }
 

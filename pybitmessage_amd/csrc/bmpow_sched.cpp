@@ -2,6 +2,8 @@
 // compiled into the library by hipcc and, for tests/native/, by g++ under the sanitizers.
 #include "bmpow_sched.h"
 
+#include <openssl/sha.h>
+
 #include <algorithm>
 #include <chrono>
 #include <cstring>
@@ -13,6 +15,15 @@ uint64_t load_be64(const uint8_t* p) {
   uint64_t v = 0;
   for (int j = 0; j < 8; ++j) v = (v << 8) | p[j];
   return v;
+}
+
+uint64_t host_trial(const uint8_t ih[64], uint64_t nonce) {
+  uint8_t msg[72], h1[64], h2[64];
+  for (int i = 0; i < 8; ++i) msg[i] = (uint8_t)(nonce >> (56 - 8 * i));
+  memcpy(msg + 8, ih, 64);
+  SHA512(msg, sizeof msg, h1);
+  SHA512(h1, sizeof h1, h2);
+  return load_be64(h2);
 }
 
 void pack_obj(const uint8_t* ih, uint64_t target, bm_obj* o) {
@@ -416,7 +427,9 @@ int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, in
 // ---------------------------------------------------------------------------------------
 // Service
 // ---------------------------------------------------------------------------------------
-Service::Service(ServiceOps ops) : ops_(std::move(ops)) { th_ = std::thread(&Service::loop, this); }
+Service::Service(ServiceOps ops, bool verify) : ops_(std::move(ops)), verify_(verify) {
+  th_ = std::thread(&Service::loop, this);
+}
 
 Service::~Service() { stop(); }
 
@@ -452,6 +465,7 @@ int Service::poll(size_t cap, int timeout_ms, uint64_t* tickets, uint64_t* nonce
                   std::string& err) {
   std::unique_lock<std::mutex> lk(mu_);
   auto ready = [&] { return !out_.empty() || error_ || stopping_; };
+  thread_local std::vector<Out> popped;
   // (a plain wait is used for < 0: GCC 11's ThreadSanitizer mis-reports timed waits)
   if (timeout_ms < 0) cv_out_.wait(lk, ready);
   else if (!cv_out_.wait_for(lk, std::chrono::milliseconds(timeout_ms), ready)) return 0;
@@ -459,17 +473,23 @@ int Service::poll(size_t cap, int timeout_ms, uint64_t* tickets, uint64_t* nonce
     err = err_;
     return error_;
   }
-  size_t k = 0;
   cap = std::min<size_t>(cap, 0x7fffffff);
-  for (; k < cap && !out_.empty(); ++k) {
-    const Done& d = out_.front();
-    tickets[k] = d.ticket;
-    if (nonce) nonce[k] = d.nonce;
-    if (trial) trial[k] = d.trial;
-    if (done) done[k] = d.done;
-    out_.pop_front();
-  }
+  const size_t k = std::min(cap, out_.size());
+  popped.assign(out_.begin(), out_.begin() + (ptrdiff_t)k);
+  out_.erase(out_.begin(), out_.begin() + (ptrdiff_t)k);
   outstanding_ -= k;
+  lk.unlock();
+  // the host re-check runs on the polling thread, outside the lock, while the next step runs
+  for (size_t j = 0; j < k; ++j) {
+    Done d = popped[j].d;
+    if (verify_ && d.done == BMPOW_DONE_FOUND &&
+        (host_trial(popped[j].ih, d.nonce) != d.trial || d.trial > popped[j].target))
+      d.done = BMPOW_DONE_BADHASH;
+    tickets[j] = d.ticket;
+    if (nonce) nonce[j] = d.nonce;
+    if (trial) trial[j] = d.trial;
+    if (done) done[j] = d.done;
+  }
   return (int)k;
 }
 
@@ -495,13 +515,14 @@ size_t Service::outstanding() {
 
 void Service::loop() {
   std::vector<uint8_t> ih;
-  std::vector<uint64_t> tg, tk, slot_ticket;
+  std::vector<uint64_t> tg, tk, slot_ticket, slot_target;
+  std::vector<uint8_t> slot_ih;  // 64 B per slot: the object's initialHash, for the re-check
   std::vector<uint32_t> slots;
   constexpr size_t kTake = 4096;
   std::vector<uint32_t> fs(kTake);
   std::vector<uint64_t> fn(kTake), ft(kTake);
   std::vector<uint8_t> fd(kTake);
-  std::vector<Done> fin;
+  std::vector<Out> fin;
   size_t live = 0;  // objects in the session
   for (;;) {
     bool cancel = false;
@@ -527,8 +548,14 @@ void Service::loop() {
       rc = ops_.add(tk.size(), ih.data(), tg.data(), slots.data(), err);
       if (rc >= 0) {
         for (size_t i = 0; i < tk.size(); ++i) {
-          if (slot_ticket.size() <= slots[i]) slot_ticket.resize((size_t)slots[i] + 1);
+          if (slot_ticket.size() <= slots[i]) {
+            slot_ticket.resize((size_t)slots[i] + 1);
+            slot_target.resize((size_t)slots[i] + 1);
+            slot_ih.resize(64 * ((size_t)slots[i] + 1));
+          }
           slot_ticket[slots[i]] = tk[i];
+          slot_target[slots[i]] = tg[i];
+          memcpy(&slot_ih[64 * (size_t)slots[i]], &ih[64 * i], 64);
         }
         live += tk.size();
       }
@@ -537,7 +564,13 @@ void Service::loop() {
     if (rc >= 0) {
       for (;;) {
         const size_t k = ops_.take(kTake, fs.data(), fn.data(), ft.data(), fd.data());
-        for (size_t j = 0; j < k; ++j) fin.push_back({slot_ticket[fs[j]], fn[j], ft[j], fd[j]});
+        for (size_t j = 0; j < k; ++j) {
+          Out o;
+          o.d = {slot_ticket[fs[j]], fn[j], ft[j], fd[j]};
+          o.target = slot_target[fs[j]];
+          memcpy(o.ih, &slot_ih[64 * (size_t)fs[j]], 64);
+          fin.push_back(o);
+        }
         live -= k;
         if (k < kTake) break;
       }

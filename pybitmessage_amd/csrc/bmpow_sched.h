@@ -31,6 +31,8 @@ namespace bmsched {
 constexpr uint64_t kU64Max = ~0ULL;
 
 uint64_t load_be64(const uint8_t* p);
+// trial(nonce, ih) on the host (OpenSSL SHA-512): the re-check of device answers, never a search
+uint64_t host_trial(const uint8_t ih[64], uint64_t nonce);
 void pack_obj(const uint8_t* ih, uint64_t target, bm_obj* o);
 
 // Host mirror of a device-resident batch (one slot per object; slots of finished objects are
@@ -160,7 +162,9 @@ class Service {
     uint64_t ticket, nonce, trial;
     uint8_t done;
   };
-  explicit Service(ServiceOps ops);
+  // verify: poll() re-hashes every found nonce on the host (host_trial) and reports a wrong trial or
+  // one above the target as BMPOW_DONE_BADHASH
+  explicit Service(ServiceOps ops, bool verify = false);
   ~Service();  // stop()
   // Queue n objects; tickets_out[i] (may be null) = object i's ticket, ascending over the service's
   // life.  BMPOW_E_STATE once stopping.
@@ -176,12 +180,18 @@ class Service {
 
  private:
   void loop();
+  struct Out {
+    Done d;
+    uint64_t target;
+    uint8_t ih[64];
+  };
   ServiceOps ops_;
+  const bool verify_;
   std::mutex mu_;  // guards every member below
   std::condition_variable cv_in_, cv_out_;
   std::vector<uint8_t> in_ih_;
   std::vector<uint64_t> in_target_, in_ticket_;
-  std::deque<Done> out_;
+  std::deque<Out> out_;
   uint64_t next_ticket_ = 0;
   size_t outstanding_ = 0;
   bool stopping_ = false, cancel_ = false;

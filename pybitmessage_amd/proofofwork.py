@@ -38,7 +38,8 @@ U64_MAX = _lib.U64_MAX
 #: trials per bounded ``bmpow_search`` call from ``run``: a few steps of the scheduler
 #: (~0.1-0.3 s on one MI355X), i.e. the shutdown-poll interval of the Python loop.
 CALL_TRIALS = 1 << 30
-#: re-check every returned nonce with hashlib, as ``_doGPUPoW`` does (``:176-190``)
+#: re-check every returned nonce on the host, as ``_doGPUPoW`` does with hashlib (``:176-190``):
+#: hashlib here for ``run``; the library's OpenSSL SHA-512 (``BMPOW_SERVICE_VERIFY``) for batches
 VERIFY = True
 
 
@@ -132,8 +133,9 @@ def iter_batch(objects, step_trials=0):
     ``bmpow_service_submit``): its native thread keeps the object table in HBM and steps it --
     each step one bounded launch per device over the pending objects, large objects nonce-sharded
     and small ones packed many per launch -- without ever waiting on this interpreter's GIL.  This
-    generator pops the finished objects (``bmpow_service_poll``, GIL released while it waits),
-    re-checks each with hashlib and yields it while the next step runs.  ``state.shutdown`` is
+    generator pops the finished objects (``bmpow_service_poll``, GIL released while it waits; the
+    library re-hashes each found nonce on the host there, ``BMPOW_SERVICE_VERIFY``) and yields
+    them while the next step runs.  ``state.shutdown`` is
     polled at least every 100 ms and raises :class:`PowInterrupted`; closing the generator stops
     the service after its current step."""
     import numpy as np
@@ -152,7 +154,7 @@ def iter_batch(objects, step_trials=0):
         targets[i] = t
     ihs = bytes(ihs)
     p64 = ctypes.POINTER(ctypes.c_uint64)
-    s = lib.bmpow_service_create(step_trials)
+    s = lib.bmpow_service_create(step_trials, _lib.SERVICE_VERIFY if VERIFY else 0)
     if not s:
         raise BmpowError(_lib.E_HIP, 'bmpow_service_create: %s' % lib.bmpow_last_error().decode())
     try:
@@ -174,9 +176,10 @@ def iter_batch(objects, step_trials=0):
                            'bmpow_service_poll')
             for t, tv, nn, d in zip(tick[:k].tolist(), trial[:k].tolist(), nonce[:k].tolist(), done[:k].tolist()):
                 i = t - base
+                if d == _lib.DONE_BADHASH:
+                    raise BmpowError(_lib.E_HIP, 'object %d: GPU answer (nonce %d) failed the host re-check' % (i, nn))
                 if d != _lib.DONE_FOUND:
                     raise BmpowError(_lib.E_ARG, 'object %d: nonce space exhausted' % i)
-                _verify(int(targets[i]), ihs[64 * i:64 * i + 64], tv, nn)
                 yield i, tv, nn
             remaining -= k
     finally:

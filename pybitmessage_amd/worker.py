@@ -33,6 +33,7 @@ from . import state
 from . import targets
 
 logger = logging.getLogger('default')
+_P64 = ctypes.POINTER(ctypes.c_uint64)
 
 #: ``protocol.Header`` (``protocol.py:63``) and the network magic (``:298``)
 _HEADER = struct.Struct('!L12sL4s')
@@ -364,7 +365,7 @@ class BatchResult(object):
         self._wait(timeout)
         return self._exc
 
-    # completion side (the service's completion thread; waiters are woken by _notify)
+    # completion side (the service's completion thread; waiters are woken by _Sub.notify)
     def set_result(self, value):
         self._value = value
         self._done = True
@@ -374,20 +375,22 @@ class BatchResult(object):
         self._done = True
 
 
-def _notify(entries):
-    groups = {id(e.future._group): e.future._group for e in entries if type(e.future) is BatchResult}
-    for g in groups.values():
-        with g.cv:
-            g.cv.notify_all()
+class _Sub(object):
+    """The objects of one ``bmpow_service_submit`` call: tickets ``base .. base + n - 1``."""
+    __slots__ = ('base', 'ihs', 'targets', 'futs', 'group', 'left')
 
+    def __init__(self, ihs, targets, futs, group):
+        self.base = 0
+        self.ihs = ihs  # n x 64 bytes
+        self.targets = targets  # n clamped targets
+        self.futs = futs
+        self.group = group  # the shared _Group of BatchResults, or None for Futures
+        self.left = len(futs)
 
-class _Entry(object):
-    __slots__ = ('ih', 'target', 'future')
-
-    def __init__(self, ih, target, future):
-        self.ih = ih
-        self.target = target
-        self.future = future
+    def notify(self):
+        if self.group is not None:
+            with self.group.cv:
+                self.group.cv.notify_all()
 
 
 class PowService(object):
@@ -401,7 +404,8 @@ class PowService(object):
     each bounded step over every pending object and queues the finished ones -- the per-step host
     work is O(new + finished) and no Python thread (so no GIL) sits between two steps.  This
     object's completion thread pops finished objects (``bmpow_service_poll``, GIL released while
-    it waits), re-checks each nonce with hashlib as ``_doGPUPoW`` does and resolves its future,
+    it waits; the library re-hashes each found nonce on the host inside that call, the check
+    ``_doGPUPoW`` makes with hashlib) and resolves the futures,
     overlapping the Python work with the device's next step.  An object submitted mid-flight joins
     the next step (~40 ms on one MI355X) instead of waiting for the objects ahead of it, and
     producers never contend for the device.  Replaces concurrent blocking ``run`` calls from the
@@ -409,11 +413,14 @@ class PowService(object):
 
     TAKE = 4096  # finished objects popped per bmpow_service_poll call
     POLL_MS = 100  # longest wait in one poll: bounds the reaction time to state.shutdown / stop()
+    SUBMIT_SLICE = 8192  # submit_many hands the library this many objects at a time, so the device
+    #                      starts on the first slice while Python prepares the next
 
     def __init__(self, step_trials=0):
         self.step_trials = step_trials
-        self._lock = threading.Lock()  # guards _live and the service handle
-        self._live = {}  # ticket -> _Entry
+        self._lock = threading.Lock()  # guards _subs / _bases and the service handle
+        self._subs = []  # live _Sub records in ticket order
+        self._bases = []  # their first tickets (bisect)
         self._lib = None
         self._lib_err = None
         self._h = None
@@ -428,7 +435,8 @@ class PowService(object):
                 self._lib_err = None
                 try:
                     self._lib = _lib.get()
-                    h = self._lib.bmpow_service_create(self.step_trials)
+                    h = self._lib.bmpow_service_create(self.step_trials,
+                                                       _lib.SERVICE_VERIFY if proofofwork.VERIFY else 0)
                     if not h:
                         raise _lib.BmpowError(_lib.E_HIP, 'bmpow_service_create: %s'
                                               % self._lib.bmpow_last_error().decode())
@@ -454,50 +462,55 @@ class PowService(object):
         if not ok:
             fut.set_exception(ValueError('negative target: no nonce can satisfy it'))
             return fut
-        self._enqueue([_Entry(proofofwork._ih_bytes(initialHash), t, fut)])
+        self._enqueue(_Sub(proofofwork._ih_bytes(initialHash), [t], [fut], None))
         return fut
 
     def submit_many(self, objects):
-        """``[submit(t, ih) for t, ih in objects]`` in one library call: a producer with many
+        """``[submit(t, ih) for t, ih in objects]`` in a few library calls: a producer with many
         objects at once (a flood of acks, every pending pubkey) joins the next step together.
         Returns one :class:`BatchResult` per object (``result()`` gives ``[trialValue, nonce]``)."""
-        futs, entries = [], []
         group = _Group()
-        for target, initialHash in objects:
-            fut = BatchResult(group)
-            futs.append(fut)
-            t, ok = proofofwork._clamp_target(target)
-            if not ok:
-                fut.set_exception(ValueError('negative target: no nonce can satisfy it'))
-                continue
-            entries.append(_Entry(proofofwork._ih_bytes(initialHash), t, fut))
-        self._enqueue(entries)
-        return futs
+        out = []
+        clamp, ihb = proofofwork._clamp_target, proofofwork._ih_bytes
+        objects = list(objects)
+        for lo in range(0, len(objects), self.SUBMIT_SLICE):
+            futs, ihs, tgs = [], [], []
+            for target, initialHash in objects[lo:lo + self.SUBMIT_SLICE]:
+                fut = BatchResult(group)
+                out.append(fut)
+                t, ok = clamp(target)
+                if not ok:
+                    fut.set_exception(ValueError('negative target: no nonce can satisfy it'))
+                    continue
+                futs.append(fut)
+                ihs.append(ihb(initialHash))
+                tgs.append(t)
+            if futs:
+                self._enqueue(_Sub(b''.join(ihs), tgs, futs, group))
+        return out
 
-    def _enqueue(self, entries):
-        import numpy as np
+    def _enqueue(self, sub):
+        import array
         with self._lock:
             if self._stopping or self._completer is None:
                 raise RuntimeError('PowService is not running')
-            if not entries:
-                return
             if self._h is None:
-                self._fail(entries, self._lib_err)
+                self._fail([sub], self._lib_err)
                 return
             if state.shutdown != 0:
-                self._fail(entries, StopIteration('Interrupted'))
+                self._fail([sub], StopIteration('Interrupted'))
                 return
-            p64 = ctypes.POINTER(ctypes.c_uint64)
-            n = len(entries)
-            tg = np.fromiter((e.target for e in entries), dtype=np.uint64, count=n)
-            tickets = np.empty(n, dtype=np.uint64)
-            rc = self._lib.bmpow_service_submit(self._h, n, b''.join(e.ih for e in entries),
-                                                tg.ctypes.data_as(p64), tickets.ctypes.data_as(p64))
+            n = len(sub.futs)
+            tg = array.array('Q', sub.targets)
+            tk = (ctypes.c_uint64 * n)()
+            rc = self._lib.bmpow_service_submit(self._h, n, sub.ihs, ctypes.cast(tg.buffer_info()[0], _P64), tk)
             if rc < 0:
-                self._fail(entries, _lib.BmpowError(rc, 'bmpow_service_submit: %s'
-                                                    % self._lib.bmpow_last_error().decode()))
+                self._fail([sub], _lib.BmpowError(rc, 'bmpow_service_submit: %s'
+                                                  % self._lib.bmpow_last_error().decode()))
                 return
-            self._live.update(zip(tickets.tolist(), entries))
+            sub.base = tk[0]  # tickets are consecutive within one call
+            self._subs.append(sub)
+            self._bases.append(sub.base)
 
     def run(self, target, initialHash):
         """Blocking ``proofofwork.run`` through the shared batch."""
@@ -506,25 +519,27 @@ class PowService(object):
         return self.submit(target, initialHash).result()
 
     @staticmethod
-    def _fail(entries, exc):
-        for e in entries:
-            if not e.future.done():
-                e.future.set_exception(exc)
-        _notify(entries)
+    def _fail(subs, exc):
+        for sub in subs:
+            for f in sub.futs:
+                if not f.done():
+                    f.set_exception(exc)
+            sub.notify()
 
     def _drop_live(self, exc):
         """Cancel everything in the library and fail its futures (caller holds the lock)."""
-        dead = list(self._live.values())
-        self._live.clear()
+        dead = self._subs
+        self._subs, self._bases = [], []
         self._lib.bmpow_service_cancel(self._h)
         self._fail(dead, exc)
 
     def _complete(self):
-        """Completion thread: pop finished objects, re-check each found nonce with hashlib and
-        resolve its future; cancels on state.shutdown; destroys the library service on stop()."""
+        """Completion thread: pop finished objects (each found nonce re-checked on the host by the
+        library) and resolve their futures; cancels on state.shutdown; destroys the library service on stop()."""
+        import bisect
+
         import numpy as np
         lib, h = self._lib, self._h
-        p64 = ctypes.POINTER(ctypes.c_uint64)
         tick = np.zeros(self.TAKE, dtype=np.uint64)
         nonce = np.zeros(self.TAKE, dtype=np.uint64)
         trial = np.zeros(self.TAKE, dtype=np.uint64)
@@ -534,12 +549,12 @@ class PowService(object):
                 if h is None:
                     time.sleep(self.POLL_MS / 1000.0)
                     continue
-                if state.shutdown != 0 and self._live:
+                if state.shutdown != 0 and self._subs:
                     with self._lock:
                         self._drop_live(StopIteration('Interrupted'))
                     continue
-                k = lib.bmpow_service_poll(h, self.TAKE, self.POLL_MS, tick.ctypes.data_as(p64),
-                                           nonce.ctypes.data_as(p64), trial.ctypes.data_as(p64),
+                k = lib.bmpow_service_poll(h, self.TAKE, self.POLL_MS, tick.ctypes.data_as(_P64),
+                                           nonce.ctypes.data_as(_P64), trial.ctypes.data_as(_P64),
                                            done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
                 if k < 0:
                     err = _lib.BmpowError(k, 'bmpow service step: %s' % lib.bmpow_last_error().decode())
@@ -548,26 +563,43 @@ class PowService(object):
                     continue
                 if not k:
                     continue
+                work = []
                 with self._lock:
-                    batch = [self._live.pop(t, None) for t in tick[:k].tolist()]
-                for e, d, tv, nn in zip(batch, done[:k].tolist(), trial[:k].tolist(), nonce[:k].tolist()):
-                    if e is None:  # dropped by a cancel that raced this poll
-                        continue
-                    if d == _lib.DONE_FOUND:
-                        try:
-                            proofofwork._verify(e.target, e.ih, tv, nn)
-                        except Exception as err:  # noqa: BLE001
-                            e.future.set_exception(err)
+                    subs, bases = self._subs, self._bases
+                    for t, d, tv, nn in zip(tick[:k].tolist(), done[:k].tolist(), trial[:k].tolist(),
+                                            nonce[:k].tolist()):
+                        j = bisect.bisect_right(bases, t) - 1
+                        if j < 0:
+                            continue  # dropped by a cancel that raced this poll
+                        sub = subs[j]
+                        i = t - sub.base
+                        if i >= len(sub.futs):
                             continue
+                        sub.left -= 1
+                        work.append((sub, i, d, tv, nn))
+                    if any(s.left == 0 for s in subs):
+                        keep = [s for s in subs if s.left > 0]
+                        self._subs, self._bases = keep, [s.base for s in keep]
+                touched = {}
+                for sub, i, d, tv, nn in work:
+                    fut = sub.futs[i]
+                    if fut.done():
+                        continue
+                    if d == _lib.DONE_FOUND:  # re-checked on the host by the library (SERVICE_VERIFY)
                         self.solved += 1
-                        e.future.set_result([tv, nn])
+                        fut.set_result([tv, nn])
+                    elif d == _lib.DONE_BADHASH:
+                        fut.set_exception(_lib.BmpowError(_lib.E_HIP, 'GPU answer (nonce %d) failed the host re-check'
+                                                          % nn))
                     else:
-                        e.future.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
-                _notify([e for e in batch if e is not None])
+                        fut.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
+                    touched[id(sub)] = sub
+                for sub in touched.values():
+                    sub.notify()
         finally:
             with self._lock:
-                dead = list(self._live.values())
-                self._live.clear()
+                dead = self._subs
+                self._subs, self._bases = [], []
                 if h is not None:
                     lib.bmpow_service_destroy(h)
                 self._h = None

@@ -395,7 +395,7 @@ static void scenario_service() {
   BatchState b;
   init(b, 0, nullptr, nullptr, nullptr);
   std::vector<SimShard> shards(2);
-  std::atomic<int> fail_step{0};
+  std::atomic<int> fail_step{0}, corrupt{0};
   ServiceOps ops;
   ops.add = [&](size_t n, const uint8_t* ihs, const uint64_t* tg, uint32_t* slots, std::string&) {
     std::lock_guard<std::mutex> lk(gmu);
@@ -422,7 +422,9 @@ static void scenario_service() {
   };
   ops.take = [&](size_t cap, uint32_t* slot, uint64_t* nonce, uint64_t* trial, uint8_t* done) {
     std::lock_guard<std::mutex> lk(gmu);
-    return take_done(b, cap, slot, nonce, trial, done);
+    const size_t k = take_done(b, cap, slot, nonce, trial, done);
+    if (k && corrupt.exchange(0)) trial[0] ^= 1;  // a wrong device answer for the host re-check to catch
+    return k;
   };
   ops.reset = [&](std::string&) {
     std::lock_guard<std::mutex> lk(gmu);
@@ -431,7 +433,7 @@ static void scenario_service() {
     shards.assign(2, SimShard());
     return 0;
   };
-  Service svc(ops);
+  Service svc(ops, true);
   auto submit_objs = [&](const std::vector<Obj>& objs, std::vector<uint64_t>& tk) {
     std::vector<uint8_t> ihs(64 * objs.size());
     std::vector<uint64_t> tg(objs.size());
@@ -510,6 +512,12 @@ static void scenario_service() {
   k = svc.poll(64, -1, tk, nn, tv, dn, err);
   CHECK(k == 1 && tk[0] == t[0], "after error: k=%d", k);
   if (k == 1) expect_exact(easy[0], dn[0], nn[0], tv[0], "after error", 0);
+
+  // the host re-check reports a wrong trial as BMPOW_DONE_BADHASH
+  corrupt = 1;
+  submit_objs(easy, t);
+  k = svc.poll(64, -1, tk, nn, tv, dn, err);
+  CHECK(k == 1 && dn[0] == BMPOW_DONE_BADHASH, "corrupted answer: k=%d done=%d", k, k > 0 ? dn[0] : -1);
   svc.stop();
   CHECK(submit_objs(easy, t) == BMPOW_E_STATE, "submit after stop");
   fprintf(stderr, "service: %zu objects from 4 producers, cancel and error recovery\n", total);

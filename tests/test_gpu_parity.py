@@ -412,7 +412,7 @@ def test_native_service_producers_cancel_abort(gpulib, coracle):
     flight and the service keeps going; an abort surfaces as the poll's error, and a cancel
     recovers from it."""
     gpulib.bmpow_set_step_trials(1 << 22)
-    s = gpulib.bmpow_service_create(0)
+    s = gpulib.bmpow_service_create(0, _lib.SERVICE_VERIFY)
     assert s
     cap = 512
     tk, nn = np.zeros(cap, dtype=np.uint64), np.zeros(cap, dtype=np.uint64)

@@ -30,7 +30,7 @@ def build(flavour):
     exe = os.path.join(OUT, 'sched_sim_%s' % flavour)
     # the oracle's hashing (pure computation on thread-local data) is built without instrumentation
     subprocess.check_call(['gcc', '-O3', '-c', ORACLE_C, '-o', obj])
-    subprocess.check_call(['g++', '-std=c++17', '-O1', '-g', '-Wall', '-pthread'] + flags + SRC + [obj, '-o', exe])
+    subprocess.check_call(['g++', '-std=c++17', '-O1', '-g', '-Wall', '-pthread'] + flags + SRC + [obj, '-o', exe, '-lcrypto'])
     return exe
 
 

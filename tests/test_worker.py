@@ -55,6 +55,7 @@ class BatchLib(object):
         self.next_handle = 1
         self.services = []
         self.fail_step = False
+        self.bad_tickets = set()
 
     def bmpow_batch_create(self, n, ihs, tg, start):
         h = self.next_handle
@@ -117,7 +118,8 @@ class BatchLib(object):
         del self.sessions[h]
 
     # bmpow_service_*: the library's stepping thread, emulated over the session double above
-    def bmpow_service_create(self, budget):
+    def bmpow_service_create(self, budget, flags):
+        assert flags == _lib.SERVICE_VERIFY
         svc = {'h': self.bmpow_batch_create(0, None, None, None), 'cv': threading.Condition(), 'in': [],
                'out': [], 'ticket': 0, 'stop': False, 'cancel': False, 'error': 0, 'live': {}}
         svc['th'] = threading.Thread(target=self._service_loop, args=(svc,), daemon=True)
@@ -187,6 +189,8 @@ class BatchLib(object):
             k = min(cap, len(svc['out']))
             for j in range(k):
                 tk[j], nonce[j], trial[j], done[j] = svc['out'][j]
+                if int(tk[j]) in self.bad_tickets:  # the library's host re-check caught a wrong answer
+                    done[j] = _lib.DONE_BADHASH
             del svc['out'][:k]
             return k
 
@@ -334,6 +338,10 @@ def test_iter_batch_stepping_thread(batchlib, coracle):
         timer.join()
         state.shutdown = 0
     assert not batchlib.sessions
+    batchlib.bad_tickets = {1}  # a wrong device answer caught by the library's host re-check
+    with pytest.raises(_lib.BmpowError, match='object 1: .*re-check'):
+        proofofwork.run_batch(objs[:3])
+    assert not batchlib.sessions
 
 
 def test_powservice_submit_many(batchlib, coracle):
@@ -367,6 +375,9 @@ def test_powservice_shutdown_and_errors(batchlib, coracle):
         with pytest.raises(_lib.BmpowError, match='injected'):
             svc.submit(U64 // 10, bytes(64)).result(10)
         batchlib.fail_step = False
+        batchlib.bad_tickets = {2}  # the service's third ticket: a wrong device answer
+        with pytest.raises(_lib.BmpowError, match='re-check'):
+            svc.submit(U64 // 10, bytes(64)).result(10)
         ih = bytes(range(64))
         assert svc.submit(U64 // 10, ih).result(10) == list(coracle.search(ih, U64 // 10))
         pending = svc.submit(0, bytes(64))
