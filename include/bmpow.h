@@ -192,7 +192,11 @@ BMPOW_API int bmpow_service_cancel(bmpow_service *s);
 /* Objects submitted and not yet popped by bmpow_service_poll. */
 BMPOW_API int bmpow_service_outstanding(bmpow_service *s);
 
-/* Stop the thread (after its current step) and free the session. */
+/* Stop stepping (after the current step) and wake every bmpow_service_poll: they return what is
+ * already finished, then 0 at once.  Submits fail with BMPOW_E_STATE.  The handle stays valid. */
+BMPOW_API void bmpow_service_stop(bmpow_service *s);
+
+/* Stop (as above) and free the session; no other call on s may be in progress. */
 BMPOW_API void bmpow_service_destroy(bmpow_service *s);
 
 /* ---- receive-side verification (replaces protocol.isProofOfWorkSufficient,

@@ -95,6 +95,7 @@ SIGNATURES = [
     ('bmpow_service_poll', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_int, _p64, _p64, _p64, _pu8]),
     ('bmpow_service_cancel', ctypes.c_int, [_vp]),
     ('bmpow_service_outstanding', ctypes.c_int, [_vp]),
+    ('bmpow_service_stop', None, [_vp]),
     ('bmpow_service_destroy', None, [_vp]),
     ('bmpow_get_stats', ctypes.c_int, [ctypes.POINTER(BmpowStats)]),
     ('bmpow_reset_stats', None, []),

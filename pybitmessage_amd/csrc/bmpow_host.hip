@@ -1304,6 +1304,10 @@ int bmpow_service_outstanding(bmpow_service* s) {
   return (int)std::min<size_t>(s->svc->outstanding(), 0x7fffffff);
 }
 
+void bmpow_service_stop(bmpow_service* s) {
+  if (s) s->svc->stop();
+}
+
 void bmpow_service_destroy(bmpow_service* s) {
   if (!s) return;
   s->svc.reset();  // joins the stepper thread after its current step

@@ -440,6 +440,7 @@ void Service::stop() {
   }
   cv_in_.notify_all();
   cv_out_.notify_all();
+  std::lock_guard<std::mutex> j(join_mu_);  // stop() may race from two threads
   if (th_.joinable()) th_.join();
 }
 

@@ -176,7 +176,7 @@ class Service {
            std::string& err);
   void cancel();  // drop queued, live and unpolled objects and a pending error
   size_t outstanding();  // submitted and not yet popped
-  void stop();  // after the current step; idempotent
+  void stop();  // after the current step; idempotent, thread-safe
 
  private:
   void loop();
@@ -197,6 +197,7 @@ class Service {
   bool stopping_ = false, cancel_ = false;
   int error_ = 0;
   std::string err_;
+  std::mutex join_mu_;
   std::thread th_;
 };
 

@@ -427,6 +427,7 @@ class PowService(object):
         self._stopping = False
         self._completer = None
         self.solved = 0
+        self.trace = None  # a list to record (time.perf_counter(), objects popped) per poll
 
     def start(self):
         with self._lock:
@@ -452,6 +453,8 @@ class PowService(object):
         with self._lock:
             self._stopping = True
             th = self._completer
+            if self._h is not None:  # wakes the completion thread's poll at once
+                self._lib.bmpow_service_stop(self._h)
         if th is not None:
             th.join(timeout)
         self._completer = None
@@ -563,6 +566,8 @@ class PowService(object):
                     continue
                 if not k:
                     continue
+                if self.trace is not None:
+                    self.trace.append((time.perf_counter(), k))
                 work = []
                 with self._lock:
                     subs, bases = self._subs, self._bases

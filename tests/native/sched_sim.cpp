@@ -518,7 +518,17 @@ static void scenario_service() {
   submit_objs(easy, t);
   k = svc.poll(64, -1, tk, nn, tv, dn, err);
   CHECK(k == 1 && dn[0] == BMPOW_DONE_BADHASH, "corrupted answer: k=%d done=%d", k, k > 0 ? dn[0] : -1);
+  // stop() wakes a poll blocked on an idle service
+  std::thread waiter([&] {
+    uint64_t a[4], b2[4], c[4];
+    uint8_t d[4];
+    std::string e2;
+    const int r = svc.poll(4, -1, a, b2, c, d, e2);
+    CHECK(r == 0, "poll woken by stop returned %d", r);
+  });
+  std::this_thread::sleep_for(std::chrono::milliseconds(5));
   svc.stop();
+  waiter.join();
   CHECK(submit_objs(easy, t) == BMPOW_E_STATE, "submit after stop");
   fprintf(stderr, "service: %zu objects from 4 producers, cancel and error recovery\n", total);
 }

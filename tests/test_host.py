@@ -41,9 +41,9 @@ def test_header_declares_the_boundary():
               'bmpow_addr_set_comb', 'bmpow_addr_last_comb', 'bmpow_fe_probe', 'bmpow_min_trial',
               'bmpow_min_trial_batch', 'bmpow_batch_add', 'bmpow_batch_take_done', 'bmpow_service_create',
               'bmpow_service_submit', 'bmpow_service_poll', 'bmpow_service_cancel', 'bmpow_service_outstanding',
-              'bmpow_service_destroy']:
+              'bmpow_service_stop', 'bmpow_service_destroy']:
         assert s in syms
-    assert len(syms) == 46
+    assert len(syms) == 47
 
 
 def test_library_exports_every_declared_symbol(rawlib):

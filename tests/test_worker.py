@@ -201,13 +201,16 @@ class BatchLib(object):
             svc['cv'].notify_all()
         return 0
 
-    def bmpow_service_destroy(self, sh):
+    def bmpow_service_stop(self, sh):
         svc = self.services[sh - 1]
         with svc['cv']:
             svc['stop'] = True
             svc['cv'].notify_all()
         svc['th'].join()
-        self.bmpow_batch_destroy(svc['h'])
+
+    def bmpow_service_destroy(self, sh):
+        self.bmpow_service_stop(sh)
+        self.bmpow_batch_destroy(self.services[sh - 1]['h'])
 
     def bmpow_last_error(self):
         return b'injected step failure' if self.fail_step else b''
