@@ -170,6 +170,15 @@ void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, S
   }
 }
 
+uint64_t expect_cap(uint64_t target, size_t S, uint64_t chunk) {
+  // E = 2^64 / (target + 1): the expected trials to the first hit (each trial is <= target with
+  // probability (target + 1) / 2^64)
+  const double e = 18446744073709551616.0 / ((double)target + 1.0);
+  const double cap = kExpectWindows * e;
+  const uint64_t floor_ = (uint64_t)S * chunk;  // every shard gets at least one chunk of the object
+  return cap < (double)floor_ ? floor_ : (cap >= 1.8e19 ? kU64Max : (uint64_t)cap);
+}
+
 bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p) {
   while (b.first_pending < b.n && b.done[b.first_pending] != BMPOW_PENDING) ++b.first_pending;
   if (b.pending == 0) return false;
@@ -183,11 +192,16 @@ bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, S
   // windows: pending objects in slot order, k chunks each
   p.wins.clear();
   const uint64_t k = std::max<uint64_t>(1, total_chunks / b.pending);
+  // fewer pending objects than shards: each window is nonce-sharded over several shards
+  const bool split = S > 1 && b.pending < S;
   uint64_t acc = 0;
   for (size_t i = b.first_pending; i < b.n && acc < total_chunks; ++i) {
     if (b.done[i] != BMPOW_PENDING) continue;
     const uint64_t st = b.next[i];
     uint64_t want = k * p.chunk;
+#ifndef BM_NO_EXPECT_CAP  // (A/B knob: the uncapped windows of round 1)
+    if (split) want = std::min(want, expect_cap(b.objs[i].target, S, p.chunk));
+#endif
     const uint64_t room = kU64Max - st;  // nonces remaining after st
     if (room < want - 1) want = room + 1;   // st + want - 1 <= 2^64-1
     const uint64_t ch = (want + p.chunk - 1) / p.chunk;

@@ -84,8 +84,19 @@ struct StepPlan {
 // nonce-sharded, small ones object-sharded; each item's chunk_base is relative to its shard.
 void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p);
 
+// With fewer pending objects than shards, each window is cut into contiguous per-shard slices, and a
+// shard whose slice lies above the object's first hit cannot know it: it hashes its slice up to a hit
+// of its own (~E trials) or its end.  So such a window is capped at kExpectWindows x E nonces (E =
+// 2^64 / (target + 1), the expected trials to a hit; at least one chunk per shard): a C1-sized object
+// (E ~ 1.3e7) over 8 GPUs takes a step of 2E / 8 nonces per GPU (13.5 % of the time a second one)
+// instead of 2^28-nonce slices.  With as many objects as shards or more, objects are object-sharded
+// and a shard's own early exit already stops at its object's hit: no cap (it would only add steps).
+constexpr double kExpectWindows = 2.0;
+uint64_t expect_cap(uint64_t target, size_t S, uint64_t chunk);
+
 // Windows for the next step over S shards with about `budget` trials (0 = step_trials x S): pending
-// objects in slot order, k chunks each.  Returns false (p untouched) when nothing is pending.
+// objects in slot order, k chunks each (capped by expect_cap when fewer than S are pending).
+// Returns false (p untouched) when nothing is pending.
 bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p);
 
 // Fold the step's per-shard results (res[s][k] for p.items[s][k]) into the state: the min over

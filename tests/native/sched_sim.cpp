@@ -171,6 +171,50 @@ static void scenario_batches() {
   }
 }
 
+// ---- scenario 1b: over several shards a window is capped near the expected trials to a hit ----
+static void scenario_expect_cap() {
+  std::mt19937_64 rng(11);
+  for (uint64_t E : {1000ull, 1000000ull, 12700000ull, 1ull << 40}) {
+    std::vector<Obj> objs = random_objs(rng, 1, 1);
+    objs[0].target = kU64Max / E;
+    BatchState b;
+    init(b, 1, objs[0].ih, &objs[0].target, &objs[0].start);
+    for (size_t S : {1, 2, 8}) {
+      StepPlan p;
+      CHECK(plan_step(b, 0, 1 << 28, S, p), "plan_step");
+      const uint64_t window = p.wins[0].chunks * p.chunk;
+      const uint64_t full = ((uint64_t)1 << 28) * S;
+      if (S == 1) {
+        CHECK(window == full, "S=1: window %llu != budget", (unsigned long long)window);
+      } else {
+        const uint64_t cap = std::max<uint64_t>(S * p.chunk, (uint64_t)(kExpectWindows * (double)E));
+        CHECK(window <= std::min(full, cap) + p.chunk && window >= S * p.chunk, "E=%llu S=%zu: window %llu",
+              (unsigned long long)E, S, (unsigned long long)window);
+      }
+    }
+    std::vector<SimShard> shards(8);
+    if (E <= 1000000) {  // and the capped steps still give the exact answer
+      while (sim_step(b, shards, 0, 1 << 16)) {
+      }
+      expect_exact(objs[0], b.done[0], b.nonce[0], b.trial[0], "expect_cap", 0);
+    }
+  }
+  // as many objects as shards: object-sharded, no cap (each window a shard's whole share)
+  std::vector<Obj> objs = random_objs(rng, 8, 1);
+  std::vector<uint8_t> ihs(64 * 8);
+  std::vector<uint64_t> tg(8), st(8, 1);
+  for (size_t i = 0; i < 8; ++i) {
+    memcpy(&ihs[64 * i], objs[i].ih, 64);
+    tg[i] = kU64Max / 1000;
+  }
+  BatchState b;
+  init(b, 8, ihs.data(), tg.data(), st.data());
+  StepPlan p;
+  plan_step(b, 0, 1 << 28, 8, p);
+  for (const Win& w : p.wins)
+    CHECK(w.chunks * p.chunk == ((uint64_t)1 << 28), "object-sharded window capped: %llu", (unsigned long long)w.count);
+}
+
 // ---- scenario 2: windows clipped at the top of the nonce space ----
 static void scenario_top_of_space() {
   std::mt19937_64 rng(2);
@@ -535,6 +579,7 @@ static void scenario_service() {
 
 int main() {
   scenario_batches();
+  scenario_expect_cap();
   scenario_top_of_space();
   scenario_session();
   scenario_min_trial();
