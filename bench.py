@@ -181,7 +181,11 @@ def solve_claimed(lib, h, claimer, tag, low_water):
     _lib.check(lib, lib.bmpow_batch_set_pending(h, 0, claimer.n, 0), 'bmpow_batch_set_pending')
     claimer.start(tag)
     mine, pending, exhausted = [], 0, False
+    t_last = time.perf_counter()
     while True:
+        if time.perf_counter() - t_last > 30:  # a progress line for long steps (C5 at full size)
+            t_last = time.perf_counter()
+            print('bench: %s: %d objects pending on this rank' % (tag, pending), file=sys.stderr, flush=True)
         while not exhausted and pending < low_water:
             r = claimer.claim()
             if r is None:
