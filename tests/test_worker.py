@@ -149,7 +149,9 @@ class BatchLib(object):
                 for (tk, _, _), k in zip(new, sl):
                     svc['live'][k] = tk
             fin, rc = [], 0
-            if self.fail_step:
+            if not svc['live']:  # the library steps only a non-empty session
+                pass
+            elif self.fail_step:
                 rc = -3
             else:
                 self.bmpow_batch_step(h, 0)
@@ -508,6 +510,39 @@ def test_gpu_hippow_shutdown(gpulib):
             hippow.do_opencl_pow('00' * 64, 0)
     finally:
         state.shutdown = 0
+
+
+@gpu
+def test_gpu_batch_and_service_shutdown(gpulib, coracle):
+    """state.shutdown interrupts run_batch and PowService on the device within a poll interval plus a
+    step (the dev/powinterrupttest.py pattern), and both work again once it is cleared."""
+    hard = [(0, bytes(64)), (U64 // 1000, hashlib.sha512(b'a').digest())]  # target 0: never found
+    t = threading.Timer(0.3, lambda: setattr(state, 'shutdown', 1))
+    t.start()
+    t0 = time.time()
+    try:
+        with pytest.raises(StopIteration, match='Interrupted'):
+            proofofwork.run_batch(hard)
+        assert time.time() - t0 < 5
+    finally:
+        t.join()
+        state.shutdown = 0
+    svc = worker.PowService().start()
+    try:
+        f = svc.submit(0, bytes(64))
+        time.sleep(0.2)
+        state.shutdown = 1
+        t0 = time.time()
+        with pytest.raises(StopIteration, match='Interrupted'):
+            f.result(10)
+        assert time.time() - t0 < 5
+        state.shutdown = 0
+        ih = hashlib.sha512(b'after').digest()
+        assert svc.submit(U64 // 5000, ih).result(30) == list(coracle.search(ih, U64 // 5000))
+    finally:
+        state.shutdown = 0
+        svc.stop(10)
+    assert proofofwork.run_batch(hard[1:]) == [list(coracle.search(hard[1][1], hard[1][0]))]
 
 
 # ------------------------------------------------------------------ every singleWorker object kind
