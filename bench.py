@@ -12,9 +12,10 @@ table is uploaded before the timed region (inputs resident in HBM); each step re
 per-object state on the device (bmpow_batch_reset) and runs scheduler steps to completion.
 
 Multi-GPU (torch.distributed.run, one process per GPU): each rank drives its own GPU
-(LOCAL_RANK) on its own 1,024-object batch (seed + rank): units are independent, so the
-batch is sharded with no data-path collective ("scaling": "weak").  gloo carries only the
-timing barrier and the max-over-ranks / sum-over-ranks reductions.
+(LOCAL_RANK); the global batch is 1,024 objects per GPU, resident on every rank, and ranks
+claim pieces of it on demand through the process group's TCP store (run_batch_bench), so all
+GPUs finish together.  Units are independent: no data-path collective ("scaling": "weak");
+gloo carries only the timing barrier and the max-over-ranks / sum-over-ranks reductions.
 
 value = useful double-SHA-512 trials per second over the whole job (sum over objects of the
 found nonce, i.e. the trials the sequential _doSafePoW would need -- the reference's own

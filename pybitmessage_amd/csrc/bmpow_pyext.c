@@ -39,13 +39,23 @@ static PyObject *verify_list(PyObject *self, PyObject *args) {
         Py_XDECREF(ok);
         return PyErr_NoMemory();
     }
+    PyObject **held = (PyObject **)malloc(sizeof(*held) * (size_t)(n ? n : 1));
+    if (!held) {
+        free(ptrs); free(lens); free(vn); free(ve); free(vr);
+        Py_DECREF(ok);
+        return PyErr_NoMemory();
+    }
     for (Py_ssize_t i = 0; i < n; ++i) {
         PyObject *o = PyList_GET_ITEM(list, i);
         if (!PyBytes_CheckExact(o)) {
-            free(ptrs); free(lens); free(vn); free(ve); free(vr);
+            for (Py_ssize_t j = 0; j < i; ++j) Py_DECREF(held[j]);
+            free(held); free(ptrs); free(lens); free(vn); free(ve); free(vr);
             Py_DECREF(ok);
             return PyErr_Format(PyExc_TypeError, "object %zd is not bytes", i);
         }
+        /* a reference of our own: another thread may change the list while the GIL is released */
+        Py_INCREF(o);
+        held[i] = o;
         ptrs[i] = (const uint8_t *)PyBytes_AS_STRING(o);
         lens[i] = (uint64_t)PyBytes_GET_SIZE(o);
         vn[i] = ntpb;
@@ -53,11 +63,11 @@ static PyObject *verify_list(PyObject *self, PyObject *args) {
         vr[i] = recv;
     }
     int rc;
-    /* the list (and so every bytes object) stays referenced by the caller for the whole call */
     Py_BEGIN_ALLOW_THREADS
     rc = ((verify_ptrs_fn)(uintptr_t)fn_addr)((size_t)n, ptrs, lens, vn, ve, vr, (uint8_t *)PyBytes_AS_STRING(ok));
     Py_END_ALLOW_THREADS
-    free(ptrs); free(lens); free(vn); free(ve); free(vr);
+    for (Py_ssize_t i = 0; i < n; ++i) Py_DECREF(held[i]);
+    free(held); free(ptrs); free(lens); free(vn); free(ve); free(vr);
     PyObject *res = Py_BuildValue("(iO)", rc, ok);
     Py_DECREF(ok);
     return res;

@@ -202,3 +202,38 @@ def test_fast_marshalling_passes_every_object_in_place():
     assert list(ok) == [len(o) & 1 for o in objs]
     with pytest.raises(TypeError):
         fast.verify_list(ctypes.cast(cb, ctypes.c_void_p).value, [b'x' * 20, bytearray(20)], 0, 0, 0)
+
+
+def test_fast_marshalling_holds_the_objects_while_the_gil_is_released():
+    """The walk takes a reference to every object before it releases the GIL: another thread that
+    empties the list meanwhile (here the stand-in entry point itself) frees nothing the library is
+    reading, and the references are dropped again afterwards."""
+    import ctypes
+    import sys
+
+    from pybitmessage_amd import verify
+    fast = verify._load_fast()
+    if fast is None:
+        pytest.skip('_bmpow_fast not built')
+    objs = [bytes([7, i % 256]) * (300 + i) for i in range(200)]
+    expect = [bytes(o) for o in objs]
+    refs = [sys.getrefcount(o) for o in objs]
+    shared = list(objs)
+    proto = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p),
+                             ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                             ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_int64),
+                             ctypes.POINTER(ctypes.c_uint8))
+    state = {}
+
+    def fake(n, ptrs, lens, ntpb, extra, recv, ok):
+        state['during'] = [sys.getrefcount(o) for o in objs]
+        del shared[:]
+        for i in range(n):
+            assert ctypes.string_at(ptrs[i], lens[i]) == expect[i]
+            ok[i] = 1
+        return 0
+    cb = proto(fake)
+    rc, ok = fast.verify_list(ctypes.cast(cb, ctypes.c_void_p).value, shared, 0, 0, 0)
+    assert rc == 0 and list(ok) == [1] * len(objs)
+    assert all(d == r + 2 for d, r in zip(state['during'], refs))  # the list's + the walk's own
+    assert [sys.getrefcount(o) for o in objs] == refs
