@@ -91,6 +91,9 @@ struct Shard {
   uint64_t* d_vpow = nullptr;
   uint64_t* h_vpow = nullptr;  // pinned
   size_t vobj_cap = 0;
+  uint32_t* d_vbins = nullptr;  // work bins of the binned verification kernel (grow-only)
+  size_t vbins_cap = 0;
+  int cus = 0;                  // compute units of the device (the binned kernel: 4 bins per CU)
 };
 
 std::vector<Shard> g_shards;
@@ -144,6 +147,7 @@ void free_shard(Shard& s) {
   if (s.d_vobj) (void)hipFree(s.d_vobj);
   if (s.d_vpow) (void)hipFree(s.d_vpow);
   if (s.h_vpow) (void)hipHostFree(s.h_vpow);
+  if (s.d_vbins) (void)hipFree(s.d_vbins);
   if (s.ev0) (void)hipEventDestroy(s.ev0);
   if (s.ev1) (void)hipEventDestroy(s.ev1);
   if (s.stream) (void)hipStreamDestroy(s.stream);
@@ -156,6 +160,7 @@ int make_shard(int dev, Shard& s) {
   HIPTRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   HIPTRY(hipEventCreate(&s.ev0));
   HIPTRY(hipEventCreate(&s.ev1));
+  HIPTRY(hipDeviceGetAttribute(&s.cus, hipDeviceAttributeMultiprocessorCount, dev));
   HIPTRY(hipMalloc(&s.d_trials, sizeof(unsigned long long)));
   HIPTRY(hipHostMalloc(&s.h_trials, sizeof(unsigned long long), hipHostMallocDefault));
   return ensure_items(s, 1024);
@@ -532,6 +537,7 @@ struct bmpow_vbatch {
     uint4* d_pool = nullptr;
     uint64_t* d_pow = nullptr;
     uint64_t* h_pow = nullptr;  // pinned
+    uint32_t* d_bins = nullptr; // plan_bins' offsets + group lists (binned kernel), or null
     bool borrowed = false;      // buffers belong to the shard (one-shot path)
   };
   std::vector<Part> parts;
@@ -551,6 +557,7 @@ void vbatch_free(bmpow_vbatch* vb) {
     if (pt.d_pool) (void)hipFree(pt.d_pool);
     if (pt.d_pow) (void)hipFree(pt.d_pow);
     if (pt.h_pow) (void)hipHostFree(pt.h_pow);
+    if (pt.d_bins) (void)hipFree(pt.d_bins);
   }
   vb->parts.clear();
 }
@@ -636,10 +643,27 @@ int vbatch_upload_transient(bmpow_vbatch::Part& pt, const std::vector<Span>& obj
     }
     j = j1;
   }
+  if (!pt.bins.empty()) {
+    size_t cap = sh.vbins_cap;
+    const int rc = grow_device(sh.d_vbins, cap, pt.bins.size() * sizeof(uint32_t));
+    sh.vbins_cap = cap;
+    if (rc < 0) return rc;
+    pt.d_bins = sh.d_vbins;
+    HIPTRY(hipMemcpyAsync(pt.d_bins, pt.bins.data(), pt.bins.size() * sizeof(uint32_t), hipMemcpyHostToDevice,
+                          sh.stream));
+  }
   // the descriptors last: the padding pass filled their nonces (one pass over the objects' memory)
   HIPTRY(hipMemcpyAsync(pt.d_obj, ho.data(), m * sizeof(bv_obj), hipMemcpyHostToDevice, sh.stream));
   HIPTRY(hipStreamSynchronize(sh.stream));
   return 0;
+}
+
+// The binned kernel balances the SIMDs of a flood with at least a few waves per SIMD; a smaller
+// one runs one wave per group in sorted order.  BMPOW_VBINNED=0/1 forces either (A/B runs).
+bool verify_binned(size_t m, size_t nbins) {
+  if (nbins == 0) return false;
+  if (const char* e = std::getenv("BMPOW_VBINNED")) return std::atoi(e) != 0;
+  return (m + BV_BLOCK - 1) / BV_BLOCK >= 2 * nbins;
 }
 
 int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs, bool transient = false) {
@@ -648,7 +672,12 @@ int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs, bool transient
   if (bmsched::plan_verify(objs, g_shards.size(), plan, vb->blocks) < 0)
     return set_err(BMPOW_E_ARG, "too many objects, an object too large, or a payload pool above 2^32 blocks");
   vb->parts.resize(plan.size());
-  for (size_t i = 0; i < plan.size(); ++i) static_cast<bmsched::VPart&>(vb->parts[i]) = std::move(plan[i]);
+  for (size_t i = 0; i < plan.size(); ++i) {
+    bmsched::VPart& pt = vb->parts[i];
+    pt = std::move(plan[i]);
+    const size_t nbins = 4 * (size_t)g_shards[pt.shard].cus;
+    if (verify_binned(pt.orig.size(), nbins)) bmsched::plan_bins(pt, nbins);
+  }
   for (auto& pt : vb->parts) {
     Shard& sh = g_shards[pt.shard];
     HIPTRY(hipSetDevice(sh.dev));
@@ -667,6 +696,10 @@ int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs, bool transient
     HIPTRY(hipHostMalloc(&pt.h_pow, m * sizeof(uint64_t), hipHostMallocDefault));
     HIPTRY(hipMemcpy(pt.d_obj, pt.ho.data(), m * sizeof(bv_obj), hipMemcpyHostToDevice));
     HIPTRY(hipMemcpy(pt.d_pool, pool.get(), pt.blocks * 128, hipMemcpyHostToDevice));
+    if (!pt.bins.empty()) {
+      HIPTRY(hipMalloc(&pt.d_bins, pt.bins.size() * sizeof(uint32_t)));
+      HIPTRY(hipMemcpy(pt.d_bins, pt.bins.data(), pt.bins.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
   }
   return 0;
 }
@@ -676,7 +709,11 @@ int vbatch_run_locked(bmpow_vbatch* vb, uint64_t* pow_out) {
     Shard& sh = g_shards[pt.shard];
     HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(hipEventRecord(sh.ev0, sh.stream));
-    HIPTRY(bv_launch_pow(sh.stream, pt.d_obj, (uint32_t)pt.orig.size(), pt.d_pool, pt.d_pow));
+    if (pt.d_bins)
+      HIPTRY(bv_launch_pow_binned(sh.stream, pt.d_obj, (uint32_t)pt.orig.size(), pt.d_pool, pt.d_pow, pt.d_bins,
+                                  (uint32_t)pt.nbins));
+    else
+      HIPTRY(bv_launch_pow(sh.stream, pt.d_obj, (uint32_t)pt.orig.size(), pt.d_pool, pt.d_pow));
     HIPTRY(hipEventRecord(sh.ev1, sh.stream));
     HIPTRY(hipMemcpyAsync(pt.h_pow, pt.d_pow, pt.orig.size() * sizeof(uint64_t), hipMemcpyDeviceToHost, sh.stream));
   }

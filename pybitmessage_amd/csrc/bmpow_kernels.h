@@ -7,6 +7,8 @@
 #include "secp256k1_dev.h"
 
 hipError_t bv_launch_pow(hipStream_t st, const bv_obj* objs, uint32_t n, const uint4* pool, uint64_t* pow_out);
+hipError_t bv_launch_pow_binned(hipStream_t st, const bv_obj* objs, uint32_t n, const uint4* pool, uint64_t* pow_out,
+                                const uint32_t* bins, uint32_t nbins);
 
 hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
                             const bm_item* items, uint32_t nitems, unsigned long long* best, uint32_t* found,

@@ -49,6 +49,7 @@ struct bm_minpart {
 // payload is stored SHA-512-padded in a pool of 128-B blocks; objects are sorted by block
 // count (descending) on the host so the lanes of a wave loop the same number of times.
 #define BV_BLOCK 64
+#define BV_BINNED_WG 1024  // bv_pow_binned_kernel: 16 waves per CU, 4 per SIMD
 struct bv_obj {
   uint32_t blk;    // first 128-B block of the padded payload in the pool
   uint32_t nblk;   // padded blocks (>= 1)

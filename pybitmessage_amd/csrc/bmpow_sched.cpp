@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstring>
+#include <queue>
 #include <thread>
 
 namespace bmsched {
@@ -334,7 +335,34 @@ void pad_into(const uint8_t* msg, uint64_t m, uint8_t* dst, uint64_t nblk) {
   }
 }
 
-int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& parts, uint64_t& total_blocks) {
+void plan_bins(VPart& pt, size_t nbins) {
+  const size_t m = pt.orig.size();
+  const size_t G = (m + BV_BLOCK - 1) / BV_BLOCK;
+  pt.nbins = nbins;
+  pt.bins.assign(nbins + 1 + G, 0);
+  if (nbins == 0) return;
+  // LPT: groups arrive longest first (the objects are sorted); min-heap of (load, bin)
+  using LB = std::pair<uint64_t, uint32_t>;
+  std::priority_queue<LB, std::vector<LB>, std::greater<LB>> heap;
+  for (uint32_t b = 0; b < nbins; ++b) heap.push({0, b});
+  std::vector<uint32_t> owner(G), count(nbins, 0);
+  for (size_t g = 0; g < G; ++g) {
+    LB top = heap.top();
+    heap.pop();
+    owner[g] = top.second;
+    count[top.second]++;
+    top.first += (uint64_t)pt.ho[g * BV_BLOCK].nblk + 2;
+    heap.push(top);
+  }
+  uint32_t* off = pt.bins.data();
+  for (size_t b = 0; b < nbins; ++b) off[b + 1] = off[b] + count[b];
+  std::vector<uint32_t> fill(off, off + nbins);
+  uint32_t* list = off + nbins + 1;
+  for (size_t g = 0; g < G; ++g) list[fill[owner[g]]++] = (uint32_t)g;
+}
+
+int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& parts, uint64_t& total_blocks,
+                size_t nbins) {
   const size_t n = objs.size();
   parts.clear();
   if (n > 0xffffffffULL) return BMPOW_E_ARG;
@@ -387,6 +415,7 @@ int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& par
     }
     pt.blocks = blk;
     pt.eol.assign(pt.orig.size(), 0);
+    if (nbins) plan_bins(pt, nbins);
     if (!pt.orig.empty()) parts.push_back(std::move(pt));
   }
   return 0;

@@ -135,13 +135,27 @@ struct VPart {
   std::vector<bv_obj> ho;      // per sorted position: first block (part-relative), blocks, nonce
   std::vector<uint64_t> eol;   // per sorted position: expiresTime (object[8:16]; 0 if shorter), set by pad_range
   uint64_t blocks = 0;
+  // work bins of bv_pow_binned_kernel (plan_bins): bins[0..nbins] are offsets into the group list
+  // that follows them at bins[nbins + 1 ..]; empty when the part is not binned
+  std::vector<uint32_t> bins;
+  size_t nbins = 0;
 };
 
 // Sort objects by padded block count (descending, stable) and cut them into per-shard parts of
 // equal block totals.  Reads only the lengths: the objects' bytes are first touched by pad_range,
 // which also fills each descriptor's nonce and expiresTime (one pass over memory, in parallel).
 // Returns BMPOW_E_ARG on size limits, else 0.
-int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& parts, uint64_t& total_blocks);
+int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& parts, uint64_t& total_blocks,
+                size_t nbins = 0);
+
+// Deal a part's waves to nbins work bins, one per SIMD of its device (nbins a multiple of 4: four
+// per workgroup of bv_pow_binned_kernel, one workgroup per CU).  A wave is BV_BLOCK consecutive
+// objects of the sorted order (group g = objects [g * BV_BLOCK, (g + 1) * BV_BLOCK)); it costs its
+// first object's block count + 2 (the trial's two compressions), since a wave runs as long as its
+// longest lane.  Longest first, each to the least-loaded bin (LPT), so every SIMD's total is the
+// average to within about one wave, whatever the objects' size mix.  The bins' group lists keep
+// that order (a SIMD's waves take its longest groups first).
+void plan_bins(VPart& pt, size_t nbins);
 
 // Pad objects [j0, j1) of a part (sorted order) into dst (their blocks from blk0 on) and fill their
 // nonce / expiresTime, over up to 16 host threads: a memory-bound copy of every payload.

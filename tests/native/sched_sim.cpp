@@ -430,6 +430,38 @@ static void scenario_verify() {
     }
     CHECK(seen == total, "blocks");
     for (int h : hits) CHECK(h == 1, "object placed %d times", h);
+    // the binned verification kernel's work bins: every group in exactly one bin, longest first
+    // within a bin, and LPT's bound on the most loaded bin (average + one group)
+    for (VPart& pt : parts) {
+      for (size_t nbins : {4, 8, 1024}) {
+        plan_bins(pt, nbins);
+        const size_t G = (pt.orig.size() + BV_BLOCK - 1) / BV_BLOCK;
+        CHECK(pt.nbins == nbins && pt.bins.size() == nbins + 1 + G, "bins layout");
+        CHECK(pt.bins[0] == 0 && pt.bins[nbins] == G, "bin offsets");
+        std::vector<int> got(G, 0);
+        uint64_t tot = 0, mx = 0, maxcost = 0;
+        for (size_t b = 0; b < nbins; ++b) {
+          uint64_t load = 0, prev = ~0ull;
+          for (uint32_t i = pt.bins[b]; i < pt.bins[b + 1]; ++i) {
+            const uint32_t g = pt.bins[nbins + 1 + i];
+            CHECK(g < G, "group index");
+            got[g]++;
+            const uint64_t c = pt.ho[(size_t)g * BV_BLOCK].nblk + 2;
+            for (size_t j = (size_t)g * BV_BLOCK; j < std::min(pt.orig.size(), (size_t)(g + 1) * BV_BLOCK); ++j)
+              CHECK(pt.ho[j].nblk + 2 <= c, "a group's cost is its longest object");
+            CHECK(c <= prev, "bin not longest first");
+            prev = c;
+            load += c;
+            maxcost = std::max(maxcost, c);
+          }
+          tot += load;
+          mx = std::max(mx, load);
+        }
+        for (int h : got) CHECK(h == 1, "group dealt %d times", h);
+        CHECK(mx <= tot / nbins + maxcost, "LPT bound: %llu > %llu + %llu", (unsigned long long)mx,
+              (unsigned long long)(tot / nbins), (unsigned long long)maxcost);
+      }
+    }
   }
 }
 

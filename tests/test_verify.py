@@ -119,6 +119,32 @@ def test_gpu_pow_random_flood_vs_hashlib(gpulib):
 
 
 @gpu
+def test_gpu_both_verification_kernels(gpulib, shards, monkeypatch):
+    """The binned kernel (one workgroup per CU, work bins per SIMD, bmsched::plan_bins) and the
+    sorted one-wave-per-group kernel give the same POW values, forced either way on a ragged flood
+    (BMPOW_VBINNED); the flood is too small for the default rule to bin it, so most bins are empty.
+    Then a flood large enough that the default bins it (>= 2 groups per SIMD), against hashlib."""
+    from pybitmessage_amd import verify
+    rng = random.Random(11)
+    objs = [rng.randbytes(rng.choice([8, 16, 135, 136, rng.randrange(8, 20000)])) for _ in range(4000)]
+    objs.append(bytes(8) + rng.randbytes(262144))
+    want = [targets.pow_value(o) for o in objs]
+    for layout in ([0], [0, 0, 0]):
+        shards(layout)
+        for mode in ('0', '1'):
+            monkeypatch.setenv('BMPOW_VBINNED', mode)
+            assert verify.pow_values(objs) == want, (layout, mode)
+            with verify.VerifyBatch(objs) as vb:
+                assert vb.run().tolist() == want, (layout, mode)
+    monkeypatch.delenv('BMPOW_VBINNED')
+    shards([0])
+    big = [rng.randbytes(rng.choice([54, 208, rng.randrange(520, 16392)])) for _ in range(140000)]
+    got = verify.pow_values(big)
+    for i in range(0, len(big), 97):
+        assert got[i] == targets.pow_value(big[i]), i
+
+
+@gpu
 def test_gpu_verify_session_and_shards(gpulib, shards):
     from pybitmessage_amd import verify
     rng = random.Random(8)
