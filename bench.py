@@ -449,12 +449,36 @@ def summarize_verify(args, dist, r, lib_version):
         # the outer double hash of each object
         ops = 4144 * st.verify_blocks + OPS_PER_TRIAL * st.verify_objects
         achieved = ops / (st.verify_kernel_ms * 1e-3) / 1e12
-        line['roofline'] = {'bound': 'valu', 'kernel': 'bv_pow_kernel', 'achieved': round(achieved, 3),
+        # the library bins floods of >= 2 waves per SIMD (bmpow_host.hip verify_binned)
+        binned = r['objects'] // max(args.steps, 1) >= 2 * 64 * 4 * 256
+        line['roofline'] = {'bound': 'valu', 'kernel': 'bv_pow_binned_kernel' if binned else 'bv_pow_kernel',
+                            'achieved': round(achieved, 3),
                             'peak': round(PEAK_TOPS, 3), 'unit': 'T int32 lane-ops/s', 'frac': round(achieved / PEAK_TOPS, 4),
                             'traffic': None, 'blocks_per_s': round(st.verify_blocks / (st.verify_kernel_ms * 1e-3), 1),
                             'avg_launch_ms': round(st.verify_kernel_ms / max(args.steps, 1), 3),
                             'kernel_busy_frac': round(st.verify_kernel_ms * 1e-3 / r['elapsed'], 4)}
+        pmc = kernel_pmc('verify_binned.json') if binned else None
+        if pmc:
+            line['roofline']['traffic'] = pmc.pop('hbm_bytes_per_launch', None)
+            line['roofline']['counters'] = pmc
     return line
+
+
+def kernel_pmc(name):
+    """Counters of a kernel from the committed rocprofv3 PMC passes (tools/r02_pmc_verify_addr.sh ->
+    tools/pmc_kernel.py -> profiles/r02/pmc/<name>): per-launch HBM bytes (2 x FETCH_SIZE + WRITE_SIZE)
+    and the VALU issue figures."""
+    path = os.path.join(ROOT, 'profiles', 'r02', 'pmc', name)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)['derived']
+    out = {'source': 'profiles/r02/pmc/' + name}
+    for k in ('hbm_bytes_per_launch', 'valu_issue_util', 'valu_instr_per_simd_quad_cycle', 'dual_issue_share',
+              'simd_busy_frac', 'eff_clock_ghz'):
+        if d.get(k) is not None:
+            out[k] = round(d[k], 4) if k != 'hbm_bytes_per_launch' else round(d[k])
+    return out
 
 
 def _verify_pool_worker(seconds):
@@ -553,6 +577,18 @@ def summarize_addr(args, dist, r, lib_version):
         line['kernel'] = {'name': 'ar_search_kernel', 'tries_per_s': round(st.addr_tries / (st.addr_kernel_ms * 1e-3), 1),
                           'launches': int(st.addr_launches), 'kernel_ms': round(st.addr_kernel_ms, 3),
                           'kernel_busy_frac': round(st.addr_kernel_ms * 1e-3 / r['elapsed'], 4)}
+    pmc = kernel_pmc('addrgen_%s.json' % args.addr_mode)
+    if pmc and pmc.get('valu_instr_per_simd_quad_cycle'):
+        # k*G has no implementation-independent op count like SHA-512's 8,288, so this roofline is
+        # in issued VALU lane-instructions: the measured instructions per SIMD quad-cycle against two
+        # (the 78.64 T dual-issue peak); one per quad-cycle is the single-issue ceiling
+        ipq = pmc['valu_instr_per_simd_quad_cycle']
+        clk = pmc.get('eff_clock_ghz') or 2.4
+        line['roofline'] = {'bound': 'valu', 'kernel': 'ar_search_kernel',
+                            'achieved': round(ipq * 1024 * clk * 1e9 / 4 * 64 / 1e12, 3), 'peak': round(PEAK_TOPS, 3),
+                            'unit': 'T VALU lane-instructions/s issued (no implementation-independent op count)',
+                            'frac': round(ipq / 2, 4), 'single_issue_frac': round(ipq, 4),
+                            'traffic': pmc.pop('hbm_bytes_per_launch', None), 'counters': pmc}
     return line
 
 
