@@ -666,15 +666,26 @@ bool verify_binned(size_t m, size_t nbins) {
   return (m + BV_BLOCK - 1) / BV_BLOCK >= 2 * nbins;
 }
 
+std::vector<bmsched::VPart> g_vplan;  // under g_mu
+
+// Hand a one-shot batch's plan vectors back to g_vplan before the batch is freed.
+void vbatch_release_plan(bmpow_vbatch* vb) {
+  g_vplan.resize(std::max(g_vplan.size(), vb->parts.size()));
+  for (size_t i = 0; i < vb->parts.size(); ++i) std::swap(static_cast<bmsched::VPart&>(vb->parts[i]), g_vplan[i]);
+}
+
 int vbatch_build(bmpow_vbatch* vb, const std::vector<Span>& objs, bool transient = false) {
   vb->n = objs.size();
-  std::vector<bmsched::VPart> plan;
+  // the plan's vectors live in g_vplan between calls (swapped into the parts here, back by
+  // vbatch_release_plan): a flood's descriptors are tens of MB, and fresh pages cost more than
+  // the planning
+  std::vector<bmsched::VPart>& plan = g_vplan;
   if (bmsched::plan_verify(objs, g_shards.size(), plan, vb->blocks) < 0)
     return set_err(BMPOW_E_ARG, "too many objects, an object too large, or a payload pool above 2^32 blocks");
   vb->parts.resize(plan.size());
   for (size_t i = 0; i < plan.size(); ++i) {
     bmsched::VPart& pt = vb->parts[i];
-    pt = std::move(plan[i]);
+    std::swap(pt, plan[i]);
     const size_t nbins = 4 * (size_t)g_shards[pt.shard].cus;
     if (verify_binned(pt.orig.size(), nbins)) bmsched::plan_bins(pt, nbins);
   }
@@ -1395,6 +1406,7 @@ int bmpow_pow_values(size_t n, const uint8_t* objs, const uint64_t* offsets, uin
   bmpow_vbatch vb;
   rc = vbatch_build(&vb, spans, true);
   if (rc == 0) rc = vbatch_run_locked(&vb, pow_out);
+  vbatch_release_plan(&vb);
   vbatch_free(&vb);
   return rc;
 }
@@ -1402,8 +1414,12 @@ int bmpow_pow_values(size_t n, const uint8_t* objs, const uint64_t* offsets, uin
 // shared by both verify entry points (internal linkage despite the extern "C" block)
 static int verify_spans_locked(size_t n, const uint8_t* const* ptrs, const uint64_t* lens, const uint64_t* ntpb,
                                const uint64_t* extra, const int64_t* recv_time, uint8_t* ok_out) {
-  std::vector<Span> spans;
-  std::vector<size_t> idx;
+  // scratch kept across calls under g_mu (a flood's worth of fresh pages costs several ms)
+  static std::vector<Span> spans;
+  static std::vector<size_t> idx;
+  static std::vector<uint64_t> pow, eol;
+  spans.clear();
+  idx.clear();
   spans.reserve(n);
   idx.reserve(n);
   for (size_t i = 0; i < n; ++i) {
@@ -1420,7 +1436,8 @@ static int verify_spans_locked(size_t n, const uint8_t* const* ptrs, const uint6
   using clk = std::chrono::steady_clock;
   auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
   const clk::time_point t0 = clk::now();
-  std::vector<uint64_t> pow(spans.size()), eol(spans.size());
+  pow.resize(spans.size());
+  eol.resize(spans.size());
   if (!spans.empty()) {
     bmpow_vbatch vb;
     int rc = vbatch_build(&vb, spans, true);
@@ -1430,6 +1447,7 @@ static int verify_spans_locked(size_t n, const uint8_t* const* ptrs, const uint6
     g_stats.verify_host_run_ms += ms(t1, clk::now());
     for (const auto& pt : vb.parts)  // expiresTime, read by the padding pass
       for (size_t j = 0; j < pt.orig.size(); ++j) eol[pt.orig[j]] = pt.eol[j];
+    vbatch_release_plan(&vb);
     vbatch_free(&vb);
     if (rc < 0) return rc;
   }

@@ -14,13 +14,55 @@
 #include <Python.h>
 #include <stdint.h>
 #include <stdlib.h>
+#include <string.h>
 
 typedef int (*verify_ptrs_fn)(size_t n, const uint8_t *const *objs, const uint64_t *lens, const uint64_t *ntpb,
                               const uint64_t *extra, const int64_t *recv_time, uint8_t *ok_out);
 
+/* Grow-only scratch reused across calls: a flood's arrays are MBs, and fresh pages cost a fault per
+ * 4 KB.  Taken under the GIL; a call that finds it busy (another thread inside the library with
+ * the GIL released) allocates its own. */
+typedef struct {
+    const uint8_t **ptrs;
+    uint64_t *lens, *vn, *ve;
+    int64_t *vr;
+    PyObject **held;
+    size_t cap;
+    int busy;
+} scratch_t;
+
+static scratch_t g_scratch;
+
+static void scratch_free(scratch_t *s) {
+    free(s->ptrs); free(s->lens); free(s->vn); free(s->ve); free(s->vr); free(s->held);
+    memset(s, 0, sizeof(*s));
+}
+
+static int scratch_reserve(scratch_t *s, size_t n) {
+    if (n <= s->cap) return 0;
+    scratch_t t;
+    memset(&t, 0, sizeof(t));
+    t.ptrs = (const uint8_t **)malloc(sizeof(*t.ptrs) * n);
+    t.lens = (uint64_t *)malloc(sizeof(*t.lens) * n);
+    t.vn = (uint64_t *)malloc(sizeof(*t.vn) * n);
+    t.ve = (uint64_t *)malloc(sizeof(*t.ve) * n);
+    t.vr = (int64_t *)malloc(sizeof(*t.vr) * n);
+    t.held = (PyObject **)malloc(sizeof(*t.held) * n);
+    if (!t.ptrs || !t.lens || !t.vn || !t.ve || !t.vr || !t.held) {
+        scratch_free(&t);
+        return -1;
+    }
+    t.cap = n;
+    t.busy = s->busy;
+    scratch_free(s);
+    *s = t;
+    return 0;
+}
+
 /* verify_list(fn_address, objects: list of bytes, ntpb: int, extra: int, recv: int) -> (rc, bytes ok)
  * rc < 0: the library's error code (the caller reads bmpow_last_error).  TypeError when an item
- * is not a bytes object (the caller converts those first). */
+ * is not a bytes object (the caller converts those first).  A zero ntpb / extra / recv is passed
+ * as a null array: the library reads it as 0 (the network minimum, "now"), as the reference does. */
 static PyObject *verify_list(PyObject *self, PyObject *args) {
     unsigned long long fn_addr, ntpb, extra;
     long long recv;
@@ -28,46 +70,51 @@ static PyObject *verify_list(PyObject *self, PyObject *args) {
     (void)self;
     if (!PyArg_ParseTuple(args, "KO!KKL", &fn_addr, &PyList_Type, &list, &ntpb, &extra, &recv)) return NULL;
     const Py_ssize_t n = PyList_GET_SIZE(list);
-    const uint8_t **ptrs = (const uint8_t **)malloc(sizeof(*ptrs) * (size_t)(n ? n : 1));
-    uint64_t *lens = (uint64_t *)malloc(sizeof(*lens) * (size_t)(n ? n : 1));
-    uint64_t *vn = (uint64_t *)malloc(sizeof(*vn) * (size_t)(n ? n : 1));
-    uint64_t *ve = (uint64_t *)malloc(sizeof(*ve) * (size_t)(n ? n : 1));
-    int64_t *vr = (int64_t *)malloc(sizeof(*vr) * (size_t)(n ? n : 1));
-    PyObject *ok = PyBytes_FromStringAndSize(NULL, n);
-    if (!ptrs || !lens || !vn || !ve || !vr || !ok) {
-        free(ptrs); free(lens); free(vn); free(ve); free(vr);
-        Py_XDECREF(ok);
+    const size_t cap = (size_t)(n ? n : 1);
+    scratch_t own;
+    memset(&own, 0, sizeof(own));
+    scratch_t *sc = g_scratch.busy ? &own : &g_scratch;
+    if (scratch_reserve(sc, cap) < 0) {
+        scratch_free(&own);
         return PyErr_NoMemory();
     }
-    PyObject **held = (PyObject **)malloc(sizeof(*held) * (size_t)(n ? n : 1));
-    if (!held) {
-        free(ptrs); free(lens); free(vn); free(ve); free(vr);
-        Py_DECREF(ok);
+    sc->busy = 1;
+    PyObject *ok = PyBytes_FromStringAndSize(NULL, n);
+    if (!ok) {
+        sc->busy = 0;
+        scratch_free(&own);
         return PyErr_NoMemory();
     }
     for (Py_ssize_t i = 0; i < n; ++i) {
+        /* the objects' headers are scattered over the heap: one cache miss each, so ask early */
+        if (i + 16 < n) __builtin_prefetch(PyList_GET_ITEM(list, i + 16), 1);
         PyObject *o = PyList_GET_ITEM(list, i);
         if (!PyBytes_CheckExact(o)) {
-            for (Py_ssize_t j = 0; j < i; ++j) Py_DECREF(held[j]);
-            free(held); free(ptrs); free(lens); free(vn); free(ve); free(vr);
+            for (Py_ssize_t j = 0; j < i; ++j) Py_DECREF(sc->held[j]);
+            sc->busy = 0;
+            scratch_free(&own);
             Py_DECREF(ok);
             return PyErr_Format(PyExc_TypeError, "object %zd is not bytes", i);
         }
         /* a reference of our own: another thread may change the list while the GIL is released */
         Py_INCREF(o);
-        held[i] = o;
-        ptrs[i] = (const uint8_t *)PyBytes_AS_STRING(o);
-        lens[i] = (uint64_t)PyBytes_GET_SIZE(o);
-        vn[i] = ntpb;
-        ve[i] = extra;
-        vr[i] = recv;
+        sc->held[i] = o;
+        sc->ptrs[i] = (const uint8_t *)PyBytes_AS_STRING(o);
+        sc->lens[i] = (uint64_t)PyBytes_GET_SIZE(o);
     }
+    const uint64_t *vn = NULL, *ve = NULL;
+    const int64_t *vr = NULL;
+    if (ntpb) { for (Py_ssize_t i = 0; i < n; ++i) sc->vn[i] = ntpb; vn = sc->vn; }
+    if (extra) { for (Py_ssize_t i = 0; i < n; ++i) sc->ve[i] = extra; ve = sc->ve; }
+    if (recv) { for (Py_ssize_t i = 0; i < n; ++i) sc->vr[i] = recv; vr = sc->vr; }
     int rc;
     Py_BEGIN_ALLOW_THREADS
-    rc = ((verify_ptrs_fn)(uintptr_t)fn_addr)((size_t)n, ptrs, lens, vn, ve, vr, (uint8_t *)PyBytes_AS_STRING(ok));
+    rc = ((verify_ptrs_fn)(uintptr_t)fn_addr)((size_t)n, sc->ptrs, sc->lens, vn, ve, vr,
+                                              (uint8_t *)PyBytes_AS_STRING(ok));
     Py_END_ALLOW_THREADS
-    for (Py_ssize_t i = 0; i < n; ++i) Py_DECREF(held[i]);
-    free(held); free(ptrs); free(lens); free(vn); free(ve); free(vr);
+    for (Py_ssize_t i = 0; i < n; ++i) Py_DECREF(sc->held[i]);
+    sc->busy = 0;
+    scratch_free(&own);
     PyObject *res = Py_BuildValue("(iO)", rc, ok);
     Py_DECREF(ok);
     return res;

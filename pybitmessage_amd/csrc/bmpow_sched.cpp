@@ -4,7 +4,11 @@
 
 #include <openssl/sha.h>
 
+#include <emmintrin.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <condition_variable>
 #include <chrono>
 #include <cstring>
 #include <queue>
@@ -335,6 +339,31 @@ void pad_into(const uint8_t* msg, uint64_t m, uint8_t* dst, uint64_t nblk) {
   }
 }
 
+// pad_into with non-temporal 16-B stores, for a 16-B aligned destination that is written once and
+// read by the DMA engine (the pinned staging): no read-for-ownership of the destination lines, so
+// the copy moves ~2/3 of the bytes a cached copy does.  The caller fences (stream_fence) before the
+// buffer is handed to the device.
+void pad_into_stream(const uint8_t* msg, uint64_t m, uint8_t* dst, uint64_t nblk) {
+  const uint64_t total = nblk * 128;
+  const uint64_t full = m & ~(uint64_t)15;  // whole 16-B pieces of the message
+  for (uint64_t o = 0; o < full; o += 16)
+    _mm_stream_si128((__m128i*)(dst + o), _mm_loadu_si128((const __m128i*)(msg + o)));
+  alignas(16) uint8_t tail[256];  // the rest of the message, the padding and the length: <= 2 blocks
+  const uint64_t rest = total - full;
+  std::memset(tail, 0, rest);
+  std::memcpy(tail, msg + full, m - full);
+  tail[m - full] = 0x80;
+  const uint64_t bits_lo = m << 3, bits_hi = m >> 61;
+  for (int j = 0; j < 8; ++j) {
+    tail[rest - 16 + j] = (uint8_t)(bits_hi >> (56 - 8 * j));
+    tail[rest - 8 + j] = (uint8_t)(bits_lo >> (56 - 8 * j));
+  }
+  for (uint64_t o = 0; o < rest; o += 16)
+    _mm_stream_si128((__m128i*)(dst + full + o), _mm_load_si128((const __m128i*)(tail + o)));
+}
+
+void stream_fence() { _mm_sfence(); }
+
 void plan_bins(VPart& pt, size_t nbins) {
   const size_t m = pt.orig.size();
   const size_t G = (m + BV_BLOCK - 1) / BV_BLOCK;
@@ -364,9 +393,11 @@ void plan_bins(VPart& pt, size_t nbins) {
 int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& parts, uint64_t& total_blocks,
                 size_t nbins) {
   const size_t n = objs.size();
-  parts.clear();
   if (n > 0xffffffffULL) return BMPOW_E_ARG;
-  std::vector<uint32_t> nblk(n);
+  // scratch kept across calls (a flood's vectors are tens of MB: fresh ones cost a page fault per
+  // 4 KB, more than the planning itself)
+  static thread_local std::vector<uint32_t> nblk, order;
+  nblk.resize(n);
   uint64_t total = 0;
   for (size_t i = 0; i < n; ++i) {
     const uint64_t b = padded_blocks(objs[i].len - 8);
@@ -379,7 +410,7 @@ int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& par
   // stable counting sort by block count, descending (block counts are small: <= 2,049 for the
   // protocol's 256 KiB objects, larger ones fall into one overflow bucket sorted on their own)
   constexpr uint32_t kBuckets = 4096;
-  std::vector<uint32_t> order(n);
+  order.resize(n);
   {
     std::vector<size_t> cnt(kBuckets + 1, 0);
     for (size_t i = 0; i < n; ++i) cnt[std::min(nblk[i], kBuckets)]++;
@@ -394,37 +425,130 @@ int plan_verify(const std::vector<Span>& objs, size_t S, std::vector<VPart>& par
       std::stable_sort(order.begin(), order.begin() + (ptrdiff_t)cnt[kBuckets],
                        [&](uint32_t a, uint32_t b) { return nblk[a] > nblk[b]; });
   }
-  size_t k = 0;
+  // parts are filled in place: a caller that passes the previous call's parts back keeps their
+  // vectors' capacity
+  size_t k = 0, used = 0;
   uint64_t acc = 0;
   for (size_t s = 0; s < S && k < n; ++s) {
-    VPart pt;
-    pt.shard = s;
     const uint64_t goal = total * (s + 1) / S;
+    size_t k1 = k;
+    for (uint64_t a = acc; k1 < n && (a < goal || s == S - 1); ++k1) a += nblk[order[k1]];
+    if (k1 == k) continue;
+    if (parts.size() <= used) parts.emplace_back();
+    VPart& pt = parts[used++];
+    pt.shard = s;
+    const size_t m = k1 - k;
+    pt.orig.resize(m);
+    pt.ho.resize(m);
     uint64_t blk = 0;
-    while (k < n && (acc < goal || s == S - 1)) {
-      const uint32_t i = order[k];
-      pt.orig.push_back(i);
-      bv_obj o;
-      o.blk = (uint32_t)blk;
-      o.nblk = nblk[i];
-      o.nonce = 0;  // pad_range reads it with the payload
-      pt.ho.push_back(o);
+    for (size_t j = 0; j < m; ++j) {
+      const uint32_t i = order[k + j];
+      pt.orig[j] = i;
+      pt.ho[j].blk = (uint32_t)blk;
+      pt.ho[j].nblk = nblk[i];
+      pt.ho[j].nonce = 0;  // pad_range reads it with the payload
       blk += nblk[i];
-      acc += nblk[i];
-      ++k;
     }
+    acc += blk;
+    k = k1;
     pt.blocks = blk;
-    pt.eol.assign(pt.orig.size(), 0);
+    pt.eol.assign(m, 0);
+    pt.bins.clear();
+    pt.nbins = 0;
     if (nbins) plan_bins(pt, nbins);
-    if (!pt.orig.empty()) parts.push_back(std::move(pt));
   }
+  parts.resize(used);
   return 0;
 }
 
+namespace {
+
+// Persistent workers for parallel_for: a flood's padding calls it once per 64 MB staging chunk
+// (17 times for 1.1 GB), and creating 15 threads per call cost more than the copy they share.
+// One caller at a time uses the pool; a concurrent caller (or a forked child, which inherits the
+// pool's state but not its threads) spawns threads of its own, as before.
+class Pool {
+ public:
+  explicit Pool(size_t workers) : pid_(getpid()) {
+    for (size_t w = 1; w <= workers; ++w) th_.emplace_back(&Pool::work, this, w);
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  size_t workers() const { return th_.size(); }
+  bool usable() const { return getpid() == pid_; }
+  std::mutex call_mu;  // held by the one caller using the pool
+  // Run body over nparts contiguous parts of [0, n): part 0 on the caller, the others on workers.
+  void run(size_t n, size_t nparts, const std::function<void(size_t, size_t)>& body) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      body_ = &body;
+      n_ = n;
+      nparts_ = nparts;
+      pending_ = nparts - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    body(0, n / nparts);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+    body_ = nullptr;
+  }
+
+ private:
+  void work(size_t id) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(size_t, size_t)>* body;
+      size_t n, nparts;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return quit_ || gen_ != seen; });
+        if (quit_) return;
+        seen = gen_;
+        if (id >= nparts_) continue;
+        body = body_;
+        n = n_;
+        nparts = nparts_;
+      }
+      (*body)(n * id / nparts, n * (id + 1) / nparts);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  const pid_t pid_;
+  std::vector<std::thread> th_;
+  std::mutex mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(size_t, size_t)>* body_ = nullptr;
+  size_t n_ = 0, nparts_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool quit_ = false;
+};
+
+constexpr size_t kMaxThreads = 16;  // the GPU box's CPU share
+
+Pool& pool() {
+  static Pool p(std::min<size_t>(kMaxThreads, std::max<size_t>(1, std::thread::hardware_concurrency())) - 1);
+  return p;
+}
+
+}  // namespace
+
 void parallel_for(size_t n, size_t grain, const std::function<void(size_t, size_t)>& body) {
   const size_t hw = std::max<size_t>(1, std::thread::hardware_concurrency());
-  const size_t nth = std::max<size_t>(1, std::min<size_t>({16, hw, n / std::max<size_t>(grain, 1) + 1}));
+  const size_t nth = std::max<size_t>(1, std::min<size_t>({kMaxThreads, hw, n / std::max<size_t>(grain, 1) + 1}));
   if (nth == 1) return body(0, n);
+  Pool& p = pool();
+  if (p.usable() && nth <= p.workers() + 1) {
+    std::unique_lock<std::mutex> lk(p.call_mu, std::try_to_lock);
+    if (lk.owns_lock()) return p.run(n, nth, body);
+  }
   std::vector<std::thread> th;
   for (size_t t = 1; t < nth; ++t) th.emplace_back(body, n * t / nth, n * (t + 1) / nth);
   body(0, n / nth);
@@ -439,12 +563,24 @@ void pad_range(const std::vector<Span>& objs, VPart& pt, size_t j0, size_t j1, u
   // a thread per ~2 MB (and per >= 64 objects), at most 16
   const size_t grain = std::max<size_t>(64, (size_t)(m / (bytes / (2u << 20) + 1)));
   parallel_for(m, grain, [&](size_t a, size_t b) {
+    constexpr size_t kAhead = 8;  // objects are read in sorted order, i.e. scattered: prefetch them
     for (size_t j = j0 + a; j < j0 + b; ++j) {
+      if (j + 2 * kAhead < j0 + b) __builtin_prefetch(&objs[pt.orig[j + 2 * kAhead]]);
+      if (j + kAhead < j0 + b) {
+        const Span& nx = objs[pt.orig[j + kAhead]];
+        __builtin_prefetch(nx.p);
+        __builtin_prefetch(nx.p + 64);
+      }
       const Span& sp = objs[pt.orig[j]];
       ho[j].nonce = load_be64(sp.p);
       pt.eol[j] = sp.len >= 16 ? load_be64(sp.p + 8) : 0;
+#ifdef BMSCHED_PAD_CACHED
       pad_into(sp.p + 8, sp.len - 8, dst + (uint64_t)(ho[j].blk - blk0) * 128, ho[j].nblk);
+#else
+      pad_into_stream(sp.p + 8, sp.len - 8, dst + (uint64_t)(ho[j].blk - blk0) * 128, ho[j].nblk);
+#endif
     }
+    stream_fence();  // this thread's streaming stores are globally visible before the join
   });
 }
 

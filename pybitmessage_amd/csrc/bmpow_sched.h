@@ -128,6 +128,9 @@ struct Span {
 // blocks of SHA-512 padding for an m-byte message: m + 1 (0x80) + 16 (bit length) rounded up
 uint64_t padded_blocks(uint64_t m);
 void pad_into(const uint8_t* msg, uint64_t m, uint8_t* dst, uint64_t nblk);
+// the same with non-temporal stores (dst 16-B aligned); stream_fence() before the device reads it
+void pad_into_stream(const uint8_t* msg, uint64_t m, uint8_t* dst, uint64_t nblk);
+void stream_fence();
 
 struct VPart {
   size_t shard = 0;

@@ -229,6 +229,17 @@ def test_fast_marshalling_passes_every_object_in_place():
     with pytest.raises(TypeError):
         fast.verify_list(ctypes.cast(cb, ctypes.c_void_p).value, [b'x' * 20, bytearray(20)], 0, 0, 0)
 
+    # zero difficulty / recvTime (the network minimum, "now") go as null arrays, which the library
+    # reads as 0 for every object
+    def fake0(n, ptrs, lens, ntpb, extra, recv, ok):
+        seen['null'] = (not ntpb, not extra, not recv)
+        for i in range(n):
+            ok[i] = 1
+        return 0
+    cb0 = proto(fake0)
+    rc, ok = fast.verify_list(ctypes.cast(cb0, ctypes.c_void_p).value, objs[:50], 0, 0, 0)
+    assert rc == 0 and seen['null'] == (True, True, True) and list(ok) == [1] * 50
+
 
 def test_fast_marshalling_holds_the_objects_while_the_gil_is_released():
     """The walk takes a reference to every object before it releases the GIL: another thread that
