@@ -337,42 +337,40 @@ class BatchResult(object):
     """The result of one object of a ``PowService.submit_many`` call: ``result(timeout)``,
     ``exception(timeout)`` and ``done()`` as on a ``concurrent.futures.Future``, without its
     per-object lock and condition (a Future costs more to create than the object's whole host-side
-    handling; the results of one call share one condition, notified once per completed batch)."""
-    __slots__ = ('_group', '_value', '_exc', '_done')
+    handling; the results of one call share one condition, notified once per completed batch).
+    ``_out`` is None while pending, then ``[trialValue, nonce]`` or the exception."""
+    __slots__ = ('_group', '_out')
 
     def __init__(self, group):
         self._group = group
-        self._value = None
-        self._exc = None
-        self._done = False
+        self._out = None
 
     def done(self):
-        return self._done
+        return self._out is not None
 
     def _wait(self, timeout):
-        if not self._done:
+        if self._out is None:
             with self._group.cv:
-                if not self._group.cv.wait_for(lambda: self._done, timeout):
+                if not self._group.cv.wait_for(self.done, timeout):
                     raise TimeoutError('PoW result not ready')
+        return self._out
 
     def result(self, timeout=None):
-        self._wait(timeout)
-        if self._exc is not None:
-            raise self._exc
-        return self._value
+        out = self._wait(timeout)
+        if isinstance(out, BaseException):
+            raise out
+        return out
 
     def exception(self, timeout=None):
-        self._wait(timeout)
-        return self._exc
+        out = self._wait(timeout)
+        return out if isinstance(out, BaseException) else None
 
     # completion side (the service's completion thread; waiters are woken by _Sub.notify)
     def set_result(self, value):
-        self._value = value
-        self._done = True
+        self._out = value
 
     def set_exception(self, exc):
-        self._exc = exc
-        self._done = True
+        self._out = exc
 
 
 class _Sub(object):
@@ -475,21 +473,30 @@ class PowService(object):
         group = _Group()
         out = []
         clamp, ihb = proofofwork._clamp_target, proofofwork._ih_bytes
+        top = _lib.U64_MAX
         objects = list(objects)
         for lo in range(0, len(objects), self.SUBMIT_SLICE):
-            futs, ihs, tgs = [], [], []
-            for target, initialHash in objects[lo:lo + self.SUBMIT_SLICE]:
-                fut = BatchResult(group)
-                out.append(fut)
+            chunk = objects[lo:lo + self.SUBMIT_SLICE]
+            futs = [BatchResult(group) for _ in chunk]
+            out.extend(futs)
+            # the common case in one pass per field: 64-byte hashes and in-range int targets
+            tgs = [t for t, _ in chunk]
+            ihs = [ih for _, ih in chunk]
+            if all(type(t) is int and 0 <= t < top for t in tgs) and \
+                    all(type(ih) is bytes and len(ih) == 64 for ih in ihs):
+                self._enqueue(_Sub(b''.join(ihs), tgs, futs, group))
+                continue
+            kf, kih, kt = [], [], []
+            for fut, (target, initialHash) in zip(futs, chunk):
                 t, ok = clamp(target)
                 if not ok:
                     fut.set_exception(ValueError('negative target: no nonce can satisfy it'))
                     continue
-                futs.append(fut)
-                ihs.append(ihb(initialHash))
-                tgs.append(t)
-            if futs:
-                self._enqueue(_Sub(b''.join(ihs), tgs, futs, group))
+                kf.append(fut)
+                kih.append(ihb(initialHash))
+                kt.append(t)
+            if kf:
+                self._enqueue(_Sub(b''.join(kih), kt, kf, group))
         return out
 
     def _enqueue(self, sub):
@@ -592,7 +599,10 @@ class PowService(object):
                         continue
                     if d == _lib.DONE_FOUND:  # re-checked on the host by the library (SERVICE_VERIFY)
                         self.solved += 1
-                        fut.set_result([tv, nn])
+                        if sub.group is not None:  # a BatchResult: its field, without the call
+                            fut._out = [tv, nn]
+                        else:
+                            fut.set_result([tv, nn])
                     elif d == _lib.DONE_BADHASH:
                         fut.set_exception(_lib.BmpowError(_lib.E_HIP, 'GPU answer (nonce %d) failed the host re-check'
                                                           % nn))

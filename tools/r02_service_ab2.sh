@@ -1,5 +1,5 @@
 #!/bin/bash
-# PowService A/B: the in-tree worker.py (array-backed results) against the previous one
+# PowService A/B: in-tree worker.py (new) against variants/oldsvc (old: a copy of bench.py and the package, here with another SUBMIT_SLICE)
 # (variants/oldsvc: a copy of bench.py and the package with the old worker.py), C5 test mode 100k.
 set -euo pipefail
 OUT=gpurun_out/r02_svc2; mkdir -p $OUT
