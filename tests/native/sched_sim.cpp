@@ -465,6 +465,45 @@ static void scenario_verify() {
   }
 }
 
+// ---- scenario 5b: concurrent padding: several callers at once share (or fall back from) the
+// persistent workers of parallel_for, each into its own staging, every byte checked ----
+static void scenario_verify_concurrent() {
+  std::mt19937_64 rng(9);
+  std::vector<std::vector<uint8_t>> bufs;
+  for (int r = 0; r < 4000; ++r) {
+    std::vector<uint8_t> v(8 + rng() % 6000);
+    for (auto& c : v) c = (uint8_t)rng();
+    bufs.push_back(std::move(v));
+  }
+  std::vector<Span> spans;
+  for (auto& v : bufs) spans.push_back({v.data(), v.size()});
+  std::vector<std::thread> th;
+  std::atomic<int> bad{0};
+  for (int t = 0; t < 4; ++t)
+    th.emplace_back([&, t] {
+      for (int rep = 0; rep < 3; ++rep) {
+        std::vector<VPart> parts;
+        uint64_t total = 0;
+        if (plan_verify(spans, 1 + (size_t)t % 2, parts, total) != 0) {
+          bad++;
+          return;
+        }
+        for (VPart& pt : parts) {
+          std::vector<uint8_t> pool(pt.blocks * 128 + 16, 0xEE);
+          pad_range(spans, pt, 0, pt.orig.size(), 0, pool.data());
+          for (size_t j = 0; j < pt.orig.size(); ++j) {
+            const Span& sp = spans[pt.orig[j]];
+            const uint64_t m = sp.len - 8;
+            const uint8_t* got = pool.data() + (uint64_t)pt.ho[j].blk * 128;
+            if (memcmp(got, sp.p + 8, m) != 0 || got[m] != 0x80 || pt.ho[j].nonce != load_be64(sp.p)) bad++;
+          }
+        }
+      }
+    });
+  for (auto& x : th) x.join();
+  CHECK(bad.load() == 0, "concurrent padding: %d mismatches", bad.load());
+}
+
 // ---- scenario 6: the library's continuous-batching service (bmpow_service_*) over the stand-in ----
 static void scenario_service() {
   std::mutex gmu;  // the library's g_mu: every op takes it
@@ -616,6 +655,7 @@ int main() {
   scenario_session();
   scenario_min_trial();
   scenario_verify();
+  scenario_verify_concurrent();
   scenario_service();
   if (g_fail) {
     fprintf(stderr, "%d check(s) failed\n", g_fail);
