@@ -81,6 +81,7 @@ def pow_objects(objects, step_trials=0, on_done=None):
         raise RuntimeError('No active exception to reraise')  # run()'s bare raise, proofofwork.py:291-292
     out = [None] * len(objs)
     t0 = time.time()
+    trials0 = _trials_hashed()
     try:
         for i, tv, nonce in proofofwork.iter_batch([(o.target, o.initial_hash) for o in objs], step_trials):
             out[i] = pack('>Q', nonce) + objs[i].payload
@@ -90,7 +91,34 @@ def pow_objects(objects, step_trials=0, on_done=None):
                 on_done(i, tv, nonce)
     except proofofwork.PowInterrupted:
         raise StopIteration('Interrupted')
+    trials1 = _trials_hashed()
+    _log_batch(len(objs), time.time() - t0, None if trials0 is None or trials1 is None else trials1 - trials0)
     return out
+
+
+def _trials_hashed():
+    """Trials the library's kernels have hashed so far (every device; bmpow_get_stats), or None
+    when no statistics are available (a test double of the library)."""
+    try:
+        lib = _lib.get()
+        st = _lib.BmpowStats()
+        lib.bmpow_get_stats(ctypes.byref(st))
+        return st.trials
+    except (_lib.BmpowError, AttributeError):
+        return None
+
+
+def _log_batch(n, seconds, trials):
+    """The batch's line in the reference's log (``_doPOWDefaults`` logs "PoW took %.1f seconds, speed
+    %s", ``class_singleWorker.py:234-246``, with nonce / time as the rate): here the trials the
+    devices actually hashed, objects/s and the device count."""
+    seconds = max(seconds, 1e-9)
+    if trials is None:
+        logger.info('PoW batch of %d objects took %.1f seconds, %.1f objects/s', n, seconds, n / seconds)
+        return
+    logger.info('PoW batch of %d objects took %.1f seconds, speed %.3f GH/s (%d trials hashed), '
+                '%.1f objects/s on %d device shard(s)', n, seconds, trials / seconds / 1e9, trials,
+                n / seconds, proofofwork._device_count())
 
 
 def pow_payload(payload, ttl, step_trials=0):

@@ -251,12 +251,15 @@ def test_create_packet_layout():
     assert ck == hashlib.sha512(b'abc').digest()[:4] and p[24:] == b'abc'
 
 
-def test_pow_objects_order_and_bytes(oracle_batch, coracle, golden):
+def test_pow_objects_order_and_bytes(oracle_batch, coracle, golden, caplog):
     kats = golden('batch_kats.json')
     rng = random.Random(kats['seed'])
     objs = [worker.PowObject(rng.randbytes(k['L']), kats['ttl'], kats['ntpb'], kats['extra']) for k in kats['kats']]
     seen = []
-    out = worker.pow_objects(objs, on_done=lambda i, tv, n: seen.append(i))
+    with caplog.at_level('INFO', logger='default'):
+        out = worker.pow_objects(objs, on_done=lambda i, tv, n: seen.append(i))
+    # the batch's line in the log (per-batch rate; here without device statistics)
+    assert any(r.getMessage().startswith('PoW batch of %d objects took' % len(objs)) for r in caplog.records)
     assert oracle_batch == [len(objs)]  # one batch for all objects
     for o, k, fin in zip(objs, kats['kats'], out):
         assert o.initial_hash.hex() == k['ih'] and int(o.target) == k['target']
