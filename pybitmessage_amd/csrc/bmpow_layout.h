@@ -12,7 +12,9 @@
 #define BM_ITERS 32
 #endif
 #define BM_ITERS_SMALL 4
-#define BM_BLOCK 256
+#ifndef BM_BLOCK
+#define BM_BLOCK 256  // lanes per search workgroup (A/B builds may override it)
+#endif
 #define BM_CHUNK ((uint64_t)BM_BLOCK * BM_ITERS)
 
 // Per-object record, device resident for the life of a batch (128 B, one per object).
