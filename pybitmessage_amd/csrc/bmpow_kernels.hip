@@ -57,6 +57,9 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
   unsigned long long* bestp = best + it.obj;
   if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < first) return;
 
+#ifdef BM_PRIO_MOD
+  if (b % BM_PRIO_MOD == 0) __builtin_amdgcn_s_setprio(2);  // A/B knob: a share of the waves issue first
+#endif
 #ifdef BM_STAGGER
   for (uint32_t z = 0; z < (b & 3); ++z) __builtin_amdgcn_s_sleep(BM_STAGGER);  // A/B knob: de-phase the waves sharing a SIMD
 #endif
