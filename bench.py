@@ -31,6 +31,7 @@ import os
 import random
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -268,10 +269,19 @@ def run_service_bench(args, dist):
 
     def once():
         svc = worker.PowService().start()
+        stop = threading.Event()
+
+        def progress():  # a line every 30 s, so a long run (C5 at full size) shows it is alive
+            while not stop.wait(30):
+                print('bench: service: %d of %d objects solved' % (svc.solved, len(objs)), file=sys.stderr, flush=True)
+        th = threading.Thread(target=progress, daemon=True)
+        th.start()
         try:
             futs = svc.submit_many(objs)
             return [f.result() for f in futs]
         finally:
+            stop.set()
+            th.join()
             svc.stop(30)
     for _ in range(args.warmup):
         once()
