@@ -193,9 +193,35 @@ BM_DEV void round_step(uint64_t (&s)[8], uint64_t (&w)[16]) {
     // are summed first and hoisted out of the nonce loop by LICM
     w[T & 15] = (w[(T - 7) & 15] + sig0<kU0>(w[(T - 15) & 15]) + w[(T - 16) & 15]) + sig1<kU1>(w[(T - 2) & 15]);
   }
+#ifdef BM_GROUP_BITOP3
+  // A/B variant: the round's eight 3-input ops (Sigma1 / Sigma0 XOR3, Ch, Maj on both halves) issue
+  // back to back, so waves sharing a SIMD meet at them together more often (they co-issue only
+  // with each other); rotates and adds stay the compiler's.
+  const uint64_t e = s[E], a = s[A];
+  const uint64_t r14 = rotr<14>(e), r18 = rotr<18>(e), r41 = rotr<41>(e);
+  const uint64_t r28 = rotr<28>(a), r34 = rotr<34>(a), r39 = rotr<39>(a);
+  uint32_t s1l, s1h, s0l, s0h, chl, chh, mjl, mjh;
+  asm("v_bitop3_b32 %0, %8, %9, %10 bitop3:0x96\n\t"
+      "v_bitop3_b32 %1, %11, %12, %13 bitop3:0x96\n\t"
+      "v_bitop3_b32 %2, %14, %15, %16 bitop3:0x96\n\t"
+      "v_bitop3_b32 %3, %17, %18, %19 bitop3:0x96\n\t"
+      "v_bitop3_b32 %4, %20, %21, %22 bitop3:0xca\n\t"
+      "v_bitop3_b32 %5, %23, %24, %25 bitop3:0xca\n\t"
+      "v_bitop3_b32 %6, %26, %27, %28 bitop3:0xe8\n\t"
+      "v_bitop3_b32 %7, %29, %30, %31 bitop3:0xe8"
+      : "=&v"(s1l), "=&v"(s1h), "=&v"(s0l), "=&v"(s0h), "=&v"(chl), "=&v"(chh), "=&v"(mjl), "=&v"(mjh)
+      : "v"(lo32(r14)), "v"(lo32(r18)), "v"(lo32(r41)), "v"(hi32(r14)), "v"(hi32(r18)), "v"(hi32(r41)),
+        "v"(lo32(r28)), "v"(lo32(r34)), "v"(lo32(r39)), "v"(hi32(r28)), "v"(hi32(r34)), "v"(hi32(r39)),
+        "v"(lo32(e)), "v"(lo32(s[F])), "v"(lo32(s[G])), "v"(hi32(e)), "v"(hi32(s[F])), "v"(hi32(s[G])),
+        "v"(lo32(a)), "v"(lo32(s[B])), "v"(lo32(s[C])), "v"(hi32(a)), "v"(hi32(s[B])), "v"(hi32(s[C])));
+  const uint64_t t1 = add64(add64(add64(s[H], opaque(mk64(s1l, s1h))), opaque(mk64(chl, chh))), K(T) + w[T & 15]);
+  s[D] = add64(s[D], t1);
+  s[H] = add64(add64(t1, opaque(mk64(s0l, s0h))), opaque(mk64(mjl, mjh)));
+#else
   const uint64_t t1 = add64(add64(add64(s[H], Sig1(s[E])), Ch(s[E], s[F], s[G])), K(T) + w[T & 15]);
   s[D] = add64(s[D], t1);
   s[H] = add64(add64(t1, Sig0(s[A])), Maj(s[A], s[B], s[C]));
+#endif
 }
 
 template <int T, int END, bool kTrial1 = false>
