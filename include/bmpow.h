@@ -65,8 +65,13 @@ BMPOW_API int bmpow_device_count(void);
 
 /* Use exactly these device ordinals for subsequent searches (n >= 1).  A device may be
  * listed more than once: each entry is a separate nonce shard with its own stream.
- * n == 0 selects every visible device.  Returns the number of shards or < 0. */
+ * n == 0 selects every visible device; ids == NULL with n >= 1 the first n visible devices.
+ * Returns the number of shards or < 0. */
 BMPOW_API int bmpow_set_devices(const int *ids, int n);
+
+/* SURVEY 8(b)'s `int bmpow_set_devices(int ndev)` form: the first ndev visible gfx950 devices
+ * (1/2/4/8-GPU runs).  Same as bmpow_set_devices(NULL, ndev).  Returns the shard count or < 0. */
+BMPOW_API int bmpow_set_device_count(int ndev);
 
 /* Copy the active shard -> device map into ids[0..cap); returns the shard count. */
 BMPOW_API int bmpow_get_devices(int *ids, int cap);
@@ -86,9 +91,21 @@ BMPOW_API void bmpow_clear_abort(void);
 
 /* ---- the hot path ---- */
 
+/* initialHash length.  Every caller in the reference passes a 64-byte sha512 digest
+ * (src/class_singleWorker.py:233, src/api.py:1300), the layout the search kernel is specialised for;
+ * the reference's _doSafePoW hashes pack('>Q', nonce) + initialHash as given, at any length
+ * (src/proofofwork.py:104-107), so the *_len / *_var entry points take any length up to
+ * BMPOW_MAX_IH_LEN bytes (a separate kernel, bm_search_var_kernel) with the same semantics. */
+#ifndef BMPOW_MAX_IH_LEN
+#define BMPOW_MAX_IH_LEN (1u << 20)
+#endif
+
 /* trial(nonces[i], ih) for i < n, computed on the first shard's device.
  * Parity probe for the trial function (reference src/proofofwork.py:106-107). */
 BMPOW_API int bmpow_trials(const uint8_t ih[64], const uint64_t *nonces, size_t n, uint64_t *trials_out);
+/* The same for an initialHash of ih_len bytes (any length <= BMPOW_MAX_IH_LEN). */
+BMPOW_API int bmpow_trials_len(const uint8_t *ih, size_t ih_len, const uint64_t *nonces, size_t n,
+                               uint64_t *trials_out);
 
 /* Bounded single-object search of [start, start + max_trials) (never past 2^64-1), nonce
  * space sharded over the active devices.  Replaces BitmessagePOW
@@ -96,6 +113,10 @@ BMPOW_API int bmpow_trials(const uint8_t ih[64], const uint64_t *nonces, size_t 
  * Returns BMPOW_FOUND with the exact first hit, BMPOW_NOT_FOUND, or < 0. */
 BMPOW_API int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials,
                  uint64_t *nonce_out, uint64_t *trial_out);
+/* The same for an initialHash of ih_len bytes: _doSafePoW's answer for pack('>Q', n) + ih as given
+ * (src/proofofwork.py:100-111) -- run(target, initialHash) for any initialHash. */
+BMPOW_API int bmpow_search_len(const uint8_t *ih, size_t ih_len, uint64_t target, uint64_t start,
+                               uint64_t max_trials, uint64_t *nonce_out, uint64_t *trial_out);
 
 /* Bounded batch search: n objects (ihs: n x 64 bytes, targets: n), each resuming at
  * next_start[i] (in/out).  Spends about `budget` trials in total, then returns the number
@@ -117,6 +138,10 @@ BMPOW_API int bmpow_min_trial(const uint8_t ih[64], uint64_t start, uint64_t cou
 /* The same for n objects (ihs: n x 64 bytes) with their own ranges, in one pass over the devices. */
 BMPOW_API int bmpow_min_trial_batch(size_t n, const uint8_t *ihs, const uint64_t *start, const uint64_t *count,
                                     uint64_t *min_out, uint64_t *argmin_out);
+/* The same for initialHashes of any length: object i is ihs[ih_off[i] .. ih_off[i+1]) (n + 1
+ * ascending offsets). */
+BMPOW_API int bmpow_min_trial_var(size_t n, const uint8_t *ihs, const uint64_t *ih_off, const uint64_t *start,
+                                  const uint64_t *count, uint64_t *min_out, uint64_t *argmin_out);
 
 /* ---- device-resident batch session (the object table stays in HBM across steps) ---- */
 typedef struct bmpow_batch bmpow_batch;
@@ -150,6 +175,9 @@ BMPOW_API int bmpow_batch_set_pending(bmpow_batch *b, size_t first, size_t count
  * producers join at any step boundary without a re-upload of the table.) */
 BMPOW_API int bmpow_batch_add(bmpow_batch *b, size_t n, const uint8_t *ihs, const uint64_t *targets,
                               const uint64_t *start, uint32_t *slot_out);
+/* bmpow_batch_add for initialHashes of any length (object i = ihs[ih_off[i] .. ih_off[i+1])). */
+BMPOW_API int bmpow_batch_add_var(bmpow_batch *b, size_t n, const uint8_t *ihs, const uint64_t *ih_off,
+                                  const uint64_t *targets, const uint64_t *start, uint32_t *slot_out);
 
 /* Pop up to `cap` objects finished (FOUND or EXHAUSTED) since the last call, in the order the
  * steps finished them: slot, nonce, trial, done state (any output but slot_out may be NULL).
@@ -178,6 +206,9 @@ BMPOW_API bmpow_service *bmpow_service_create(uint64_t step_budget, uint32_t fla
  * service's life).  Returns 0 or < 0. */
 BMPOW_API int bmpow_service_submit(bmpow_service *s, size_t n, const uint8_t *ihs, const uint64_t *targets,
                                    uint64_t *tickets_out);
+/* bmpow_service_submit for initialHashes of any length (object i = ihs[ih_off[i] .. ih_off[i+1])). */
+BMPOW_API int bmpow_service_submit_var(bmpow_service *s, size_t n, const uint8_t *ihs, const uint64_t *ih_off,
+                                       const uint64_t *targets, uint64_t *tickets_out);
 
 /* Pop up to cap finished objects (ticket, nonce, trial, BMPOW_DONE_FOUND or BMPOW_DONE_EXHAUSTED),
  * waiting up to timeout_ms (< 0: forever) for the first.  Returns the count (0 on timeout), or the

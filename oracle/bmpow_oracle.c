@@ -22,6 +22,7 @@
 #include <pthread.h>
 #include <stdint.h>
 #include <stddef.h>
+#include <stdlib.h>
 #include <string.h>
 
 static const uint64_t K512[80] = {
@@ -45,6 +46,9 @@ static const uint64_t K512[80] = {
     0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
     0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
     0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+/* the table itself, for the scheduler simulator's CPU stand-in (tests/native/sched_sim.cpp) */
+const uint64_t *bmo_k512(void) { return K512; }
 
 static const uint64_t IV512[8] = {
     0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL, 0xa54ff53a5f1d36f1ULL,
@@ -126,6 +130,34 @@ uint64_t bmo_trial(const uint8_t ih[64], uint64_t nonce) {
     memcpy(h, IV512, sizeof h);
     compress(h, blk);
     return h[0];
+}
+
+/* trial(n, ih) for an initialHash of any length: the reference hashes pack('>Q', n) + ih as given
+ * (src/proofofwork.py:104-107), so the first hash is the general SHA-512 of 8 + len bytes. */
+uint64_t bmo_trial_len(const uint8_t *ih, size_t len, uint64_t nonce) {
+    uint8_t stackbuf[8 + 256], *msg = stackbuf, h1[64], h2[64];
+    if (len > 256) {
+        msg = (uint8_t *)malloc(8 + len);
+        if (!msg) return 0;
+    }
+    store_be64(msg, nonce);
+    if (len) memcpy(msg + 8, ih, len);
+    bmo_sha512(msg, 8 + len, h1);
+    bmo_sha512(h1, 64, h2);
+    if (msg != stackbuf) free(msg);
+    return load_be64(h2);
+}
+
+/* _doSafePoW over an initialHash of any length, with a budget (as bmo_search). */
+int bmo_search_len(const uint8_t *ih, size_t len, uint64_t target, uint64_t start, uint64_t max_trials,
+                   uint64_t *nonce_out, uint64_t *trial_out) {
+    for (uint64_t i = 0; i < max_trials; i++) {
+        uint64_t n = start + i;
+        uint64_t tv = bmo_trial_len(ih, len, n);
+        if (tv <= target) { *nonce_out = n; *trial_out = tv; return 1; }
+        if (n == UINT64_MAX) break;
+    }
+    return 0;
 }
 
 void bmo_trials(const uint8_t ih[64], const uint64_t *nonces, size_t n, uint64_t *out) {

@@ -70,6 +70,10 @@ class COracle(object):
         lib.bmo_sha512.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p]
         lib.bmo_min_trial.restype = ctypes.c_int
         lib.bmo_min_trial.argtypes = [ctypes.c_char_p, u64, u64, p64, p64]
+        lib.bmo_trial_len.restype = u64
+        lib.bmo_trial_len.argtypes = [ctypes.c_char_p, ctypes.c_size_t, u64]
+        lib.bmo_search_len.restype = ctypes.c_int
+        lib.bmo_search_len.argtypes = [ctypes.c_char_p, ctypes.c_size_t, u64, u64, u64, p64, p64]
 
     def sha512(self, data):
         out = ctypes.create_string_buffer(64)
@@ -78,6 +82,18 @@ class COracle(object):
 
     def trial(self, nonce, ih):
         return self.lib.bmo_trial(ih, nonce)
+
+    def trial_len(self, nonce, ih):
+        """trial for an initialHash of any length (the reference hashes it as given)."""
+        return self.lib.bmo_trial_len(ih, len(ih), nonce)
+
+    def search_len(self, ih, target, start=1, max_trials=U64_MAX):
+        """Sequential exact search for an initialHash of any length; (trialValue, nonce) or None."""
+        n, t = ctypes.c_uint64(), ctypes.c_uint64()
+        if self.lib.bmo_search_len(ih, len(ih), min(target, U64_MAX), start, max_trials, ctypes.byref(n),
+                                   ctypes.byref(t)):
+            return t.value, n.value
+        return None
 
     def trials(self, ih, nonces):
         import numpy as np

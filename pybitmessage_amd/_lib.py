@@ -29,6 +29,7 @@ DONE_BADHASH = 5
 SERVICE_VERIFY = 1
 
 U64_MAX = (1 << 64) - 1
+MAX_IH_LEN = 1 << 20  # BMPOW_MAX_IH_LEN: longest initialHash the library accepts
 
 
 class BmpowError(RuntimeError):
@@ -70,6 +71,7 @@ SIGNATURES = [
     ('bmpow_init', ctypes.c_int, []),
     ('bmpow_device_count', ctypes.c_int, []),
     ('bmpow_set_devices', ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ('bmpow_set_device_count', ctypes.c_int, [ctypes.c_int]),
     ('bmpow_get_devices', ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ('bmpow_shutdown', None, []),
     ('bmpow_last_error', ctypes.c_char_p, []),
@@ -77,9 +79,12 @@ SIGNATURES = [
     ('bmpow_abort', None, []),
     ('bmpow_clear_abort', None, []),
     ('bmpow_trials', ctypes.c_int, [ctypes.c_char_p, _p64, ctypes.c_size_t, _p64]),
+    ('bmpow_trials_len', ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, _p64, ctypes.c_size_t, _p64]),
     ('bmpow_search', ctypes.c_int, [ctypes.c_char_p, _u64, _u64, _u64, _p64, _p64]),
+    ('bmpow_search_len', ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, _u64, _u64, _u64, _p64, _p64]),
     ('bmpow_min_trial', ctypes.c_int, [ctypes.c_char_p, _u64, _u64, _p64, _p64]),
     ('bmpow_min_trial_batch', ctypes.c_int, [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _p64, _p64]),
+    ('bmpow_min_trial_var', ctypes.c_int, [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _p64, _p64, _p64]),
     ('bmpow_search_batch', ctypes.c_int,
      [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _u64, _p64, _p64, _pu8]),
     ('bmpow_batch_create', _vp, [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64]),
@@ -88,10 +93,12 @@ SIGNATURES = [
     ('bmpow_batch_reset', ctypes.c_int, [_vp, _p64]),
     ('bmpow_batch_set_pending', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int]),
     ('bmpow_batch_add', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _pu32]),
+    ('bmpow_batch_add_var', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _p64, _pu32]),
     ('bmpow_batch_take_done', ctypes.c_int, [_vp, ctypes.c_size_t, _pu32, _p64, _p64, _pu8]),
     ('bmpow_batch_destroy', None, [_vp]),
     ('bmpow_service_create', _vp, [_u64, ctypes.c_uint32]),
     ('bmpow_service_submit', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_char_p, _p64, _p64]),
+    ('bmpow_service_submit_var', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_char_p, _p64, _p64, _p64]),
     ('bmpow_service_poll', ctypes.c_int, [_vp, ctypes.c_size_t, ctypes.c_int, _p64, _p64, _p64, _pu8]),
     ('bmpow_service_cancel', ctypes.c_int, [_vp]),
     ('bmpow_service_outstanding', ctypes.c_int, [_vp]),

@@ -68,8 +68,9 @@ struct Shard {
   bm_result* h_res = nullptr;      // pinned
   unsigned long long* h_trials = nullptr;  // pinned
   size_t item_cap = 0;
-  // step bookkeeping
-  uint32_t nitems = 0, nchunks = 0;
+  // step bookkeeping: items [0, nmain) / chunks [0, chmain) are 64-byte objects (bm_search_kernel),
+  // the rest var-form objects (bm_search_var_kernel)
+  uint32_t nitems = 0, nchunks = 0, nmain = 0, chmain = 0;
   // min-trial probe: one bm_minpart per workgroup of a launch (grow-only)
   bm_minpart* d_parts = nullptr;
   bm_minpart* h_parts = nullptr;  // pinned
@@ -231,8 +232,12 @@ struct bmpow_batch : bmsched::BatchState {
     bm_obj* d_obj = nullptr;
     unsigned long long* d_best = nullptr;  // running minimum hit nonce (valid where d_found)
     uint32_t* d_found = nullptr;           // 1 once the object has a hit on this shard
+    uint64_t* d_vpool = nullptr;           // copy of vpool (var-form objects' words), vcap words
   };
   std::vector<Dev> dev;  // one per shard (indexed like g_shards)
+  size_t vcap = 0;         // words allocated per shard for the var pool
+  size_t vsynced = 0;      // vpool words already on the devices (of epoch vepoch)
+  uint64_t vepoch = ~0ULL;
 };
 
 namespace {
@@ -243,8 +248,45 @@ void batch_free_dev(bmpow_batch* b) {
     if (b->dev[s].d_obj) (void)hipFree(b->dev[s].d_obj);
     if (b->dev[s].d_best) (void)hipFree(b->dev[s].d_best);
     if (b->dev[s].d_found) (void)hipFree(b->dev[s].d_found);
+    if (b->dev[s].d_vpool) (void)hipFree(b->dev[s].d_vpool);
   }
   b->dev.clear();
+  b->vcap = 0;
+  b->vsynced = 0;
+  b->vepoch = ~0ULL;
+}
+
+// Bring the devices' copy of the var pool up to date: the words appended since the last sync (one
+// copy per shard), or all of them after a reallocation or a new epoch (bmsched::add emptied it).
+// Stream-ordered before the next launch on each shard.
+int sync_vpool(bmpow_batch* b) {
+  const size_t n = b->vpool.size();
+  if (b->vepoch != b->vpool_epoch) {
+    b->vsynced = 0;
+    b->vepoch = b->vpool_epoch;
+  }
+  if (n == b->vsynced) return 0;
+  const bool grow = n > b->vcap;
+  const size_t cap = grow ? std::max<size_t>(n, 2 * b->vcap) : b->vcap;
+  const size_t from = grow ? 0 : b->vsynced;
+  for (size_t s = 0; s < g_shards.size(); ++s) {
+    Shard& sh = g_shards[s];
+    HIPTRY(hipSetDevice(sh.dev));
+    if (grow) {
+      if (b->dev[s].d_vpool) {
+        HIPTRY(hipStreamSynchronize(sh.stream));  // no launch may still read the old copy
+        HIPTRY(hipFree(b->dev[s].d_vpool));
+        b->dev[s].d_vpool = nullptr;
+      }
+      HIPTRY(hipMalloc(&b->dev[s].d_vpool, cap * sizeof(uint64_t)));
+    }
+    // the host vector may be appended to before the copy runs: stage through a synchronous copy
+    HIPTRY(hipMemcpy(b->dev[s].d_vpool + from, b->vpool.data() + from, (n - from) * sizeof(uint64_t),
+                     hipMemcpyHostToDevice));
+  }
+  b->vcap = cap;
+  b->vsynced = n;
+  return 0;
 }
 
 int batch_upload(bmpow_batch* b) {
@@ -268,11 +310,12 @@ int batch_upload(bmpow_batch* b) {
     HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(hipStreamSynchronize(sh.stream));
   }
-  return 0;
+  return sync_vpool(b);
 }
 
-int batch_init(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
-  bmsched::init(*b, n, ihs, targets, start);
+int batch_init(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
+               const uint64_t* ih_off = nullptr) {
+  bmsched::init(*b, n, ihs, targets, start, ih_off);
   return batch_upload(b);
 }
 
@@ -282,12 +325,12 @@ int batch_init(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* tar
 // Resetting best[] and found[] over those runs is safe between steps: a pending object's device
 // state is always (UINT64_MAX, 0) there, since a hit finishes its object in the step that finds it.
 int batch_add_locked(bmpow_batch* b, size_t m, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
-                     uint32_t* slot_out) {
+                     uint32_t* slot_out, const uint64_t* ih_off = nullptr) {
   if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
   const size_t fresh = m > b->free_slots.size() ? m - b->free_slots.size() : 0;
   if (b->n + fresh > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many objects");
   std::vector<uint32_t> slots;
-  const bool grew = bmsched::add(*b, m, ihs, targets, start, slots);
+  const bool grew = bmsched::add(*b, m, ihs, targets, start, slots, ih_off);
   if (slot_out) std::copy(slots.begin(), slots.end(), slot_out);
   if (grew) {
     b->cap = std::max<size_t>({b->n, 2 * b->cap, 1024});
@@ -313,7 +356,7 @@ int batch_add_locked(bmpow_batch* b, size_t m, const uint8_t* ihs, const uint64_
     HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(hipStreamSynchronize(sh.stream));
   }
-  return 0;
+  return sync_vpool(b);
 }
 
 // Stage the plan's per-shard item lists in the shards' pinned buffers (sized once per step, so
@@ -328,6 +371,8 @@ int stage_items(const bmsched::StepPlan& p) {
     if (!items.empty()) std::memcpy(sh.h_items, items.data(), items.size() * sizeof(bm_item));
     sh.nitems = (uint32_t)items.size();
     sh.nchunks = p.nchunks[s];
+    sh.nmain = p.nmain.empty() ? sh.nitems : p.nmain[s];
+    sh.chmain = p.chmain.empty() ? sh.nchunks : p.chmain[s];
   }
   return 0;
 }
@@ -343,7 +388,8 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
   if (!bmsched::plan_step(*b, budget, g_step_trials, S, plan)) return 0;
   const uint32_t iters = plan.iters;
   {
-    const int rc = stage_items(plan);
+    int rc = stage_items(plan);
+    if (rc == 0) rc = sync_vpool(b);
     if (rc < 0) return rc;
   }
 
@@ -355,11 +401,16 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     HIPTRY(hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream));
     HIPTRY(hipMemsetAsync(sh.d_trials, 0, sizeof(unsigned long long), sh.stream));
     HIPTRY(hipEventRecord(sh.ev0, sh.stream));
-    HIPTRY(bm_launch_search(sh.stream, sh.nchunks, iters, b->dev[s].d_obj, sh.d_items, sh.nitems,
-                            b->dev[s].d_best, b->dev[s].d_found, sh.d_trials));
+    if (sh.nmain)
+      HIPTRY(bm_launch_search(sh.stream, sh.chmain, iters, b->dev[s].d_obj, sh.d_items, sh.nmain,
+                              b->dev[s].d_best, b->dev[s].d_found, sh.d_trials));
+    if (sh.nitems > sh.nmain)
+      HIPTRY(bm_launch_search_var(sh.stream, sh.nchunks - sh.chmain, iters, b->dev[s].d_obj, sh.d_items + sh.nmain,
+                                  sh.nitems - sh.nmain, b->dev[s].d_best, b->dev[s].d_found, sh.d_trials,
+                                  b->dev[s].d_vpool));
     HIPTRY(hipEventRecord(sh.ev1, sh.stream));
     HIPTRY(bm_launch_resolve(sh.stream, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best,
-                             b->dev[s].d_found, sh.d_res));
+                             b->dev[s].d_found, sh.d_res, b->dev[s].d_vpool));
     HIPTRY(hipMemcpyAsync(sh.h_res, sh.d_res, sh.nitems * sizeof(bm_result), hipMemcpyDeviceToHost, sh.stream));
     HIPTRY(hipMemcpyAsync(sh.h_trials, sh.d_trials, sizeof(unsigned long long), hipMemcpyDeviceToHost, sh.stream));
   }
@@ -413,20 +464,26 @@ int ensure_parts(Shard& s, size_t n) {
 // like a search step, and each workgroup's (trial, nonce) minimum is reduced here,
 // lexicographically, so ties keep the smaller nonce.
 int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const uint64_t* count, uint64_t* min_out,
-                     uint64_t* argmin_out) {
+                     uint64_t* argmin_out, const uint64_t* ih_off = nullptr) {
   if (n > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many objects");
   const size_t S = g_shards.size();
   std::vector<bm_obj> objs(n);
-  for (size_t i = 0; i < n; ++i) pack_obj(ihs + 64 * i, 0, &objs[i]);
+  std::vector<uint64_t> vpool;
+  bool any_var = false;
+  for (size_t i = 0; i < n; ++i) {
+    bmsched::pack_var(bmsched::ih_ptr(ihs, ih_off, i), bmsched::ih_len(ih_off, i), 0, &objs[i], vpool);
+    any_var = any_var || objs[i].ihlen != BM_IH_MAIN;
+  }
   bmsched::MinTrial mt;
   mt.init(n, start, count, min_out, argmin_out);
   std::vector<bm_obj*> d_obj(S, nullptr);
+  std::vector<uint64_t*> d_vpool(S, nullptr);
   auto release = [&]() {
-    for (size_t s = 0; s < S; ++s)
-      if (d_obj[s]) {
-        (void)hipSetDevice(g_shards[s].dev);
-        (void)hipFree(d_obj[s]);
-      }
+    for (size_t s = 0; s < S; ++s) {
+      if (d_obj[s] || d_vpool[s]) (void)hipSetDevice(g_shards[s].dev);
+      if (d_obj[s]) (void)hipFree(d_obj[s]);
+      if (d_vpool[s]) (void)hipFree(d_vpool[s]);
+    }
   };
   int rc = 0;
   for (size_t s = 0; s < S && rc == 0; ++s) {
@@ -435,6 +492,9 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
     if (e == hipSuccess) e = hipMalloc(&d_obj[s], std::max<size_t>(n, 1) * sizeof(bm_obj));
     if (e == hipSuccess && n)
       e = hipMemcpyAsync(d_obj[s], objs.data(), n * sizeof(bm_obj), hipMemcpyHostToDevice, sh.stream);
+    if (e == hipSuccess && !vpool.empty()) e = hipMalloc(&d_vpool[s], vpool.size() * sizeof(uint64_t));
+    if (e == hipSuccess && !vpool.empty())
+      e = hipMemcpyAsync(d_vpool[s], vpool.data(), vpool.size() * sizeof(uint64_t), hipMemcpyHostToDevice, sh.stream);
     if (e != hipSuccess) rc = set_err(BMPOW_E_HIP, std::string("min-trial upload: ") + hipGetErrorString(e));
   }
   const uint64_t total_chunks = std::max<uint64_t>(g_step_trials * S / BM_CHUNK, S);
@@ -447,6 +507,7 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
     uint64_t C = 0;
     if (!mt.plan(total_chunks, plan.wins, C)) break;
     bmsched::slice(plan.wins, C, BM_CHUNK, S, plan);
+    bmsched::split_kinds(objs, BM_CHUNK, any_var, plan);
     rc = stage_items(plan);
     if (rc < 0) break;
     for (size_t s = 0; s < S && rc == 0; ++s) {
@@ -458,8 +519,11 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
       if (e == hipSuccess)
         e = hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream);
       if (e == hipSuccess) e = hipEventRecord(sh.ev0, sh.stream);
-      if (e == hipSuccess)
-        e = bm_launch_mintrial(sh.stream, sh.nchunks, BM_ITERS, d_obj[s], sh.d_items, sh.nitems, sh.d_parts);
+      if (e == hipSuccess && sh.nmain)
+        e = bm_launch_mintrial(sh.stream, sh.chmain, BM_ITERS, d_obj[s], sh.d_items, sh.nmain, sh.d_parts);
+      if (e == hipSuccess && sh.nitems > sh.nmain)
+        e = bm_launch_mintrial_var(sh.stream, sh.nchunks - sh.chmain, BM_ITERS, d_obj[s], sh.d_items + sh.nmain,
+                                   sh.nitems - sh.nmain, sh.d_parts + sh.chmain, d_vpool[s]);
       if (e == hipSuccess) e = hipEventRecord(sh.ev1, sh.stream);
       if (e == hipSuccess)
         e = hipMemcpyAsync(sh.h_parts, sh.d_parts, sh.nchunks * sizeof(bm_minpart), hipMemcpyDeviceToHost,
@@ -478,7 +542,11 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
         break;
       }
       g_stats.probe_kernel_ms += ms;
-      mt.reduce_parts(plan.items[s], sh.h_parts, min_out, argmin_out);
+      const std::vector<bm_item>& its = plan.items[s];
+      const std::vector<bm_item> main_items(its.begin(), its.begin() + sh.nmain),
+          var_items(its.begin() + sh.nmain, its.end());
+      mt.reduce_parts(main_items, sh.h_parts, min_out, argmin_out);
+      if (!var_items.empty()) mt.reduce_parts(var_items, sh.h_parts + sh.chmain, min_out, argmin_out);
     }
     if (rc < 0) break;
     for (const bmsched::Win& w : plan.wins) g_stats.probe_trials += w.count;
@@ -493,11 +561,14 @@ bmpow_batch* g_scratch = nullptr;
 
 // Reused while it is large enough and the device set is unchanged: a run() call (one object per
 // bounded bmpow_search) then pays one upload of its 128-B record, not three hipMalloc/hipFree pairs.
-int scratch_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
+int scratch_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
+                  const uint64_t* ih_off = nullptr) {
   if (g_scratch && g_scratch->dev.size() == g_shards.size() && g_scratch->cap >= n) {
     const size_t cap = g_scratch->cap;
-    bmsched::init(*g_scratch, n, ihs, targets, start);
+    bmsched::init(*g_scratch, n, ihs, targets, start, ih_off);
     g_scratch->cap = cap;
+    const int rc = sync_vpool(g_scratch);
+    if (rc < 0) return rc;
     for (size_t s = 0; s < g_shards.size(); ++s) {
       Shard& sh = g_shards[s];
       HIPTRY(hipSetDevice(sh.dev));
@@ -516,7 +587,7 @@ int scratch_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, const u
     g_scratch = nullptr;
   }
   g_scratch = new bmpow_batch();
-  return batch_init(g_scratch, n, ihs, targets, start);
+  return batch_init(g_scratch, n, ihs, targets, start, ih_off);
 }
 
 }  // namespace
@@ -1001,9 +1072,10 @@ namespace {
 
 bmsched::ServiceOps service_ops(bmpow_service* s) {
   bmsched::ServiceOps ops;
-  ops.add = [s](size_t n, const uint8_t* ihs, const uint64_t* tg, uint32_t* slots, std::string& err) {
+  ops.add = [s](size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* tg, uint32_t* slots,
+                std::string& err) {
     std::lock_guard<std::mutex> g(g_mu);
-    const int rc = batch_add_locked(s->b, n, ihs, tg, nullptr, slots);
+    const int rc = batch_add_locked(s->b, n, ihs, tg, nullptr, slots, ih_off);
     if (rc < 0) err = g_err;
     return rc;
   };
@@ -1045,19 +1117,32 @@ int bmpow_device_count(void) { return (int)visible_gfx950().size(); }
 
 int bmpow_set_devices(const int* ids, int n) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (n < 0 || (n > 0 && !ids)) return set_err(BMPOW_E_ARG, "bad device list");
+  if (n < 0) return set_err(BMPOW_E_ARG, "bad device list");
+  std::vector<int> v;
+  if (n == 0) {
+    v = visible_gfx950();
+  } else if (!ids) {  // the first n visible devices (int bmpow_set_devices(int ndev))
+    v = visible_gfx950();
+    if ((size_t)n > v.size())
+      return set_err(BMPOW_E_ARG, std::to_string(n) + " devices asked for, " + std::to_string(v.size()) + " visible");
+    v.resize((size_t)n);
+  } else {
+    v.assign(ids, ids + n);
+  }
   if (g_scratch) {
     batch_free_dev(g_scratch);
     delete g_scratch;
     g_scratch = nullptr;
   }
-  std::vector<int> v;
-  if (n == 0) v = visible_gfx950();
-  else v.assign(ids, ids + n);
   if (v.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
   int rc = select_devices(v);
   g_inited = rc > 0;
   return rc;
+}
+
+int bmpow_set_device_count(int ndev) {
+  if (ndev < 1) return set_err(BMPOW_E_ARG, "device count must be >= 1");
+  return bmpow_set_devices(nullptr, ndev);
 }
 
 int bmpow_get_devices(int* ids, int cap) {
@@ -1089,41 +1174,62 @@ const char* bmpow_version(void) {
 void bmpow_abort(void) { g_abort.store(1); }
 void bmpow_clear_abort(void) { g_abort.store(0); }
 
-int bmpow_trials(const uint8_t ih[64], const uint64_t* nonces, size_t n, uint64_t* trials_out) {
+int bmpow_trials_len(const uint8_t* ih, size_t ih_len, const uint64_t* nonces, size_t n, uint64_t* trials_out) {
   std::lock_guard<std::mutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
-  if (!ih || (n && (!nonces || !trials_out))) return set_err(BMPOW_E_ARG, "null pointer");
+  if ((!ih && ih_len) || (n && (!nonces || !trials_out))) return set_err(BMPOW_E_ARG, "null pointer");
+  if (ih_len > BMPOW_MAX_IH_LEN) return set_err(BMPOW_E_ARG, "initialHash longer than BMPOW_MAX_IH_LEN");
   if (n == 0) return 0;
   Shard& sh = g_shards[0];
   HIPTRY(hipSetDevice(sh.dev));
   bm_obj o;
-  pack_obj(ih, 0, &o);
+  std::vector<uint64_t> vpool;
+  const uint8_t zero = 0;
+  bmsched::pack_var(ih ? ih : &zero, ih_len, 0, &o, vpool);
   bm_obj* d_o = nullptr;
-  uint64_t *d_n = nullptr, *d_t = nullptr;
+  uint64_t *d_n = nullptr, *d_t = nullptr, *d_v = nullptr;
   HIPTRY(hipMalloc(&d_o, sizeof(bm_obj)));
   HIPTRY(hipMalloc(&d_n, n * sizeof(uint64_t)));
   HIPTRY(hipMalloc(&d_t, n * sizeof(uint64_t)));
+  if (!vpool.empty()) HIPTRY(hipMalloc(&d_v, vpool.size() * sizeof(uint64_t)));
   hipError_t e = hipMemcpyAsync(d_o, &o, sizeof o, hipMemcpyHostToDevice, sh.stream);
+  if (e == hipSuccess && d_v)
+    e = hipMemcpyAsync(d_v, vpool.data(), vpool.size() * sizeof(uint64_t), hipMemcpyHostToDevice, sh.stream);
   if (e == hipSuccess) e = hipMemcpyAsync(d_n, nonces, n * sizeof(uint64_t), hipMemcpyHostToDevice, sh.stream);
-  if (e == hipSuccess) e = bm_launch_trials(sh.stream, d_o, d_n, n, d_t);
+  if (e == hipSuccess) e = bm_launch_trials(sh.stream, d_o, d_n, n, d_t, d_v);
   if (e == hipSuccess) e = hipMemcpyAsync(trials_out, d_t, n * sizeof(uint64_t), hipMemcpyDeviceToHost, sh.stream);
   if (e == hipSuccess) e = hipStreamSynchronize(sh.stream);
   (void)hipFree(d_o);
   (void)hipFree(d_n);
   (void)hipFree(d_t);
+  if (d_v) (void)hipFree(d_v);
   if (e != hipSuccess) return set_err(BMPOW_E_HIP, std::string("bmpow_trials: ") + hipGetErrorString(e));
   return 0;
 }
 
+int bmpow_trials(const uint8_t ih[64], const uint64_t* nonces, size_t n, uint64_t* trials_out) {
+  if (!ih) return set_err(BMPOW_E_ARG, "null pointer");
+  return bmpow_trials_len(ih, 64, nonces, n, trials_out);
+}
+
 int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials,
                  uint64_t* nonce_out, uint64_t* trial_out) {
+  if (!ih) return set_err(BMPOW_E_ARG, "null pointer");
+  return bmpow_search_len(ih, 64, target, start, max_trials, nonce_out, trial_out);
+}
+
+int bmpow_search_len(const uint8_t* ih, size_t ih_len, uint64_t target, uint64_t start, uint64_t max_trials,
+                     uint64_t* nonce_out, uint64_t* trial_out) {
   std::lock_guard<std::mutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
-  if (!ih || !nonce_out || !trial_out) return set_err(BMPOW_E_ARG, "null pointer");
+  if ((!ih && ih_len) || !nonce_out || !trial_out) return set_err(BMPOW_E_ARG, "null pointer");
+  if (ih_len > BMPOW_MAX_IH_LEN) return set_err(BMPOW_E_ARG, "initialHash longer than BMPOW_MAX_IH_LEN");
   if (max_trials == 0) return BMPOW_NOT_FOUND;
-  rc = scratch_batch(1, ih, &target, &start);
+  const uint8_t zero = 0;
+  const uint64_t off[2] = {0, ih_len};
+  rc = scratch_batch(1, ih ? ih : &zero, &target, &start, ih_len == 64 ? nullptr : off);
   if (rc < 0) return rc;
   bmpow_batch* b = g_scratch;
   uint64_t left = max_trials;
@@ -1174,6 +1280,30 @@ int bmpow_min_trial_batch(size_t n, const uint8_t* ihs, const uint64_t* start, c
   if (n == 0) return 0;
   if (!ihs || !start || !count || !min_out || !argmin_out) return set_err(BMPOW_E_ARG, "null pointer");
   return min_trial_locked(n, ihs, start, count, min_out, argmin_out);
+}
+
+// shared argument check of the *_var entry points: n + 1 ascending offsets, lengths in range
+static int check_ih_offsets(size_t n, const uint8_t* ihs, const uint64_t* ih_off) {
+  if (!ih_off || (!ihs && ih_off[n] > ih_off[0])) return set_err(BMPOW_E_ARG, "null pointer");
+  for (size_t i = 0; i < n; ++i) {
+    if (ih_off[i + 1] < ih_off[i]) return set_err(BMPOW_E_ARG, "initialHash offsets are not ascending");
+    if (ih_off[i + 1] - ih_off[i] > BMPOW_MAX_IH_LEN)
+      return set_err(BMPOW_E_ARG, "initialHash longer than BMPOW_MAX_IH_LEN");
+  }
+  return 0;
+}
+
+int bmpow_min_trial_var(size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* start,
+                        const uint64_t* count, uint64_t* min_out, uint64_t* argmin_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = init_locked();
+  if (rc < 0) return rc;
+  if (n == 0) return 0;
+  if (!start || !count || !min_out || !argmin_out) return set_err(BMPOW_E_ARG, "null pointer");
+  rc = check_ih_offsets(n, ihs, ih_off);
+  if (rc < 0) return rc;
+  const uint8_t zero = 0;
+  return min_trial_locked(n, ihs ? ihs : &zero, start, count, min_out, argmin_out, ih_off);
 }
 
 int bmpow_search_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* next_start,
@@ -1290,6 +1420,20 @@ int bmpow_batch_add(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
+int bmpow_batch_add_var(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* targets,
+                        const uint64_t* start, uint32_t* slot_out) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!b) return set_err(BMPOW_E_STATE, "null batch");
+  if (n == 0) return (int)std::min<size_t>(b->pending, 0x7fffffff);
+  if (!targets) return set_err(BMPOW_E_ARG, "null pointer");
+  int rc = check_ih_offsets(n, ihs, ih_off);
+  if (rc < 0) return rc;
+  const uint8_t zero = 0;
+  rc = batch_add_locked(b, n, ihs ? ihs : &zero, targets, start, slot_out, ih_off);
+  if (rc < 0) return rc;
+  return (int)std::min<size_t>(b->pending, 0x7fffffff);
+}
+
 int bmpow_batch_take_done(bmpow_batch* b, size_t cap, uint32_t* slot_out, uint64_t* nonce_out, uint64_t* trial_out,
                           uint8_t* done_out) {
   std::lock_guard<std::mutex> lk(g_mu);
@@ -1328,6 +1472,18 @@ int bmpow_service_submit(bmpow_service* s, size_t n, const uint8_t* ihs, const u
   if (!s) return set_err(BMPOW_E_STATE, "null service");
   if (n && (!ihs || !targets)) return set_err(BMPOW_E_ARG, "null pointer");
   const int rc = s->svc->submit(n, ihs, targets, tickets_out);
+  return rc < 0 ? set_err(rc, "service stopping") : rc;
+}
+
+int bmpow_service_submit_var(bmpow_service* s, size_t n, const uint8_t* ihs, const uint64_t* ih_off,
+                             const uint64_t* targets, uint64_t* tickets_out) {
+  if (!s) return set_err(BMPOW_E_STATE, "null service");
+  if (n == 0) return 0;
+  if (!targets) return set_err(BMPOW_E_ARG, "null pointer");
+  int rc = check_ih_offsets(n, ihs, ih_off);
+  if (rc < 0) return rc;
+  const uint8_t zero = 0;
+  rc = s->svc->submit(n, ihs ? ihs : &zero, targets, tickets_out, ih_off);
   return rc < 0 ? set_err(rc, "service stopping") : rc;
 }
 

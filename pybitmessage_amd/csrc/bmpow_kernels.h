@@ -13,12 +13,19 @@ hipError_t bv_launch_pow_binned(hipStream_t st, const bv_obj* objs, uint32_t n, 
 hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
                             const bm_item* items, uint32_t nitems, unsigned long long* best, uint32_t* found,
                             unsigned long long* trials_done);
+hipError_t bm_launch_search_var(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
+                                const bm_item* items, uint32_t nitems, unsigned long long* best, uint32_t* found,
+                                unsigned long long* trials_done, const uint64_t* vpool);
+// vpool: the batch's var pool (may be null when no object of the launch is var-form)
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
-                             const unsigned long long* best, const uint32_t* found, bm_result* res);
+                             const unsigned long long* best, const uint32_t* found, bm_result* res,
+                             const uint64_t* vpool);
 hipError_t bm_launch_mintrial(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
                               const bm_item* items, uint32_t nitems, bm_minpart* parts);
+hipError_t bm_launch_mintrial_var(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
+                                  const bm_item* items, uint32_t nitems, bm_minpart* parts, const uint64_t* vpool);
 hipError_t bm_launch_trials(hipStream_t st, const bm_obj* obj, const uint64_t* nonces, uint64_t n,
-                            uint64_t* out);
+                            uint64_t* out, const uint64_t* vpool);
 
 // RIPE-prefix address search (ar_*, bmpow_addr.hip).  Parameters are uniform per search.
 struct ar_params {

@@ -18,11 +18,28 @@
 #define BM_CHUNK ((uint64_t)BM_BLOCK * BM_ITERS)
 
 // Per-object record, device resident for the life of a batch (128 B, one per object).
+//   ihlen == 64 (every caller in the reference: sha512(payload).digest()): w[] holds the
+//     initialHash, searched by bm_search_kernel;
+//   any other length: w[] is unused and the object's message words live in the batch's var pool
+//     from word vword on (16 words of block 0, then 80 K+W words per further block, nblk blocks in
+//     the first hash; bmsched::pack_var), searched by bm_search_var_kernel.
+constexpr uint32_t BM_IH_MAIN = 64;
 struct bm_obj {
-  uint64_t w[8];     // initialHash as 8 big-endian words = W1..W8 of SHA-512 block 1
+  uint64_t w[8];     // initialHash as 8 big-endian words = W1..W8 of SHA-512 block 1 (ihlen == 64)
   uint64_t target;   // accept trial <= target
-  uint64_t pad[7];
+  uint32_t ihlen;    // initialHash length in bytes
+  uint32_t nblk;     // var form: blocks of the first hash's message
+  uint64_t vword;    // var form: first word of this object in the var pool
+  uint64_t pad[5];
 };
+static_assert(sizeof(bm_obj) == 128, "bm_obj is 128 B");
+
+// Words an initialHash of len bytes (!= 64) takes in the var pool.
+inline uint64_t bm_var_blocks(uint64_t len) { return (8 + len + 17 + 127) / 128; }
+inline uint64_t bm_var_words(uint64_t len) { return 16 + 80 * (bm_var_blocks(len) - 1); }
+#ifndef BMPOW_MAX_IH_LEN  // (also in include/bmpow.h)
+#define BMPOW_MAX_IH_LEN (1u << 20)  // longest initialHash the library accepts (1 MiB)
+#endif
 
 // Work item = one object's contiguous nonce window inside one launch (32 B).
 struct bm_item {

@@ -31,17 +31,92 @@ uint64_t host_trial(const uint8_t ih[64], uint64_t nonce) {
   return load_be64(h2);
 }
 
+uint64_t host_trial_len(const uint8_t* ih, size_t len, uint64_t nonce) {
+  if (len == 64) return host_trial(ih, nonce);
+  std::vector<uint8_t> msg(8 + len);
+  for (int i = 0; i < 8; ++i) msg[i] = (uint8_t)(nonce >> (56 - 8 * i));
+  if (len) memcpy(msg.data() + 8, ih, len);
+  uint8_t h1[64], h2[64];
+  SHA512(msg.data(), msg.size(), h1);
+  SHA512(h1, sizeof h1, h2);
+  return load_be64(h2);
+}
+
 void pack_obj(const uint8_t* ih, uint64_t target, bm_obj* o) {
   std::memset(o, 0, sizeof(*o));
   for (int i = 0; i < 8; ++i) o->w[i] = load_be64(ih + 8 * i);
   o->target = target;
+  o->ihlen = BM_IH_MAIN;
+  o->nblk = 1;
+}
+
+namespace {
+
+// FIPS 180-4 4.2.3 (the K+W words of pack_var's later blocks are summed on the host)
+constexpr uint64_t kK512[80] = {
+    0x428a2f98d728ae22ULL, 0x7137449123ef65cdULL, 0xb5c0fbcfec4d3b2fULL, 0xe9b5dba58189dbbcULL,
+    0x3956c25bf348b538ULL, 0x59f111f1b605d019ULL, 0x923f82a4af194f9bULL, 0xab1c5ed5da6d8118ULL,
+    0xd807aa98a3030242ULL, 0x12835b0145706fbeULL, 0x243185be4ee4b28cULL, 0x550c7dc3d5ffb4e2ULL,
+    0x72be5d74f27b896fULL, 0x80deb1fe3b1696b1ULL, 0x9bdc06a725c71235ULL, 0xc19bf174cf692694ULL,
+    0xe49b69c19ef14ad2ULL, 0xefbe4786384f25e3ULL, 0x0fc19dc68b8cd5b5ULL, 0x240ca1cc77ac9c65ULL,
+    0x2de92c6f592b0275ULL, 0x4a7484aa6ea6e483ULL, 0x5cb0a9dcbd41fbd4ULL, 0x76f988da831153b5ULL,
+    0x983e5152ee66dfabULL, 0xa831c66d2db43210ULL, 0xb00327c898fb213fULL, 0xbf597fc7beef0ee4ULL,
+    0xc6e00bf33da88fc2ULL, 0xd5a79147930aa725ULL, 0x06ca6351e003826fULL, 0x142929670a0e6e70ULL,
+    0x27b70a8546d22ffcULL, 0x2e1b21385c26c926ULL, 0x4d2c6dfc5ac42aedULL, 0x53380d139d95b3dfULL,
+    0x650a73548baf63deULL, 0x766a0abb3c77b2a8ULL, 0x81c2c92e47edaee6ULL, 0x92722c851482353bULL,
+    0xa2bfe8a14cf10364ULL, 0xa81a664bbc423001ULL, 0xc24b8b70d0f89791ULL, 0xc76c51a30654be30ULL,
+    0xd192e819d6ef5218ULL, 0xd69906245565a910ULL, 0xf40e35855771202aULL, 0x106aa07032bbd1b8ULL,
+    0x19a4c116b8d2d0c8ULL, 0x1e376c085141ab53ULL, 0x2748774cdf8eeb99ULL, 0x34b0bcb5e19b48a8ULL,
+    0x391c0cb3c5c95a63ULL, 0x4ed8aa4ae3418acbULL, 0x5b9cca4f7763e373ULL, 0x682e6ff3d6b2b8a3ULL,
+    0x748f82ee5defb2fcULL, 0x78a5636f43172f60ULL, 0x84c87814a1f0ab72ULL, 0x8cc702081a6439ecULL,
+    0x90befffa23631e28ULL, 0xa4506cebde82bde9ULL, 0xbef9a3f7b2c67915ULL, 0xc67178f2e372532bULL,
+    0xca273eceea26619cULL, 0xd186b8c721c0c207ULL, 0xeada7dd6cde0eb1eULL, 0xf57d4f7fee6ed178ULL,
+    0x06f067aa72176fbaULL, 0x0a637dc5a2c898a6ULL, 0x113f9804bef90daeULL, 0x1b710b35131c471bULL,
+    0x28db77f523047d84ULL, 0x32caab7b40c72493ULL, 0x3c9ebe0a15c9bebcULL, 0x431d67c49c100d4cULL,
+    0x4cc5d4becb3e42b6ULL, 0x597f299cfc657e2aULL, 0x5fcb6fab3ad6faecULL, 0x6c44198c4a475817ULL};
+
+inline uint64_t ror(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+
+}  // namespace
+
+void pack_var(const uint8_t* ih, size_t len, uint64_t target, bm_obj* o, std::vector<uint64_t>& pool) {
+  if (len == BM_IH_MAIN) {
+    pack_obj(ih, target, o);
+    return;
+  }
+  std::memset(o, 0, sizeof(*o));
+  o->target = target;
+  o->ihlen = (uint32_t)len;
+  // BE64(nonce) || ih || 0x80 || zeros || BE128(bit length), the nonce bytes left zero (the kernel's W0)
+  const uint64_t m = 8 + (uint64_t)len, nblk = bm_var_blocks(len);
+  std::vector<uint8_t> buf(nblk * 128, 0);
+  if (len) memcpy(buf.data() + 8, ih, len);
+  buf[m] = 0x80;
+  for (int i = 0; i < 8; ++i) buf[nblk * 128 - 1 - i] = (uint8_t)((m * 8) >> (8 * i));
+  buf[nblk * 128 - 9] = (uint8_t)(m >> 61);
+  o->nblk = (uint32_t)nblk;
+  o->vword = pool.size();
+  for (int i = 0; i < 16; ++i) pool.push_back(load_be64(buf.data() + 8 * i));
+  uint64_t w[80];
+  for (uint64_t j = 1; j < nblk; ++j) {
+    for (int t = 0; t < 16; ++t) w[t] = load_be64(buf.data() + 128 * j + 8 * t);
+    for (int t = 16; t < 80; ++t) {
+      const uint64_t s0 = ror(w[t - 15], 1) ^ ror(w[t - 15], 8) ^ (w[t - 15] >> 7);
+      const uint64_t s1 = ror(w[t - 2], 19) ^ ror(w[t - 2], 61) ^ (w[t - 2] >> 6);
+      w[t] = s1 + w[t - 7] + s0 + w[t - 16];
+    }
+    for (int t = 0; t < 80; ++t) pool.push_back(kK512[t] + w[t]);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
 // sessions
 // ---------------------------------------------------------------------------------------
-void init(BatchState& b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
+void init(BatchState& b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
+          const uint64_t* ih_off) {
+  const uint64_t epoch = b.vpool_epoch + 1;
   b = BatchState();
+  b.vpool_epoch = epoch;
   b.n = n;
   b.objs.resize(n);
   b.next.resize(n);
@@ -49,7 +124,8 @@ void init(BatchState& b, size_t n, const uint8_t* ihs, const uint64_t* targets, 
   b.trial.assign(n, 0);
   b.done.assign(n, BMPOW_PENDING);
   for (size_t i = 0; i < n; ++i) {
-    pack_obj(ihs + 64 * i, targets[i], &b.objs[i]);
+    pack_var(ih_ptr(ihs, ih_off, i), ih_len(ih_off, i), targets[i], &b.objs[i], b.vpool);
+    if (b.objs[i].ihlen != BM_IH_MAIN) b.nvar_slots++;
     b.next[i] = start ? start[i] : 1;
   }
   b.pending = n;
@@ -69,7 +145,11 @@ void mark_finished(BatchState& b, uint32_t slot) {
 }  // namespace
 
 bool add(BatchState& b, size_t m, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
-         std::vector<uint32_t>& slots) {
+         std::vector<uint32_t>& slots, const uint64_t* ih_off) {
+  if (b.nvar_slots == 0 && !b.vpool.empty()) {  // nothing refers to the old words any more
+    b.vpool.clear();
+    b.vpool_epoch++;
+  }
   slots.resize(m);
   const size_t n0 = b.n;
   for (size_t i = 0; i < m; ++i) {
@@ -89,7 +169,8 @@ bool add(BatchState& b, size_t m, const uint8_t* ihs, const uint64_t* targets, c
   }
   for (size_t i = 0; i < m; ++i) {
     const uint32_t k = slots[i];
-    pack_obj(ihs + 64 * i, targets[i], &b.objs[k]);
+    pack_var(ih_ptr(ihs, ih_off, i), ih_len(ih_off, i), targets[i], &b.objs[k], b.vpool);
+    if (b.objs[k].ihlen != BM_IH_MAIN) b.nvar_slots++;
     b.next[k] = start ? start[i] : 1;
     b.nonce[k] = b.trial[k] = 0;
     b.done[k] = BMPOW_PENDING;
@@ -109,6 +190,7 @@ size_t take_done(BatchState& b, size_t cap, uint32_t* slot_out, uint64_t* nonce_
     if (trial_out) trial_out[k] = b.trial[s];
     if (done_out) done_out[k] = b.done[s];
     b.done[s] = BMPOW_FREE;
+    if (b.objs[s].ihlen != BM_IH_MAIN) b.nvar_slots--;
     b.free_slots.push_back(s);
     ++k;
   }
@@ -215,7 +297,43 @@ bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, S
   }
   p.C = acc;
   slice(p.wins, p.C, p.chunk, S, p);
+  split_kinds(b.objs, p.chunk, b.nvar_slots > 0, p);
   return true;
+}
+
+void split_kinds(const std::vector<bm_obj>& objs, uint64_t chunk, bool any_var, StepPlan& p) {
+  const size_t S = p.items.size();
+  p.nmain.assign(S, 0);
+  p.chmain.assign(S, 0);
+  std::vector<bm_item> var;
+  for (size_t s = 0; s < S; ++s) {
+    std::vector<bm_item>& v = p.items[s];
+    if (!any_var) {
+      p.nmain[s] = (uint32_t)v.size();
+      p.chmain[s] = p.nchunks[s];
+      continue;
+    }
+    var.clear();
+    size_t k = 0;
+    uint64_t cm = 0, cv = 0;
+    for (const bm_item& it0 : v) {
+      bm_item it = it0;
+      const uint64_t nch = (it.count + chunk - 1) / chunk;
+      if (objs[it.obj].ihlen == BM_IH_MAIN) {
+        it.chunk_base = (uint32_t)cm;
+        cm += nch;
+        v[k++] = it;
+      } else {
+        it.chunk_base = (uint32_t)cv;
+        cv += nch;
+        var.push_back(it);
+      }
+    }
+    p.nmain[s] = (uint32_t)k;
+    p.chmain[s] = (uint32_t)cm;
+    std::copy(var.begin(), var.end(), v.begin() + (ptrdiff_t)k);
+    p.nchunks[s] = (uint32_t)(cm + cv);
+  }
 }
 
 void apply_step(BatchState& b, const StepPlan& p, const std::vector<const bm_result*>& res) {
@@ -623,12 +741,20 @@ void Service::stop() {
   if (th_.joinable()) th_.join();
 }
 
-int Service::submit(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* tickets_out) {
+int Service::submit(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* tickets_out,
+                    const uint64_t* ih_off) {
   if (n == 0) return 0;
   {
     std::lock_guard<std::mutex> lk(mu_);
     if (stopping_) return BMPOW_E_STATE;
-    in_ih_.insert(in_ih_.end(), ihs, ihs + 64 * n);
+    if (ih_off || !in_off_.empty()) {  // any length: the queue keeps per-object offsets from here on
+      if (in_off_.empty())
+        for (size_t i = 0; i <= in_ticket_.size(); ++i) in_off_.push_back(64 * i);
+      const uint64_t base = in_ih_.size();
+      for (size_t i = 1; i <= n; ++i) in_off_.push_back(base + (ih_off ? ih_off[i] - ih_off[0] : 64 * i));
+    }
+    if (ih_off) in_ih_.insert(in_ih_.end(), ihs + ih_off[0], ihs + ih_off[n]);
+    else in_ih_.insert(in_ih_.end(), ihs, ihs + 64 * n);
     in_target_.insert(in_target_.end(), targets, targets + n);
     for (size_t i = 0; i < n; ++i) {
       const uint64_t t = next_ticket_++;
@@ -662,8 +788,10 @@ int Service::poll(size_t cap, int timeout_ms, uint64_t* tickets, uint64_t* nonce
   // the host re-check runs on the polling thread, outside the lock, while the next step runs
   for (size_t j = 0; j < k; ++j) {
     Done d = popped[j].d;
+    const Out& o = popped[j];
     if (verify_ && d.done == BMPOW_DONE_FOUND &&
-        (host_trial(popped[j].ih, d.nonce) != d.trial || d.trial > popped[j].target))
+        ((o.var ? host_trial_len(o.ihv.data(), o.ihv.size(), d.nonce) : host_trial(o.ih, d.nonce)) != d.trial ||
+         d.trial > o.target))
       d.done = BMPOW_DONE_BADHASH;
     tickets[j] = d.ticket;
     if (nonce) nonce[j] = d.nonce;
@@ -680,6 +808,7 @@ void Service::cancel() {
     error_ = 0;
     err_.clear();
     in_ih_.clear();
+    in_off_.clear();
     in_target_.clear();
     in_ticket_.clear();
     out_.clear();
@@ -695,8 +824,10 @@ size_t Service::outstanding() {
 
 void Service::loop() {
   std::vector<uint8_t> ih;
-  std::vector<uint64_t> tg, tk, slot_ticket, slot_target;
+  std::vector<uint64_t> off, tg, tk, slot_ticket, slot_target;
   std::vector<uint8_t> slot_ih;  // 64 B per slot: the object's initialHash, for the re-check
+  std::vector<std::vector<uint8_t>> slot_ihv;  // per slot: an initialHash of another length
+  std::vector<uint8_t> slot_var;               // per slot: 1 when slot_ihv holds its initialHash
   std::vector<uint32_t> slots;
   constexpr size_t kTake = 4096;
   std::vector<uint32_t> fs(kTake);
@@ -713,6 +844,7 @@ void Service::loop() {
       cancel = cancel_;
       cancel_ = false;
       ih.swap(in_ih_);
+      off.swap(in_off_);
       tg.swap(in_target_);
       tk.swap(in_ticket_);
     }
@@ -725,17 +857,28 @@ void Service::loop() {
     }
     if (rc >= 0 && !tk.empty()) {
       slots.resize(tk.size());
-      rc = ops_.add(tk.size(), ih.data(), tg.data(), slots.data(), err);
+      const uint64_t* ih_off = off.empty() ? nullptr : off.data();
+      rc = ops_.add(tk.size(), ih.data(), ih_off, tg.data(), slots.data(), err);
       if (rc >= 0) {
         for (size_t i = 0; i < tk.size(); ++i) {
           if (slot_ticket.size() <= slots[i]) {
             slot_ticket.resize((size_t)slots[i] + 1);
             slot_target.resize((size_t)slots[i] + 1);
             slot_ih.resize(64 * ((size_t)slots[i] + 1));
+            slot_ihv.resize((size_t)slots[i] + 1);
+            slot_var.resize((size_t)slots[i] + 1);
           }
           slot_ticket[slots[i]] = tk[i];
           slot_target[slots[i]] = tg[i];
-          memcpy(&slot_ih[64 * (size_t)slots[i]], &ih[64 * i], 64);
+          const size_t len = ih_len(ih_off, i);
+          const uint8_t* p = ih_ptr(ih.data(), ih_off, i);
+          slot_var[slots[i]] = len != 64;
+          if (len == 64) {
+            memcpy(&slot_ih[64 * (size_t)slots[i]], p, 64);
+            std::vector<uint8_t>().swap(slot_ihv[slots[i]]);
+          } else {
+            slot_ihv[slots[i]].assign(p, p + len);
+          }
         }
         live += tk.size();
       }
@@ -748,8 +891,13 @@ void Service::loop() {
           Out o;
           o.d = {slot_ticket[fs[j]], fn[j], ft[j], fd[j]};
           o.target = slot_target[fs[j]];
-          memcpy(o.ih, &slot_ih[64 * (size_t)fs[j]], 64);
-          fin.push_back(o);
+          if (slot_var[fs[j]]) {
+            o.var = true;
+            o.ihv = slot_ihv[fs[j]];
+          } else {
+            memcpy(o.ih, &slot_ih[64 * (size_t)fs[j]], 64);
+          }
+          fin.push_back(std::move(o));
         }
         live -= k;
         if (k < kTake) break;
@@ -767,6 +915,7 @@ void Service::loop() {
     }
     cv_out_.notify_all();
     ih.clear();
+    off.clear();
     tg.clear();
     tk.clear();
   }

@@ -33,7 +33,16 @@ constexpr uint64_t kU64Max = ~0ULL;
 uint64_t load_be64(const uint8_t* p);
 // trial(nonce, ih) on the host (OpenSSL SHA-512): the re-check of device answers, never a search
 uint64_t host_trial(const uint8_t ih[64], uint64_t nonce);
+// the same for an initialHash of any length (src/proofofwork.py:106-107 hashes it as given)
+uint64_t host_trial_len(const uint8_t* ih, size_t len, uint64_t nonce);
 void pack_obj(const uint8_t* ih, uint64_t target, bm_obj* o);
+// An object of any initialHash length: 64 bytes -> pack_obj; otherwise the var form, its message words
+// appended to pool (block 0's 16 words, then K[t] + W[t] for t < 80 of every further block).
+void pack_var(const uint8_t* ih, size_t len, uint64_t target, bm_obj* o, std::vector<uint64_t>& pool);
+// Object i of a list given as concatenated bytes: 64 bytes each when off is null, else bytes
+// [off[i], off[i+1]).
+inline const uint8_t* ih_ptr(const uint8_t* ihs, const uint64_t* off, size_t i) { return ihs + (off ? off[i] : 64 * i); }
+inline size_t ih_len(const uint64_t* off, size_t i) { return off ? (size_t)(off[i + 1] - off[i]) : 64; }
 
 // Host mirror of a device-resident batch (one slot per object; slots of finished objects are
 // released by take_done and reused by add).
@@ -48,14 +57,21 @@ struct BatchState {
   std::vector<uint32_t> finished;  // slots finished since the last take_done, in finishing order
   size_t finished_head = 0;
   std::vector<uint32_t> free_slots;  // slots released by take_done, reused by add (LIFO)
+  // var-form objects (initialHash length != 64): their words, appended by add; emptied by add when
+  // no slot holds a var object any more (vpool_epoch then counts up, so the device copy restarts)
+  std::vector<uint64_t> vpool;
+  size_t nvar_slots = 0;  // non-free slots holding a var-form object
+  uint64_t vpool_epoch = 0;
 };
 
-void init(BatchState& b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start);
+// ih_off: null (n x 64-byte initialHashes) or n + 1 byte offsets into ihs (any lengths)
+void init(BatchState& b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
+          const uint64_t* ih_off = nullptr);
 
 // Append m objects (slots reused first).  slots[i] = object i's slot.  Returns true when the table
 // outgrew b.cap (the caller reallocates and re-uploads); false when only `slots` need uploading.
 bool add(BatchState& b, size_t m, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
-         std::vector<uint32_t>& slots);
+         std::vector<uint32_t>& slots, const uint64_t* ih_off = nullptr);
 
 // Pop up to cap finished slots (any output but slot_out may be null); they become BMPOW_FREE.
 size_t take_done(BatchState& b, size_t cap, uint32_t* slot_out, uint64_t* nonce_out, uint64_t* trial_out,
@@ -77,8 +93,15 @@ struct StepPlan {
   uint64_t C = 0;       // chunks in the step
   std::vector<Win> wins;                    // ascending object order
   std::vector<std::vector<bm_item>> items;  // per shard, ascending chunk_base
-  std::vector<uint32_t> nchunks;            // per shard: workgroups of its launch
+  std::vector<uint32_t> nchunks;            // per shard: workgroups of its launch(es)
+  // after split_kinds: per shard, items[s][0, nmain[s]) are 64-byte objects (bm_search_kernel, chunk_base
+  // from 0, chmain[s] chunks) and the rest var-form objects (bm_search_var_kernel, chunk_base again from 0)
+  std::vector<uint32_t> nmain, chmain;
 };
+
+// Reorder each shard's items into the two kernels' launches (see StepPlan); with any_var false every
+// item is 64-byte and nothing moves.
+void split_kinds(const std::vector<bm_obj>& objs, uint64_t chunk, bool any_var, StepPlan& p);
 
 // Cut C chunks of windows (ascending chunk0) into S contiguous per-shard slices: big windows are
 // nonce-sharded, small ones object-sharded; each item's chunk_base is relative to its shard.
@@ -177,8 +200,11 @@ int pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t extra, in
 // (ops.take) for poll().  The ops run on the stepper thread only and never under the service's
 // mutex, so a caller of submit/poll/cancel waits at most for a queue operation, never for a step.
 struct ServiceOps {
-  // append n objects (64-byte hashes, targets; searches start at nonce 1); slots[i] = object i's slot
-  std::function<int(size_t n, const uint8_t* ihs, const uint64_t* targets, uint32_t* slots, std::string& err)> add;
+  // append n objects (initialHashes: 64 bytes each, or by ih_off as in init; targets; searches start at
+  // nonce 1); slots[i] = object i's slot
+  std::function<int(size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* targets, uint32_t* slots,
+                    std::string& err)>
+      add;
   std::function<int(std::string& err)> step;  // one step over the pending objects
   std::function<size_t(size_t cap, uint32_t* slot, uint64_t* nonce, uint64_t* trial, uint8_t* done)> take;
   std::function<int(std::string& err)> reset;  // drop every object of the session
@@ -196,7 +222,9 @@ class Service {
   ~Service();  // stop()
   // Queue n objects; tickets_out[i] (may be null) = object i's ticket, ascending over the service's
   // life.  BMPOW_E_STATE once stopping.
-  int submit(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* tickets_out);
+  // ih_off: null (64-byte initialHashes) or n + 1 offsets into ihs (any lengths)
+  int submit(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* tickets_out,
+             const uint64_t* ih_off = nullptr);
   // Pop up to cap finished objects, waiting up to timeout_ms (< 0: forever) for the first.  Returns
   // the count, 0 on timeout, or the error a step hit (err = its text) once everything before it was
   // popped; nothing is stepped after an error until cancel().
@@ -212,12 +240,15 @@ class Service {
     Done d;
     uint64_t target;
     uint8_t ih[64];
+    std::vector<uint8_t> ihv;  // an initialHash of another length (ih unused), else empty
+    bool var = false;
   };
   ServiceOps ops_;
   const bool verify_;
   std::mutex mu_;  // guards every member below
   std::condition_variable cv_in_, cv_out_;
   std::vector<uint8_t> in_ih_;
+  std::vector<uint64_t> in_off_;  // n + 1 offsets into in_ih_ once any queued object is not 64 bytes, else empty
   std::vector<uint64_t> in_target_, in_ticket_;
   std::deque<Out> out_;
   uint64_t next_ticket_ = 0;

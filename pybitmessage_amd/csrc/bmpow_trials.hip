@@ -20,7 +20,17 @@ __device__ __noinline__ uint64_t trial_ool(uint64_t w0, uint64_t w1, uint64_t w2
   return trial_of(ihw, nonce);
 }
 
-__device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce) {
+// The same for a var-form object (an initialHash of another length, bmpow_var.hip).
+__device__ __noinline__ uint64_t trial_var_ool(const uint64_t* __restrict__ m, uint32_t nblk, uint64_t nonce) {
+  uint64_t mw[16];
+  mw[0] = 0;
+#pragma unroll
+  for (int i = 1; i < 16; ++i) mw[i] = m[i];
+  return trial_var(mw, m + 16, nblk, nonce);
+}
+
+__device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce, const uint64_t* vpool) {
+  if (o->ihlen != BM_IH_MAIN) return trial_var_ool(vpool + o->vword, o->nblk, nonce);
   return trial_ool(o->w[0], o->w[1], o->w[2], o->w[3], o->w[4], o->w[5], o->w[6], o->w[7], nonce);
 }
 
@@ -29,7 +39,8 @@ __device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce) {
 // the found flag, not the nonce, says whether there is a hit (2^64-1 is a legal answer).
 __global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
                                   uint32_t nitems, const unsigned long long* __restrict__ best,
-                                  const uint32_t* __restrict__ found, bm_result* __restrict__ res) {
+                                  const uint32_t* __restrict__ found, bm_result* __restrict__ res,
+                                  const uint64_t* __restrict__ vpool) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nitems) return;
   const uint32_t obj = items[k].obj;
@@ -38,33 +49,35 @@ __global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item
   r.trial = 0;
   r.found = found[obj];
   r.pad = 0;
-  if (r.found) r.trial = trial_obj(objs + obj, r.nonce);
+  if (r.found) r.trial = trial_obj(objs + obj, r.nonce, vpool);
   res[k] = r;
 }
 
-// Trial values for an arbitrary list of nonces of one object (parity probe / verification).
+// Trial values for an arbitrary list of nonces of one object, either form (parity probe).
 __global__ __launch_bounds__(BM_BLOCK) void bm_trials_kernel(const bm_obj* __restrict__ obj,
                                                              const uint64_t* __restrict__ nonces,
-                                                             uint64_t n, uint64_t* __restrict__ out) {
+                                                             uint64_t n, uint64_t* __restrict__ out,
+                                                             const uint64_t* __restrict__ vpool) {
   const uint64_t k = (uint64_t)blockIdx.x * BM_BLOCK + threadIdx.x;
   if (k >= n) return;
-  out[k] = trial_obj(obj, nonces[k]);
+  out[k] = trial_obj(obj, nonces[k], vpool);
 }
 
 // ---------------------------------------------------------------------------------------
 // Launch wrappers (C++ linkage, used by bmpow_host.hip).
 // ---------------------------------------------------------------------------------------
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
-                             const unsigned long long* best, const uint32_t* found, bm_result* res) {
+                             const unsigned long long* best, const uint32_t* found, bm_result* res,
+                             const uint64_t* vpool) {
   const uint32_t bs = 64;
   hipLaunchKernelGGL(bm_resolve_kernel, dim3((nitems + bs - 1) / bs), dim3(bs), 0, st, objs, items, nitems,
-                     best, found, res);
+                     best, found, res, vpool);
   return hipGetLastError();
 }
 
 hipError_t bm_launch_trials(hipStream_t st, const bm_obj* obj, const uint64_t* nonces, uint64_t n,
-                            uint64_t* out) {
+                            uint64_t* out, const uint64_t* vpool) {
   const uint64_t nb = (n + BM_BLOCK - 1) / BM_BLOCK;
-  hipLaunchKernelGGL(bm_trials_kernel, dim3((uint32_t)nb), dim3(BM_BLOCK), 0, st, obj, nonces, n, out);
+  hipLaunchKernelGGL(bm_trials_kernel, dim3((uint32_t)nb), dim3(BM_BLOCK), 0, st, obj, nonces, n, out, vpool);
   return hipGetLastError();
 }

@@ -181,14 +181,18 @@ constexpr uint64_t PAD = 0x8000000000000000ULL;
 // kTrial1: block 1 of the trial, whose W1..W8 are the object's (wave-uniform) initialHash words: the
 // sigma0 of W1..W8 (T = 16..23) and the sigma1 of the uniform W17, W19, W21 (T = 19, 21, 23) take the
 // hoistable builtin form.
-template <int T, bool kTrial1 = false>
+// kVar0: block 0 of a trial over an initialHash of any other length (trial_var): W1..W15 are all
+// per-object (uniform, not compile-time), so the sigma0 of W1..W15 (T = 16..30) and the sigma1 of
+// W14, W15, W17, W19, W21 (T = 16, 17, 19, 21, 23) are hoistable.
+template <int T, bool kTrial1 = false, bool kVar0 = false>
 BM_DEV void round_step(uint64_t (&s)[8], uint64_t (&w)[16]) {
   constexpr int A = (8 - (T & 7)) & 7;
   constexpr int B = (A + 1) & 7, C = (A + 2) & 7, D = (A + 3) & 7;
   constexpr int E = (A + 4) & 7, F = (A + 5) & 7, G = (A + 6) & 7, H = (A + 7) & 7;
   if constexpr (T >= 16) {
-    constexpr bool kU0 = kTrial1 && T <= 23;
-    constexpr bool kU1 = kTrial1 && (T == 19 || T == 21 || T == 23);
+    constexpr bool kU0 = (kTrial1 && T <= 23) || (kVar0 && T <= 30);
+    constexpr bool kU1 = (kTrial1 && (T == 19 || T == 21 || T == 23)) ||
+                         (kVar0 && (T == 16 || T == 17 || T == 19 || T == 21 || T == 23));
     // grouped so the terms that do not depend on the nonce (per-object or compile-time)
     // are summed first and hoisted out of the nonce loop by LICM
     w[T & 15] = (w[(T - 7) & 15] + sig0<kU0>(w[(T - 15) & 15]) + w[(T - 16) & 15]) + sig1<kU1>(w[(T - 2) & 15]);
@@ -224,11 +228,27 @@ BM_DEV void round_step(uint64_t (&s)[8], uint64_t (&w)[16]) {
 #endif
 }
 
-template <int T, int END, bool kTrial1 = false>
+template <int T, int END, bool kTrial1 = false, bool kVar0 = false>
 BM_DEV void rounds(uint64_t (&s)[8], uint64_t (&w)[16]) {
   if constexpr (T < END) {
-    round_step<T, kTrial1>(s, w);
-    rounds<T + 1, END, kTrial1>(s, w);
+    round_step<T, kTrial1, kVar0>(s, w);
+    rounds<T + 1, END, kTrial1, kVar0>(s, w);
+  }
+}
+
+// Rounds of a block whose whole message schedule is per-object: kw[t] = K[t] + W[t] precomputed on
+// the host (the later blocks of a long initialHash's first hash, bmsched::pack_var), read with
+// uniform (scalar) loads, so a round is its state update alone.
+template <int T, int END>
+BM_DEV void rounds_kw(uint64_t (&s)[8], const uint64_t* __restrict__ kw) {
+  if constexpr (T < END) {
+    constexpr int A = (8 - (T & 7)) & 7;
+    constexpr int B = (A + 1) & 7, C = (A + 2) & 7, D = (A + 3) & 7;
+    constexpr int E = (A + 4) & 7, F = (A + 5) & 7, G = (A + 6) & 7, H = (A + 7) & 7;
+    const uint64_t t1 = add64(add64(add64(s[H], Sig1(s[E])), Ch(s[E], s[F], s[G])), kw[T]);
+    s[D] = add64(s[D], t1);
+    s[H] = add64(add64(t1, Sig0(s[A])), Maj(s[A], s[B], s[C]));
+    rounds_kw<T + 1, END>(s, kw);
   }
 }
 
@@ -250,6 +270,44 @@ BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
   uint64_t w2[16];
 #pragma unroll
   for (int i = 0; i < 8; ++i) w2[i] = s[i] + IV(i);
+  w2[8] = PAD;
+#pragma unroll
+  for (int i = 9; i < 15; ++i) w2[i] = 0;
+  w2[15] = 64 * 8;
+  uint64_t s2[8] = {IV(0), IV(1), IV(2), w2[0] + E1C, IV(4), IV(5), IV(6), w2[0] + A1C};
+  rounds<1, 80>(s2, w2);
+  return s2[0] + IV(0);
+}
+
+// trial(n, ih) for an initialHash of any length L != 64 (the reference hashes pack('>Q', n) + ih as
+// given, src/proofofwork.py:104-107).  The first hash's message BE64(n) || ih || padding is
+// nblk = ceil((8 + L + 17) / 128) blocks (bmsched::pack_var lays out the per-object words):
+//   mw[1..15]  block 0's words after the nonce (ih bytes, the 0x80 pad, the bit length when it fits);
+//   kw[80 (j-1) .. 80 j)  K[t] + W[t] of block j = 1 .. nblk-1 (those blocks hold no nonce bit).
+// Block 0 starts from the IV with W0 = n, so round 0 folds as in trial_of; the second hash is the
+// one-block digest hash of trial_of.
+BM_DEV uint64_t trial_var(const uint64_t (&mw)[16], const uint64_t* __restrict__ kw, uint32_t nblk,
+                          uint64_t nonce) {
+  uint64_t w[16];
+  w[0] = nonce;
+#pragma unroll
+  for (int i = 1; i < 16; ++i) w[i] = mw[i];
+  uint64_t s[8] = {IV(0), IV(1), IV(2), nonce + E1C, IV(4), IV(5), IV(6), nonce + A1C};
+  rounds<1, 80, false, true>(s, w);
+  uint64_t h[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) h[i] = s[i] + IV(i);
+  for (uint32_t j = 1; j < nblk; ++j) {
+    uint64_t t[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = h[i];
+    rounds_kw<0, 80>(t, kw + (size_t)80 * (j - 1));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = opaque(h[i] + t[i]);
+  }
+  uint64_t w2[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w2[i] = h[i];
   w2[8] = PAD;
 #pragma unroll
   for (int i = 9; i < 15; ++i) w2[i] = 0;

@@ -17,7 +17,6 @@ Differences from the reference, each a fix of an Appendix-B quirk:
 """
 import ctypes
 import logging
-import time
 
 from . import _lib
 from . import proofofwork
@@ -87,27 +86,26 @@ def openclEnabled():
 
 
 def do_opencl_pow(hash_, target):
-    """Nonce for ``hash_`` (initialHash as hex, ``proofofwork.py:175``) and ``target``
-    (``openclpow.py:77-111``).  Returns 0 when no GPU is enabled, like the reference; raises
-    ``Exception("Interrupted")`` when ``state.shutdown`` is set between bounded calls."""
+    """Nonce for ``hash_`` (initialHash as hex, ``proofofwork.py:175``, any length) and ``target``
+    (``openclpow.py:77-111``): the ``_doSafePoW`` nonce.  Returns 0 when no GPU is enabled, like
+    the reference; raises ``Exception("Interrupted")`` when ``state.shutdown`` is set between
+    bounded calls and ``ValueError`` on a negative target."""
     if not enabledGpus:
         return 0
-    ih = bytes.fromhex(hash_) if isinstance(hash_, str) else bytes(hash_)
-    ih = ih + b'\x00' * (64 - len(ih))
-    # a negative target is unsatisfiable (never wrapped into a u64, which would accept nonce 1):
-    # wait, interruptibly, as the reference's kernel loop would spin
+    ih = proofofwork._ih_bytes(bytes.fromhex(hash_) if isinstance(hash_, str) else bytes(hash_))
+    # a negative target is unsatisfiable (never wrapped into a u64, which would accept nonce 1);
+    # the reference's numpy packing raises OverflowError on it or wraps it -- it never blocks
     target, satisfiable = proofofwork._clamp_target(target)
+    if not satisfiable:
+        raise ValueError('negative target: no nonce can satisfy it')
     lib = _lib.get()
     n, tv = ctypes.c_uint64(), ctypes.c_uint64()
     start = 1
     while True:
         if state.shutdown != 0:
             raise Exception('Interrupted')
-        if not satisfiable:
-            time.sleep(0.05)
-            continue
-        rc = _lib.check(lib, lib.bmpow_search(ih, target, start, CALL_TRIALS, ctypes.byref(n), ctypes.byref(tv)),
-                        'bmpow_search')
+        rc = _lib.check(lib, lib.bmpow_search_len(ih, len(ih), target, start, CALL_TRIALS, ctypes.byref(n),
+                                                  ctypes.byref(tv)), 'bmpow_search_len')
         if rc == _lib.FOUND:
             return n.value
         if start > _lib.U64_MAX - CALL_TRIALS:

@@ -13,11 +13,19 @@ plus the batched entry point BASELINE.json's north star asks for:
   caller release msgs whose embedded ack just finished, ``class_singleWorker.py:1220``).
 
 Every answer is the ``_doSafePoW`` answer (``:100-111``): the first ``nonce >= 1`` with
-``trialValue <= target``.  The search runs on gfx950 through ``libbmpow_hip.so`` in bounded
-steps; between steps ``state.shutdown`` is polled and a set flag raises
+``trialValue <= target``, for an ``initialHash`` of any length (hashed as given, ``:104-107``;
+every caller passes a 64-byte digest, the layout the main kernel is specialised for, other
+lengths run on ``bm_search_var_kernel``).  The search runs on gfx950 through ``libbmpow_hip.so``
+in bounded steps; between steps ``state.shutdown`` is polled and a set flag raises
 ``StopIteration("Interrupted")`` (the reference contract, ``:104-109``; the polling
 pattern of ``dev/powinterrupttest.py:22-37``).  There is NO CPU fallback: a missing library
 or device raises :class:`BmpowUnavailable` (the reference silently degraded to Python).
+
+A GPU answer that fails the host re-check disables the backend, as ``_doGPUPoW`` disables
+OpenCL (``:176-190``): the reference's error line is logged, ``hippow.enabledGpus`` is cleared,
+:func:`getPowType` reports ``"none"`` and every later call raises :class:`BmpowUnavailable`
+until :func:`resetPoW` -- the reference's fallback chain would continue on the CPU, which this
+product does not have.
 """
 import ctypes
 import hashlib
@@ -44,15 +52,16 @@ VERIFY = True
 
 
 def _ih_bytes(initialHash):
-    """The reference passes ``create_string_buffer(initialHash, 64)`` (``:161``): shorter
-    input is zero-padded to 64 bytes.  The GPU kernel's block layout is fixed to a 64-byte
-    initialHash (``sha512(payload).digest()`` at every call site)."""
+    """initialHash as bytes, at its own length: ``_doSafePoW`` hashes ``pack('>Q', nonce) +
+    initialHash`` as given (``:104-107``), so no padding (round 2 zero-padded to 64 bytes, the
+    ``_doCPoW`` buffer's behaviour, ``:161``, which gives other nonces).  Up to
+    ``_lib.MAX_IH_LEN`` bytes (1 MiB; the reference has no limit, its callers pass 64)."""
     if isinstance(initialHash, str):
         initialHash = initialHash.encode('latin-1')
     ih = bytes(initialHash)
-    if len(ih) > 64:
-        raise ValueError('initialHash must be at most 64 bytes (got %d)' % len(ih))
-    return ih + b'\x00' * (64 - len(ih))
+    if len(ih) > _lib.MAX_IH_LEN:
+        raise ValueError('initialHash longer than %d bytes (got %d)' % (_lib.MAX_IH_LEN, len(ih)))
+    return ih
 
 
 def _clamp_target(target):
@@ -70,11 +79,41 @@ def _trial_host(nonce, ih):
     return unpack('>Q', hashlib.sha512(hashlib.sha512(pack('>Q', nonce) + ih).digest()).digest()[0:8])[0]
 
 
+#: set by :func:`gpu_failed` (a wrong GPU answer), cleared by :func:`resetPoW`
+_disabled = None
+#: optional ``callable(message)`` the application sets to surface :func:`gpu_failed` in its UI (the
+#: reference puts an ``updateStatusBar`` signal on ``queues.UISignalQueue``, ``:178-185``)
+ui_notify = None
+
+
+def gpu_failed(detail):
+    """Disable the GPU backend after a wrong answer (``_doGPUPoW``, ``:176-190``) and raise."""
+    global _disabled
+    from . import hippow
+    names = ', '.join(g.name for g in hippow.enabledGpus) or 'gfx950'
+    logger.error('Your GPUs (%s) did not calculate correctly, disabling OpenCL. Please report to the developers.',
+                 names)
+    if ui_notify is not None:
+        try:
+            ui_notify('Your GPU(s) did not calculate correctly, disabling OpenCL. Please report to the developers.')
+        except Exception:  # noqa: BLE001 -- a UI hook never masks the error below
+            logger.exception('ui_notify failed')
+    del hippow.enabledGpus[:]
+    _disabled = detail
+    raise BmpowError(_lib.E_HIP, 'GPU did not calculate correctly: %s' % detail)
+
+
+def check_enabled():
+    if _disabled is not None:
+        raise BmpowUnavailable(_lib.E_NODEV, 'HIP PoW disabled after a wrong GPU answer (%s); resetPoW() '
+                                             're-enables it' % _disabled)
+
+
 def _verify(target, ih, trial, nonce):
     if VERIFY and _trial_host(nonce, ih) != trial:
-        raise BmpowError(_lib.E_HIP, 'GPU returned a wrong trial value for nonce %d' % nonce)
+        gpu_failed('wrong trial value for nonce %d' % nonce)
     if trial > target:
-        raise BmpowError(_lib.E_HIP, 'GPU returned nonce %d above target' % nonce)
+        gpu_failed('nonce %d above target' % nonce)
 
 
 def _interrupted():
@@ -83,6 +122,7 @@ def _interrupted():
 
 def _doHIPPoW(target, initialHash):
     """Single object on the GPU; replaces ``_doGPUPoW``/``_doCPoW`` (``:157-194``)."""
+    check_enabled()
     lib = _lib.get()
     ih = _ih_bytes(initialHash)
     t, satisfiable = _clamp_target(target)
@@ -97,8 +137,8 @@ def _doHIPPoW(target, initialHash):
             import time
             time.sleep(0.05)
             continue
-        rc = _lib.check(lib, lib.bmpow_search(ih, t, start, CALL_TRIALS, ctypes.byref(n), ctypes.byref(tv)),
-                        'bmpow_search')
+        rc = _lib.check(lib, lib.bmpow_search_len(ih, len(ih), t, start, CALL_TRIALS, ctypes.byref(n),
+                                                  ctypes.byref(tv)), 'bmpow_search_len')
         if rc == _lib.FOUND:
             break
         if start > U64_MAX - CALL_TRIALS:
@@ -139,20 +179,24 @@ def iter_batch(objects, step_trials=0):
     polled at least every 100 ms and raises :class:`PowInterrupted`; closing the generator stops
     the service after its current step."""
     import numpy as np
+    check_enabled()
     lib = _lib.get()
     objs = list(objects)
     n = len(objs)
     if n == 0:
         return
     ihs = bytearray()
+    offs = [0]
     targets = np.empty(n, dtype=np.uint64)
     for i, (target, ih) in enumerate(objs):
         ihs += _ih_bytes(ih)
+        offs.append(len(ihs))
         t, ok = _clamp_target(target)
         if not ok:
             raise ValueError('object %d has a negative target: no nonce can satisfy it' % i)
         targets[i] = t
     ihs = bytes(ihs)
+    var = len(ihs) != 64 * n or any(b - a != 64 for a, b in zip(offs, offs[1:]))
     p64 = ctypes.POINTER(ctypes.c_uint64)
     s = lib.bmpow_service_create(step_trials, _lib.SERVICE_VERIFY if VERIFY else 0)
     if not s:
@@ -160,8 +204,13 @@ def iter_batch(objects, step_trials=0):
     try:
         cap = min(n, 65536)
         tick = np.zeros(max(n, cap), dtype=np.uint64)
-        _lib.check(lib, lib.bmpow_service_submit(s, n, ihs, targets.ctypes.data_as(p64), tick.ctypes.data_as(p64)),
-                   'bmpow_service_submit')
+        if var:  # some initialHash is not 64 bytes: per-object offsets
+            off = np.array(offs, dtype=np.uint64)
+            _lib.check(lib, lib.bmpow_service_submit_var(s, n, ihs, off.ctypes.data_as(p64), targets.ctypes.data_as(p64),
+                                                         tick.ctypes.data_as(p64)), 'bmpow_service_submit_var')
+        else:
+            _lib.check(lib, lib.bmpow_service_submit(s, n, ihs, targets.ctypes.data_as(p64), tick.ctypes.data_as(p64)),
+                       'bmpow_service_submit')
         base = int(tick[0])  # tickets are consecutive from the first
         nonce = np.zeros(cap, dtype=np.uint64)
         trial = np.zeros(cap, dtype=np.uint64)
@@ -177,7 +226,7 @@ def iter_batch(objects, step_trials=0):
             for t, tv, nn, d in zip(tick[:k].tolist(), trial[:k].tolist(), nonce[:k].tolist(), done[:k].tolist()):
                 i = t - base
                 if d == _lib.DONE_BADHASH:
-                    raise BmpowError(_lib.E_HIP, 'object %d: GPU answer (nonce %d) failed the host re-check' % (i, nn))
+                    gpu_failed('object %d: answer (nonce %d) failed the host re-check' % (i, nn))
                 if d != _lib.DONE_FOUND:
                     raise BmpowError(_lib.E_ARG, 'object %d: nonce space exhausted' % i)
                 yield i, tv, nn
@@ -279,14 +328,23 @@ def _device_count():
 
 
 def resetPoW():
-    """Re-select devices (reference ``:328-330`` re-ran ``openclpow.initCL``)."""
+    """Re-select devices and re-enable the backend after :func:`gpu_failed` (reference
+    ``:328-330`` re-ran ``openclpow.initCL``, which re-enables the GPUs)."""
+    global _disabled
+    _disabled = None
     _lib.reset()
-    return init()
+    n = init()
+    from . import hippow
+    hippow.initCL()
+    return n
 
 
 def getPowType():
     """``"HIP"`` when the gfx950 engine is usable (reference ``:229-236`` returned
-    ``"OpenCL"``/``"C"``/``"python"``); ``"none"`` otherwise (there is no CPU fallback)."""
+    ``"OpenCL"``/``"C"``/``"python"``); ``"none"`` otherwise -- no device, or disabled after a
+    wrong answer (:func:`gpu_failed`; there is no CPU fallback)."""
+    if _disabled is not None:
+        return 'none'
     try:
         _lib.get()
         return 'HIP'

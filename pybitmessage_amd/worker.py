@@ -403,11 +403,12 @@ class BatchResult(object):
 
 class _Sub(object):
     """The objects of one ``bmpow_service_submit`` call: tickets ``base .. base + n - 1``."""
-    __slots__ = ('base', 'ihs', 'targets', 'futs', 'group', 'left')
+    __slots__ = ('base', 'ihs', 'offs', 'targets', 'futs', 'group', 'left')
 
-    def __init__(self, ihs, targets, futs, group):
+    def __init__(self, ihs, targets, futs, group, offs=None):
         self.base = 0
-        self.ihs = ihs  # n x 64 bytes
+        self.ihs = ihs  # n x 64 bytes, or the concatenated initialHashes of any lengths (offs)
+        self.offs = offs  # None, or n + 1 byte offsets into ihs
         self.targets = targets  # n clamped targets
         self.futs = futs
         self.group = group  # the shared _Group of BatchResults, or None for Futures
@@ -483,7 +484,11 @@ class PowService(object):
                 self._lib.bmpow_service_stop(self._h)
         if th is not None:
             th.join(timeout)
-        self._completer = None
+        with self._lock:
+            # a completer still running (join timed out) stays registered: start() must not put a
+            # second one beside it; it clears itself when it exits
+            if self._completer is th and (th is None or not th.is_alive()):
+                self._completer = None
 
     def submit(self, target, initialHash):
         fut = Future()
@@ -491,7 +496,8 @@ class PowService(object):
         if not ok:
             fut.set_exception(ValueError('negative target: no nonce can satisfy it'))
             return fut
-        self._enqueue(_Sub(proofofwork._ih_bytes(initialHash), [t], [fut], None))
+        ih = proofofwork._ih_bytes(initialHash)
+        self._enqueue(_Sub(ih, [t], [fut], None, None if len(ih) == 64 else [0, len(ih)]))
         return fut
 
     def submit_many(self, objects):
@@ -514,7 +520,7 @@ class PowService(object):
                     all(type(ih) is bytes and len(ih) == 64 for ih in ihs):
                 self._enqueue(_Sub(b''.join(ihs), tgs, futs, group))
                 continue
-            kf, kih, kt = [], [], []
+            kf, kih, kt, offs = [], [], [], [0]
             for fut, (target, initialHash) in zip(futs, chunk):
                 t, ok = clamp(target)
                 if not ok:
@@ -522,9 +528,11 @@ class PowService(object):
                     continue
                 kf.append(fut)
                 kih.append(ihb(initialHash))
+                offs.append(offs[-1] + len(kih[-1]))
                 kt.append(t)
             if kf:
-                self._enqueue(_Sub(b''.join(kih), kt, kf, group))
+                var = any(len(ih) != 64 for ih in kih)
+                self._enqueue(_Sub(b''.join(kih), kt, kf, group, offs if var else None))
         return out
 
     def _enqueue(self, sub):
@@ -538,10 +546,20 @@ class PowService(object):
             if state.shutdown != 0:
                 self._fail([sub], StopIteration('Interrupted'))
                 return
+            try:
+                proofofwork.check_enabled()
+            except _lib.BmpowUnavailable as e:
+                self._fail([sub], e)
+                return
             n = len(sub.futs)
             tg = array.array('Q', sub.targets)
             tk = (ctypes.c_uint64 * n)()
-            rc = self._lib.bmpow_service_submit(self._h, n, sub.ihs, ctypes.cast(tg.buffer_info()[0], _P64), tk)
+            if sub.offs is None:
+                rc = self._lib.bmpow_service_submit(self._h, n, sub.ihs, ctypes.cast(tg.buffer_info()[0], _P64), tk)
+            else:
+                off = array.array('Q', sub.offs)
+                rc = self._lib.bmpow_service_submit_var(self._h, n, sub.ihs, ctypes.cast(off.buffer_info()[0], _P64),
+                                                        ctypes.cast(tg.buffer_info()[0], _P64), tk)
             if rc < 0:
                 self._fail([sub], _lib.BmpowError(rc, 'bmpow_service_submit: %s'
                                                   % self._lib.bmpow_last_error().decode()))
@@ -632,8 +650,10 @@ class PowService(object):
                         else:
                             fut.set_result([tv, nn])
                     elif d == _lib.DONE_BADHASH:
-                        fut.set_exception(_lib.BmpowError(_lib.E_HIP, 'GPU answer (nonce %d) failed the host re-check'
-                                                          % nn))
+                        try:  # disables the backend, as _doGPUPoW does (proofofwork.py:176-190)
+                            proofofwork.gpu_failed('answer (nonce %d) failed the host re-check' % nn)
+                        except _lib.BmpowError as e:
+                            fut.set_exception(e)
                     else:
                         fut.set_exception(_lib.BmpowError(_lib.E_ARG, 'nonce space exhausted'))
                     touched[id(sub)] = sub
@@ -645,5 +665,8 @@ class PowService(object):
                 self._subs, self._bases = [], []
                 if h is not None:
                     lib.bmpow_service_destroy(h)
-                self._h = None
+                if self._h is h:  # never the handle of a service started after this one
+                    self._h = None
+                if self._completer is threading.current_thread():
+                    self._completer = None
             self._fail(dead, RuntimeError('PowService stopped'))

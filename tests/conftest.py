@@ -53,3 +53,12 @@ def shards(gpulib):
     yield use
     gpulib.bmpow_set_devices(None, 0)
     gpulib.bmpow_set_step_trials(1 << 28)
+
+
+@pytest.fixture(autouse=True)
+def _reenable_backend():
+    """A test that feeds a wrong GPU answer disables the backend process-wide (proofofwork.gpu_failed,
+    as the reference's _doGPUPoW clears openclpow.enabledGpus); the next test starts enabled."""
+    yield
+    from pybitmessage_amd import proofofwork
+    proofofwork._disabled = None

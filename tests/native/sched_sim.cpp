@@ -31,6 +31,10 @@ uint64_t bmo_trial(const uint8_t ih[64], uint64_t nonce);
 int bmo_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials, uint64_t* nonce_out,
                uint64_t* trial_out);
 int bmo_min_trial(const uint8_t ih[64], uint64_t start, uint64_t count, uint64_t* min_out, uint64_t* argmin_out);
+uint64_t bmo_trial_len(const uint8_t* ih, size_t len, uint64_t nonce);
+const uint64_t* bmo_k512(void);
+int bmo_search_len(const uint8_t* ih, size_t len, uint64_t target, uint64_t start, uint64_t max_trials,
+                   uint64_t* nonce_out, uint64_t* trial_out);
 }
 
 using namespace bmsched;
@@ -51,6 +55,52 @@ static void ih_of(const bm_obj& o, uint8_t ih[64]) {
     for (int j = 0; j < 8; ++j) ih[8 * i + j] = (uint8_t)(o.w[i] >> (56 - 8 * j));
 }
 
+// ---- the var form's words (bmsched::pack_var) consumed the way bm_search_var_kernel does ----
+static const uint64_t kIV[8] = {0x6a09e667f3bcc908ULL, 0xbb67ae8584caa73bULL, 0x3c6ef372fe94f82bULL,
+                                0xa54ff53a5f1d36f1ULL, 0x510e527fade682d1ULL, 0x9b05688c2b3e6c1fULL,
+                                0x1f83d9abfb41bd6bULL, 0x5be0cd19137e2179ULL};
+static uint64_t g_k[80];  // K[t] (init_k)
+static inline uint64_t ror64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
+// 80 rounds from state h over kw[t] = K[t] + W[t]
+static void rounds_kw(uint64_t h[8], const uint64_t* kw) {
+  uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+  for (int t = 0; t < 80; ++t) {
+    const uint64_t t1 = hh + (ror64(e, 14) ^ ror64(e, 18) ^ ror64(e, 41)) + ((e & f) ^ (~e & g)) + kw[t];
+    const uint64_t t2 = (ror64(a, 28) ^ ror64(a, 34) ^ ror64(a, 39)) + ((a & b) ^ (a & c) ^ (b & c));
+    hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+}
+static void compress_w(uint64_t h[8], const uint64_t blk[16]) {
+  uint64_t w[80], kw[80];
+  for (int t = 0; t < 16; ++t) w[t] = blk[t];
+  for (int t = 16; t < 80; ++t)
+    w[t] = (ror64(w[t - 2], 19) ^ ror64(w[t - 2], 61) ^ (w[t - 2] >> 6)) + w[t - 7] +
+           (ror64(w[t - 15], 1) ^ ror64(w[t - 15], 8) ^ (w[t - 15] >> 7)) + w[t - 16];
+  for (int t = 0; t < 80; ++t) kw[t] = g_k[t] + w[t];
+  rounds_kw(h, kw);
+}
+static uint64_t trial_from_pool(const bm_obj& o, const std::vector<uint64_t>& pool, uint64_t nonce) {
+  uint64_t h[8], blk[16];
+  memcpy(h, kIV, sizeof h);
+  for (int i = 0; i < 16; ++i) blk[i] = pool[o.vword + i];
+  blk[0] = nonce;
+  compress_w(h, blk);
+  for (uint32_t j = 1; j < o.nblk; ++j) rounds_kw(h, &pool[o.vword + 16 + 80 * (j - 1)]);
+  for (int i = 0; i < 8; ++i) blk[i] = h[i];
+  blk[8] = 0x8000000000000000ULL;
+  for (int i = 9; i < 15; ++i) blk[i] = 0;
+  blk[15] = 512;
+  memcpy(h, kIV, sizeof h);
+  compress_w(h, blk);
+  return h[0];
+}
+// K[t]: the C oracle's FIPS 180-4 table (the stand-in shares no table with the library)
+static void init_k() {
+  const uint64_t* k = bmo_k512();
+  for (int i = 0; i < 80; ++i) g_k[i] = k[i];
+}
+
 // ---- CPU stand-in for one shard's device state and kernels ----
 struct SimShard {
   std::vector<uint64_t> best;
@@ -60,17 +110,23 @@ struct SimShard {
 
 // bm_search_kernel + bm_resolve_kernel for one shard: per item, nonces in order up to the first hit
 // (the device's early exit gives the same per-object minimum); res[k] = the object's shard minimum.
-static void sim_step_shard(const std::vector<bm_obj>& objs, const std::vector<bm_item>& items, SimShard& sh) {
+static uint64_t sim_trial(const bm_obj& o, const std::vector<uint64_t>& vpool, uint64_t nonce) {
+  if (o.ihlen != BM_IH_MAIN) return trial_from_pool(o, vpool, nonce);
+  uint8_t ih[64];
+  ih_of(o, ih);
+  return bmo_trial(ih, nonce);
+}
+
+static void sim_step_shard(const std::vector<bm_obj>& objs, const std::vector<uint64_t>& vpool,
+                           const std::vector<bm_item>& items, SimShard& sh) {
   if (sh.best.size() < objs.size()) {
     sh.best.resize(objs.size(), kU64Max);
     sh.found.resize(objs.size(), 0);
   }
-  uint8_t ih[64];
   for (const bm_item& it : items) {
-    ih_of(objs[it.obj], ih);
     for (uint64_t j = 0; j < it.count; ++j) {
       const uint64_t n = it.start + j;
-      if (bmo_trial(ih, n) <= objs[it.obj].target) {
+      if (sim_trial(objs[it.obj], vpool, n) <= objs[it.obj].target) {
         if (!sh.found[it.obj] || n < sh.best[it.obj]) sh.best[it.obj] = n;
         sh.found[it.obj] = 1;
         break;
@@ -85,8 +141,7 @@ static void sim_step_shard(const std::vector<bm_obj>& objs, const std::vector<bm
     r.found = sh.found[o];
     r.pad = 0;
     if (r.found) {
-      ih_of(objs[o], ih);
-      r.trial = bmo_trial(ih, r.nonce);
+      r.trial = sim_trial(objs[o], vpool, r.nonce);
     } else {
       r.trial = 0;
     }
@@ -101,12 +156,22 @@ static bool sim_step(BatchState& b, std::vector<SimShard>& shards, uint64_t budg
   uint64_t chunks = 0;
   for (size_t s = 0; s < shards.size(); ++s) chunks += p.nchunks[s];
   CHECK(chunks == p.C, "shard chunks %llu != step chunks %llu", (unsigned long long)chunks, (unsigned long long)p.C);
-  for (size_t s = 0; s < shards.size(); ++s)
-    for (size_t k = 1; k < p.items[s].size(); ++k)
-      CHECK(p.items[s][k].chunk_base > p.items[s][k - 1].chunk_base, "chunk_base not ascending");
+  for (size_t s = 0; s < shards.size(); ++s) {
+    // two launches per shard (split_kinds): 64-byte objects, then var-form ones, chunk_base from 0 in each
+    uint64_t cm = 0, cv = 0;
+    for (size_t k = 0; k < p.items[s].size(); ++k) {
+      const bm_item& it = p.items[s][k];
+      const bool main_kind = k < p.nmain[s];
+      CHECK(main_kind == (b.objs[it.obj].ihlen == BM_IH_MAIN), "item %zu of shard %zu in the wrong launch", k, s);
+      uint64_t& c = main_kind ? cm : cv;
+      CHECK(it.chunk_base == c, "chunk_base %u, want %llu", it.chunk_base, (unsigned long long)c);
+      c += (it.count + p.chunk - 1) / p.chunk;
+    }
+    CHECK(cm == p.chmain[s] && cm + cv == p.nchunks[s], "shard %zu chunk totals", s);
+  }
   std::vector<std::thread> th;
-  for (size_t s = 0; s < shards.size(); ++s) th.emplace_back(sim_step_shard, std::cref(b.objs), std::cref(p.items[s]),
-                                                             std::ref(shards[s]));
+  for (size_t s = 0; s < shards.size(); ++s)
+    th.emplace_back(sim_step_shard, std::cref(b.objs), std::cref(b.vpool), std::cref(p.items[s]), std::ref(shards[s]));
   for (auto& t : th) t.join();
   std::vector<const bm_result*> res(shards.size());
   for (size_t s = 0; s < shards.size(); ++s) res[s] = shards[s].res.data();
@@ -169,6 +234,79 @@ static void scenario_batches() {
     for (size_t i = 0; i < c.n; ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "batch", i);
     fprintf(stderr, "batches: n=%zu S=%zu budget=%llu: %d steps\n", c.n, c.S, (unsigned long long)c.budget, steps);
   }
+}
+
+// ---- scenario 1c: initialHashes of any length (the var form, pack_var + split_kinds) ----
+static void scenario_var() {
+  std::mt19937_64 rng(21);
+  // the var pool's words, consumed as bm_search_var_kernel does, give the oracle's trial at every
+  // SHA-512 block edge of the first hash's message (8 + L + 17 bytes)
+  for (size_t L : std::initializer_list<size_t>{0, 1, 7, 8, 63, 65, 100, 103, 104, 111, 112, 127, 128, 200, 231, 232, 239, 240, 255, 256, 359,
+                   360, 1000, 4096}) {
+    std::vector<uint8_t> ih(L);
+    for (auto& c : ih) c = (uint8_t)rng();
+    std::vector<uint64_t> pool(3, 7);  // an object not at word 0
+    bm_obj o;
+    pack_var(ih.data(), L, 5, &o, pool);
+    CHECK(o.ihlen == L && o.target == 5 && o.vword == 3, "pack_var header L=%zu", L);
+    CHECK(pool.size() == 3 + bm_var_words(L), "pack_var words L=%zu", L);
+    for (uint64_t n : std::initializer_list<uint64_t>{0, 1, 2, 1ull << 32, 0xfedcba9876543210ull, kU64Max}) {
+      const uint64_t want = bmo_trial_len(ih.data(), L, n);
+      CHECK(trial_from_pool(o, pool, n) == want, "var trial L=%zu n=%llu", L, (unsigned long long)n);
+      CHECK(host_trial_len(ih.data(), L, n) == want, "host_trial_len L=%zu", L);
+    }
+  }
+  // mixed batches over 1..4 shards: every answer the sequential search's
+  for (size_t S : std::initializer_list<size_t>{1, 2, 4}) {
+    const size_t n = 150;
+    std::vector<std::vector<uint8_t>> ihs(n);
+    std::vector<uint8_t> cat;
+    std::vector<uint64_t> off(1, 0), tg(n);
+    for (size_t i = 0; i < n; ++i) {
+      const size_t L = (i % 3 == 0) ? 64 : (size_t)(rng() % 300);
+      ihs[i].resize(L);
+      for (auto& c : ihs[i]) c = (uint8_t)rng();
+      cat.insert(cat.end(), ihs[i].begin(), ihs[i].end());
+      off.push_back(cat.size());
+      tg[i] = kU64Max / (1 + rng() % 3000);
+    }
+    BatchState b;
+    init(b, n, cat.data(), tg.data(), nullptr, off.data());
+    std::vector<SimShard> shards(S);
+    while (sim_step(b, shards, 1 << 14, 1 << 12)) {
+    }
+    for (size_t i = 0; i < n; ++i) {
+      uint64_t nn = 0, t = 0;
+      const int hit = bmo_search_len(ihs[i].data(), ihs[i].size(), tg[i], 1, kU64Max, &nn, &t);
+      CHECK(hit && b.done[i] == BMPOW_DONE_FOUND && b.nonce[i] == nn && b.trial[i] == t,
+            "var batch S=%zu object %zu (L=%zu): got %llu want %llu", S, i, ihs[i].size(),
+            (unsigned long long)b.nonce[i], (unsigned long long)nn);
+    }
+  }
+  // a session: var objects added, taken, the pool emptied once no slot holds one (new epoch)
+  BatchState b;
+  init(b, 0, nullptr, nullptr, nullptr);
+  const uint64_t e0 = b.vpool_epoch;
+  std::vector<uint8_t> ih(100, 0x5a);
+  const uint64_t off[2] = {0, 100}, t1 = kU64Max / 50;
+  std::vector<uint32_t> sl;
+  add(b, 1, ih.data(), &t1, nullptr, sl, off);
+  CHECK(b.nvar_slots == 1 && b.vpool.size() == bm_var_words(100), "session var add");
+  std::vector<SimShard> shards(2);
+  while (sim_step(b, shards, 1 << 13, 1 << 12)) {
+  }
+  uint32_t slot;
+  uint64_t nn, tt;
+  uint8_t dn;
+  CHECK(take_done(b, 1, &slot, &nn, &tt, &dn) == 1 && dn == BMPOW_DONE_FOUND, "session var take");
+  CHECK(b.nvar_slots == 0, "var slot released");
+  uint64_t wn = 0, wt = 0;
+  bmo_search_len(ih.data(), 100, t1, 1, kU64Max, &wn, &wt);
+  CHECK(nn == wn && tt == wt, "session var answer");
+  uint8_t ih64[64] = {1};
+  add(b, 1, ih64, &t1, nullptr, sl);
+  CHECK(b.vpool.empty() && b.vpool_epoch == e0 + 1, "var pool emptied at the next add");
+  fprintf(stderr, "var: pack_var at every block edge, mixed batches over 1/2/4 shards, session pool reuse\n");
 }
 
 // ---- scenario 1b: over several shards a window is capped near the expected trials to a hit ----
@@ -512,10 +650,11 @@ static void scenario_service() {
   std::vector<SimShard> shards(2);
   std::atomic<int> fail_step{0}, corrupt{0};
   ServiceOps ops;
-  ops.add = [&](size_t n, const uint8_t* ihs, const uint64_t* tg, uint32_t* slots, std::string&) {
+  ops.add = [&](size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* tg, uint32_t* slots,
+                std::string&) {
     std::lock_guard<std::mutex> lk(gmu);
     std::vector<uint32_t> sl;
-    add(b, n, ihs, tg, nullptr, sl);
+    add(b, n, ihs, tg, nullptr, sl, ih_off);
     b.cap = std::max(b.cap, b.n);
     for (SimShard& sh : shards)
       for (uint32_t x : sl)
@@ -628,11 +767,53 @@ static void scenario_service() {
   CHECK(k == 1 && tk[0] == t[0], "after error: k=%d", k);
   if (k == 1) expect_exact(easy[0], dn[0], nn[0], tv[0], "after error", 0);
 
+  // initialHashes of other lengths in one submit beside 64-byte ones (bmpow_service_submit_var):
+  // exact answers, re-checked on the host at their own length
+  {
+    const size_t lens[5] = {0, 64, 5, 104, 300};
+    std::vector<uint8_t> cat;
+    std::vector<uint64_t> off(1, 0), tgv(5, kU64Max / 700), tkv(5);
+    std::vector<std::vector<uint8_t>> ihv(5);
+    for (size_t i = 0; i < 5; ++i) {
+      ihv[i].resize(lens[i]);
+      for (auto& c : ihv[i]) c = (uint8_t)rng();
+      cat.insert(cat.end(), ihv[i].begin(), ihv[i].end());
+      off.push_back(cat.size());
+    }
+    submit_objs(easy, t);  // a 64-byte object queued first: the queue switches to offsets
+    CHECK(svc.submit(5, cat.data(), tgv.data(), tkv.data(), off.data()) == 0, "var submit");
+    size_t seen = 0;
+    while (seen < 6) {
+      k = svc.poll(64, -1, tk, nn, tv, dn, err);
+      CHECK(k > 0, "var poll %d", k);
+      if (k <= 0) break;
+      for (int j = 0; j < k; ++j, ++seen) {
+        if (tk[j] == t[0]) {
+          expect_exact(easy[0], dn[j], nn[j], tv[j], "before var", 0);
+          continue;
+        }
+        const size_t i = tk[j] - tkv[0];
+        uint64_t wn = 0, wt = 0;
+        bmo_search_len(ihv[i].data(), lens[i], tgv[i], 1, kU64Max, &wn, &wt);
+        CHECK(i < 5 && dn[j] == BMPOW_DONE_FOUND && nn[j] == wn && tv[j] == wt, "var service object %zu", i);
+      }
+    }
+  }
+
   // the host re-check reports a wrong trial as BMPOW_DONE_BADHASH
   corrupt = 1;
   submit_objs(easy, t);
   k = svc.poll(64, -1, tk, nn, tv, dn, err);
   CHECK(k == 1 && dn[0] == BMPOW_DONE_BADHASH, "corrupted answer: k=%d done=%d", k, k > 0 ? dn[0] : -1);
+  {  // ... also for an initialHash of another length
+    std::vector<uint8_t> ih7(7, 3);
+    const uint64_t off7[2] = {0, 7}, t7 = kU64Max / 30;
+    uint64_t tk7 = 0;
+    corrupt = 1;
+    svc.submit(1, ih7.data(), &t7, &tk7, off7);
+    k = svc.poll(64, -1, tk, nn, tv, dn, err);
+    CHECK(k == 1 && tk[0] == tk7 && dn[0] == BMPOW_DONE_BADHASH, "corrupted var answer: k=%d", k);
+  }
   // stop() wakes a poll blocked on an idle service
   std::thread waiter([&] {
     uint64_t a[4], b2[4], c[4];
@@ -649,7 +830,9 @@ static void scenario_service() {
 }
 
 int main() {
+  init_k();
   scenario_batches();
+  scenario_var();
   scenario_expect_cap();
   scenario_top_of_space();
   scenario_session();

@@ -117,7 +117,10 @@ def test_edge_targets(gpulib, coracle):
     assert gpu_search(gpulib, ih, t1 - 1) == coracle.search(ih, t1 - 1)
     assert proofofwork.run(2 ** 64, ih) == [t1, 1]          # target above 2^64-1 accepts all
     assert proofofwork.run(float(2 ** 63), ih)[1] >= 1      # float targets are int()-ed
-    assert proofofwork.run(t1, b'') == list(coracle.search(bytes(64), t1))  # '' -> 64 zero bytes
+    # an initialHash is hashed as given (src/proofofwork.py:104-107): b'' is the nonce alone, not
+    # the 64 zero bytes of _doCPoW's buffer (test_gpu_len.py covers every length edge)
+    assert proofofwork.run(t1, b'') == list(coracle.search_len(b'', t1))
+    assert proofofwork.run(t1, b'') != list(coracle.search(bytes(64), t1))
 
 
 def test_budget_and_resume(gpulib):

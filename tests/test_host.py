@@ -41,9 +41,10 @@ def test_header_declares_the_boundary():
               'bmpow_addr_set_comb', 'bmpow_addr_last_comb', 'bmpow_fe_probe', 'bmpow_min_trial',
               'bmpow_min_trial_batch', 'bmpow_batch_add', 'bmpow_batch_take_done', 'bmpow_service_create',
               'bmpow_service_submit', 'bmpow_service_poll', 'bmpow_service_cancel', 'bmpow_service_outstanding',
-              'bmpow_service_stop', 'bmpow_service_destroy']:
+              'bmpow_service_stop', 'bmpow_service_destroy', 'bmpow_set_device_count', 'bmpow_trials_len',
+              'bmpow_search_len', 'bmpow_min_trial_var', 'bmpow_batch_add_var', 'bmpow_service_submit_var']:
         assert s in syms
-    assert len(syms) == 47
+    assert len(syms) == 53
 
 
 def test_library_exports_every_declared_symbol(rawlib):
@@ -76,12 +77,16 @@ def test_no_device_fails_loudly():
     assert proofofwork.init() == 0
 
 
-def test_ih_padding_mirrors_create_string_buffer():
-    assert proofofwork._ih_bytes(b'') == bytes(64)
-    assert proofofwork._ih_bytes(b'ab') == b'ab' + bytes(62)
-    assert proofofwork._ih_bytes('ab') == b'ab' + bytes(62)
+def test_ih_is_hashed_as_given():
+    """_doSafePoW hashes pack('>Q', nonce) + initialHash at its own length (src/proofofwork.py:
+    104-107): no zero-padding to the _doCPoW buffer's 64 bytes (round 2 padded)."""
+    assert proofofwork._ih_bytes(b'') == b''
+    assert proofofwork._ih_bytes(b'ab') == b'ab'
+    assert proofofwork._ih_bytes('ab') == b'ab'
+    assert proofofwork._ih_bytes(bytes(65)) == bytes(65)
+    assert proofofwork._ih_bytes(bytearray(200)) == bytes(200)
     with pytest.raises(ValueError):
-        proofofwork._ih_bytes(bytes(65))
+        proofofwork._ih_bytes(bytes(_lib.MAX_IH_LEN + 1))
 
 
 def test_target_clamp():
@@ -123,20 +128,28 @@ class ScriptedLib(object):
     """Test double of the C ABI: bmpow_search answers from the C oracle over the bounded
     window it is asked for (so loop/resume logic is exercised exactly)."""
 
-    def __init__(self, coracle, stop_after=None):
+    def __init__(self, coracle, stop_after=None, corrupt=False):
         self.co = coracle
         self.calls = []
         self.stop_after = stop_after
+        self.corrupt = corrupt  # answer with a wrong trial value (a faulty device)
 
-    def bmpow_search(self, ih, target, start, max_trials, pn, pt):
+    def bmpow_search_len(self, ih, ih_len, target, start, max_trials, pn, pt):
+        assert len(ih) == ih_len
         self.calls.append((start, max_trials))
         if self.stop_after is not None and len(self.calls) >= self.stop_after:
             state.shutdown = 1
-        res = self.co.search(ih, target, start, max_trials)
+        res = self.co.search_len(ih, target, start, max_trials)
         if res is None:
             return _lib.NOT_FOUND
         pt._obj.value, pn._obj.value = res
+        if self.corrupt:
+            pt._obj.value ^= 1
         return _lib.FOUND
+
+    def bmpow_get_devices(self, ids, cap):
+        ids[0] = 0
+        return 1
 
     def bmpow_last_error(self):
         return b''
@@ -184,13 +197,74 @@ def test_negative_target_spins_until_shutdown(scripted):
     assert lib.calls == []
 
 
+def test_run_any_length_matches_reference(scripted, golden):
+    """run() over initialHashes that are not 64 bytes answers the reference's _doSafePoW (the
+    fixture, tests/golden/make_len_golden.py) through the bounded-call loop; the C oracle stands
+    in for the device."""
+    scripted()
+    for k in golden('len_kats.json')['first']:
+        ih = bytes.fromhex(k['ih'])
+        assert len(ih) == k['len']
+        assert proofofwork.run(k['target'], ih) == [k['trial'], k['nonce']], k['len']
+
+
+def test_wrong_gpu_answer_disables_the_backend(scripted, monkeypatch, caplog):
+    """A wrong answer disables the GPU backend as _doGPUPoW disables OpenCL
+    (src/proofofwork.py:176-190): the reference's error line, enabledGpus cleared, the UI told,
+    getPowType() 'none', later calls refused until resetPoW()."""
+    from pybitmessage_amd import hippow
+    lib = scripted(corrupt=True)
+    hippow.initCL()
+    assert hippow.openclEnabled()
+    seen = []
+    monkeypatch.setattr(proofofwork, 'ui_notify', seen.append)
+    ih = hashlib.sha512(b'hello').digest()
+    try:
+        with caplog.at_level('ERROR', logger='default'):
+            with pytest.raises(_lib.BmpowError, match='did not calculate correctly'):
+                proofofwork.run(2 ** 64 // 1000, ih)
+        assert 'did not calculate correctly, disabling OpenCL' in caplog.text
+        assert seen and 'disabling' in seen[0]
+        assert hippow.enabledGpus == [] and not hippow.openclEnabled()
+        assert proofofwork.getPowType() == 'none'
+        ncalls = len(lib.calls)
+        with pytest.raises(_lib.BmpowUnavailable, match='disabled'):
+            proofofwork.run(2 ** 64 // 1000, ih)
+        assert len(lib.calls) == ncalls  # refused before touching the device
+        with pytest.raises(_lib.BmpowUnavailable):
+            next(proofofwork.iter_batch([(2 ** 64 // 1000, ih)]))
+        # resetPoW re-enables (reference resetPoW -> openclpow.initCL)
+        lib.corrupt = False
+        monkeypatch.setattr(_lib, 'reset', lambda: None)
+        proofofwork.resetPoW()
+        assert hippow.openclEnabled() and proofofwork.getPowType() == 'HIP'
+        assert proofofwork.run(2 ** 64 // 1000, ih) == [2417842470843601, 1315]
+    finally:
+        proofofwork._disabled = None
+
+
+def test_do_opencl_pow_any_length_and_negative_target(scripted, golden):
+    """hippow.do_opencl_pow: the _doSafePoW nonce for a hex initialHash of any length, and a
+    negative target raises at once (the reference's numpy packing never blocks on it)."""
+    from pybitmessage_amd import hippow
+    scripted()
+    hippow.initCL()
+    for k in golden('len_kats.json')['first'][:12]:
+        assert hippow.do_opencl_pow(k['ih'], k['target']) == k['nonce']
+    with pytest.raises(ValueError):
+        hippow.do_opencl_pow('00' * 64, -1)
+
+
 def test_verify_rejects_wrong_gpu_answer():
     ih = hashlib.sha512(b'hello').digest()
-    proofofwork._verify(2 ** 64 // 1000, ih, 2417842470843601, 1315)
-    with pytest.raises(_lib.BmpowError):
-        proofofwork._verify(2 ** 64 // 1000, ih, 2417842470843602, 1315)
-    with pytest.raises(_lib.BmpowError):
-        proofofwork._verify(10, ih, 2417842470843601, 1315)
+    try:
+        proofofwork._verify(2 ** 64 // 1000, ih, 2417842470843601, 1315)
+        with pytest.raises(_lib.BmpowError):
+            proofofwork._verify(2 ** 64 // 1000, ih, 2417842470843602, 1315)
+        with pytest.raises(_lib.BmpowError):
+            proofofwork._verify(10, ih, 2417842470843601, 1315)
+    finally:
+        proofofwork._disabled = None
 
 
 def test_sender_targets_match_the_reference_expressions(golden):

@@ -31,6 +31,25 @@ def test_trial_kats_python_and_c(golden, coracle):
         assert coracle.trial(k['nonce'], ih) == k['trial']
 
 
+def test_any_length_kats_python_and_c(golden, coracle):
+    """initialHash lengths other than 64 (tests/golden/make_len_golden.py, the reference's own
+    _pool_worker and _doSafePoW): every SHA-512 block edge of the first hash's message."""
+    d = golden('len_kats.json')
+    assert {0, 1, 63, 65, 103, 104, 231, 232, 1000} <= set(d['lengths'])
+    for k in d['trial']:
+        ih = bytes.fromhex(k['ih'])
+        assert len(ih) == k['len']
+        assert oracle.trial(k['nonce'], ih) == k['trial']
+        assert coracle.trial_len(k['nonce'], ih) == k['trial']
+    for k in d['first']:
+        ih = bytes.fromhex(k['ih'])
+        assert oracle.safe_pow(k['target'], ih) == [k['trial'], k['nonce']]
+        assert coracle.search_len(ih, k['target']) == (k['trial'], k['nonce'])
+    # the 64-byte path of the any-length function is the fixed-layout one
+    ih = hashlib.sha512(b'hello').digest()
+    assert coracle.trial_len(1315, ih) == coracle.trial(1315, ih)
+
+
 def test_survey_appendix_trial_values(coracle):
     # SURVEY.md Appendix A, computed independently during the survey
     ih0 = bytes(64)

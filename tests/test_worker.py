@@ -386,6 +386,11 @@ def test_powservice_shutdown_and_errors(batchlib, coracle):
         batchlib.bad_tickets = {2}  # the service's third ticket: a wrong device answer
         with pytest.raises(_lib.BmpowError, match='re-check'):
             svc.submit(U64 // 10, bytes(64)).result(10)
+        # a wrong answer disables the backend (_doGPUPoW, src/proofofwork.py:176-190) until resetPoW
+        assert proofofwork.getPowType() == 'none'
+        with pytest.raises(_lib.BmpowUnavailable, match='disabled'):
+            svc.submit(U64 // 10, bytes(64)).result(10)
+        proofofwork._disabled = None  # what resetPoW() does besides re-selecting the devices
         ih = bytes(range(64))
         assert svc.submit(U64 // 10, ih).result(10) == list(coracle.search(ih, U64 // 10))
         pending = svc.submit(0, bytes(64))
@@ -418,23 +423,18 @@ def test_hippow_without_device(monkeypatch):
 
 def test_hippow_negative_target_never_searches(monkeypatch):
     """A negative target is unsatisfiable: do_opencl_pow must not wrap it into a u64 (which would
-    accept nonce 1) -- it waits, interruptibly, and never calls the search."""
+    accept nonce 1) -- it raises ValueError at once and never calls the search (the reference's
+    numpy packing raises or wraps; it never blocks)."""
     calls = []
 
     class Lib(object):
-        def bmpow_search(self, *a):
+        def bmpow_search_len(self, *a):
             calls.append(a)
             return _lib.FOUND
     monkeypatch.setattr(_lib, 'get', lambda: Lib())
     monkeypatch.setattr(hippow, 'enabledGpus', [0])
-    timer = threading.Timer(0.2, lambda: setattr(state, 'shutdown', 1))
-    timer.start()
-    try:
-        with pytest.raises(Exception, match='Interrupted'):
-            hippow.do_opencl_pow('00' * 64, -5)
-    finally:
-        timer.join()
-        state.shutdown = 0
+    with pytest.raises(ValueError, match='negative target'):
+        hippow.do_opencl_pow('00' * 64, -5)
     assert calls == []
 
 
