@@ -13,6 +13,7 @@ bench.py's own (``bench.make_objects``, rank 0), targets from class_singleWorker
 """
 import ctypes
 import hashlib
+import os
 import random
 
 import numpy as np
@@ -24,6 +25,17 @@ from pybitmessage_amd import _lib, proofofwork
 pytestmark = pytest.mark.gpu
 U64 = (1 << 64) - 1
 P64 = ctypes.POINTER(ctypes.c_uint64)
+# the C oracle's exact multi-threaded search on the host's CPUs (the GPU box's quota is 16)
+CPU_THREADS = max(1, min(16, os.cpu_count() or 1))
+
+
+def oracle_sample(coracle, objs, res, idx):
+    """objects idx solved again by the C oracle (bmo_search_mt: every nonce from 1, exact first
+    hit), a restatement that shares no code with the device: the same [trialValue, nonce]."""
+    for i in idx:
+        t, ih = objs[i]
+        got, _ = coracle.search_mt(ih, int(t), 1, res[i][1] + (1 << 20), threads=CPU_THREADS)
+        assert got == tuple(res[i]), (i, got, res[i])
 
 
 def assert_exact_first_nonces(lib, objs, res):
@@ -45,19 +57,21 @@ def assert_exact_first_nonces(lib, objs, res):
     return int(counts.sum()) + n
 
 
-def test_c2_full_batch(gpulib):
+def test_c2_full_batch(gpulib, coracle):
     """C2: 1,024 pending msg objects, L ~ U[512, 16384], default difficulty, TTL 4 d (~6e10
-    trials to solve and as many to prove)."""
+    trials to solve and as many to prove); 8 of them (seeded draw) also solved by the C oracle."""
     objs, _ = bench.make_objects('c2', 0)
     assert len(objs) == 1024
     res = proofofwork.run_batch(objs)
     hashed = assert_exact_first_nonces(gpulib, objs, res)
     assert hashed > 4e10
+    oracle_sample(coracle, objs, res, random.Random(2).sample(range(len(objs)), 8))
 
 
-def test_c4_nonce_sharded_eight_ways(gpulib, shards):
+def test_c4_nonce_sharded_eight_ways(gpulib, shards, coracle):
     """C4: 64 objects at 20x nonceTrialsPerByte, TTL 28 d (~1.5e9 trials each), nonce-sharded
-    over 8 shards with early exit (8 streams on this device; the same slicing as 8 GPUs)."""
+    over 8 shards with early exit (8 streams on this device; the same slicing as 8 GPUs); the
+    object with the smallest answer (~E/64 trials for the CPU) also solved by the C oracle."""
     shards([0] * 8)
     objs, _ = bench.make_objects('c4', 0)
     assert len(objs) == 64 and all(t == 11971972251 for t, _ in objs)
@@ -68,6 +82,7 @@ def test_c4_nonce_sharded_eight_ways(gpulib, shards):
     useful = sum(nonce for _, nonce in res)
     assert st.trials >= useful and (st.trials - useful) / st.trials < 0.05  # trials past the answers
     assert_exact_first_nonces(gpulib, objs, res)
+    oracle_sample(coracle, objs, res, [min(range(len(res)), key=lambda i: res[i][1])])
 
 
 def test_c5_flood_test_mode(gpulib, coracle):
@@ -81,6 +96,27 @@ def test_c5_flood_test_mode(gpulib, coracle):
     for i in random.Random(5).sample(range(len(objs)), 500):
         t, ih = objs[i]
         assert tuple(res[i]) == coracle.search(ih, t), i
+
+
+def test_c5_default_difficulty_slice(gpulib, shards, coracle):
+    """C5 at protocol-default difficulty (the flood's own targets, class_singleWorker.py:222-230:
+    acks L = 46, TTL 28 d, E ~ 4.0e7; pubkeys L = 200, TTL 4 d, E ~ 7.6e6): a 10,000-object slice of
+    bench.make_objects('c5', 0) with steps of 2^26 trials, so a step's 8,192 chunks are fewer than
+    the pending objects -- the 100k flood's regime, where each object spans thousands of chunks
+    over many steps (round 1's lost-work-item bug lived there).  Every answer proven minimal by the
+    min-trial probe; 20 of them (seeded draw) also solved by the C oracle."""
+    shards([0])
+    gpulib.bmpow_set_step_trials(1 << 26)
+    objs, _ = bench.make_objects('c5', 0)
+    objs = objs[:10000]
+    kinds = {t for t, _ in objs}
+    assert len(kinds) == 2 and min(kinds) > 4e11  # default difficulty, both object kinds
+    res = proofofwork.run_batch(objs)
+    gpulib.bmpow_set_step_trials(1 << 28)
+    hashed = assert_exact_first_nonces(gpulib, objs, res)
+    assert hashed > 1e11
+    rng = random.Random(55)
+    oracle_sample(coracle, objs, res, rng.sample(range(len(objs)), 20))
 
 
 @pytest.mark.slow
