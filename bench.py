@@ -475,7 +475,7 @@ def summarize_verify(args, dist, r, lib_version):
 
 
 def kernel_pmc(name):
-    """Counters of a kernel from the committed rocprofv3 PMC passes (tools/r02_pmc_verify_addr.sh ->
+    """Counters of a kernel from the committed rocprofv3 PMC passes (profiles/r02/scripts/r02_pmc_verify_addr.sh ->
     tools/pmc_kernel.py -> profiles/r02/pmc/<name>): per-launch HBM bytes (2 x FETCH_SIZE + WRITE_SIZE)
     and the VALU issue figures."""
     path = os.path.join(ROOT, 'profiles', 'r02', 'pmc', name)
@@ -502,18 +502,35 @@ def _verify_pool_worker(seconds):
     return k, time.perf_counter() - t0
 
 
-def cpu_verify_baseline(seconds):
-    """The reference's per-object check (protocol.py:280-282, targets.pow_value: hashlib, i.e.
-    OpenSSL) on the same flood, one process per CPU of the box's share, each hashing for
-    `seconds` (no pickling of objects: every worker builds the flood itself)."""
+def _verify_pool(seconds, p):
+    """In a fresh child process (cpu_baseline_worker, mode 'verify'): a pool of p processes, each
+    hashing the flood for `seconds`."""
     import multiprocessing
-    info = host_cpu_info()
-    p = info['share']
     with multiprocessing.get_context('fork').Pool(p) as pool:
         t0 = time.perf_counter()
         res = pool.map(_verify_pool_worker, [seconds] * p)
         wall = time.perf_counter() - t0
-    k = sum(r[0] for r in res)
+    return {'objects': sum(r[0] for r in res), 'wall': wall}
+
+
+def cpu_verify_baseline(seconds):
+    """The reference's per-object check (protocol.py:280-282, targets.pow_value: hashlib, i.e.
+    OpenSSL) on the same flood, one process per CPU of the box's share, each hashing for
+    `seconds` (no pickling of objects: every worker builds the flood itself).  The pool runs in a
+    fresh child process that never touches the GPU (HIP_VISIBLE_DEVICES=''), like the PoW legs: this
+    process has initialised HIP and the library's padding threads, which a fork must not inherit."""
+    info = host_cpu_info()
+    p = info['share']
+    cmd = [sys.executable, os.path.abspath(__file__), '--cpu-baseline-worker', '--cpu-seconds', str(seconds),
+           '--cpu-threads', str(p), '--cpu-mode', 'verify']
+    env = dict(os.environ)
+    env['HIP_VISIBLE_DEVICES'] = ''
+    out = subprocess.run(cmd, capture_output=True, text=True, timeout=seconds * 20 + 120, env=env)
+    line = [l for l in out.stdout.splitlines() if l.startswith('{')]
+    if out.returncode != 0 or not line:
+        return {'error': (out.stderr or out.stdout)[-400:], 'host': info}
+    r = json.loads(line[-1])
+    k, wall = r['objects'], r['wall']
     return {'value': round(k / wall, 1), 'unit': 'objects/s', 'cores': p, 'kind': 'port',
             'sample': '%d objects of the same flood hashed by hashlib (OpenSSL) in %.1f s wall on a pool of %d '
                       'processes' % (k, wall, p), 'host': info}
@@ -669,6 +686,9 @@ def cpu_baseline_worker(seconds, threads, mode):
     mode 'c': the reference's BitmessagePOW (oracle/_ref) on `threads` CPUs of the affinity mask
     (it sizes its pthread pool from that mask, bitmsghash.cpp:96,109-121); mode 'fast': the
     _doFastPoW mechanism (oracle/fastpow.py) with a pool of `threads` processes."""
+    if mode == 'verify':
+        print(json.dumps(_verify_pool(seconds, threads)), flush=True)
+        return
     cpus = sorted(os.sched_getaffinity(0))
     if mode == 'c':
         os.sched_setaffinity(0, cpus[:threads])
@@ -759,7 +779,7 @@ def main():
     ap.add_argument('--step-trials', type=int, default=0, help='per-launch trial budget per GPU (0 = lib default)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0)
     ap.add_argument('--cpu-threads', type=int, default=0, help='CPU-baseline threads (0 = the box\'s CPU share)')
-    ap.add_argument('--cpu-mode', default='c', choices=['c', 'fast'], help=argparse.SUPPRESS)
+    ap.add_argument('--cpu-mode', default='c', choices=['c', 'fast', 'verify'], help=argparse.SUPPRESS)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--share-device', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--devices', type=int, default=0,
@@ -771,8 +791,8 @@ def main():
     ap.add_argument('--run-batch', action='store_true',
                     help='c2/c5: through proofofwork.run_batch (the product entry point, host re-check included)')
     ap.add_argument('--service', action='store_true',
-                    help='c2/c5: feed the objects through worker.PowService (resident session, '
-                         'bmpow_batch_add/take_done) instead of one batch')
+                    help='c2/c5: feed the objects through worker.PowService (the library\'s continuous-batching '
+                         'service, bmpow_service_submit/poll) instead of one batch')
     ap.add_argument('--cpu-baseline-worker', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_baseline_worker:
@@ -860,14 +880,21 @@ def summarize(args, dist, r, lib_version):
         'performed_ghs': round(performed / el_max / 1e9, 4),
         'wasted_frac': round(1.0 - useful / performed, 5) if performed else None,
     }
-    if kernel_ms > 0:
-        achieved = OPS_PER_TRIAL * st.trials / (kernel_ms * 1e-3) / 1e12
-        kernel_ghs = st.trials / (kernel_ms * 1e-3) / 1e9
+    # per-GPU kernel rate, averaged over the ranks (each rank's device-counted trials over its own
+    # summed kernel time, HIP events on the launching stream); one rank: that GPU's
+    rank_ghs = st.trials / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
+    mean_ghs = dist.reduce(rank_ghs, 'sum') / dist.world
+    min_ghs = -dist.reduce(-rank_ghs, 'max')
+    if mean_ghs > 0:
+        kernel_ghs = mean_ghs
+        achieved = OPS_PER_TRIAL * kernel_ghs * 1e9 / 1e12
         line['roofline'] = {
             'bound': 'valu', 'kernel': 'bm_search_kernel',
             'achieved': round(achieved, 3), 'peak': round(PEAK_TOPS, 3),
             'unit': 'T int32 lane-ops/s (8,288 algorithmic ops per trial)',
             'frac': round(achieved / PEAK_TOPS, 4), 'traffic': None,
+            'scope': ('per GPU: one MI355X' if dist.world == 1 else
+                      'per GPU: mean over the %d ranks (min %.4f GH/s); peak is one GPU\'s' % (dist.world, min_ghs)),
             'kernel_ghs': round(kernel_ghs, 4),
             'avg_launch_ms': round(kernel_ms / max(launches, 1), 3), 'launches': int(launches),
             'kernel_busy_frac': round(kernel_ms * 1e-3 / r['elapsed'], 4),
@@ -884,11 +911,31 @@ def summarize(args, dist, r, lib_version):
                     'ghs': round(ceil, 4), 'frac': round(kernel_ghs / ceil, 4),
                     'basis': '1,024 SIMDs x one VALU instruction per quad-cycle x 64 lanes / VALU instructions '
                              'per trial (SQ_INSTS_VALU), at the PMC run clock (GRBM_GUI_ACTIVE / 8 / kernel time)'}
+                mix = mix_ceiling()
+                if mix:
+                    mceil = ceil * mix['valu_per_simd_quadcycle']
+                    line['roofline']['mix_ceiling'] = dict(mix, ghs=round(mceil, 4))
+                    line['roofline']['frac_vs_mix_ceiling'] = round(kernel_ghs / mceil, 4)
     if r.get('devices'):
         line['config']['parallelism'] = ('in-process nonce/object sharding over %d devices (bmpow_set_devices, '
                                          'host min-reduction, no collective)' % r['devices'])
         line['n_gpus'] = r['devices']
     return line
+
+
+def mix_ceiling():
+    """The issue ceiling of bm_search_kernel's own instruction mix (profiles/mix_ceiling.json, from
+    tools/ubench_mix.py on the GPU box): the kernel's nonce-loop VALU stream, opcode for opcode, with
+    its data dependences removed and every v_bitop3_b32 bank-split, at the kernel's 5 waves per SIMD
+    -- the most that mix can issue per SIMD per quad-cycle (best of the compiler's order, an even
+    spread and grouped bitop3)."""
+    path = os.path.join(ROOT, 'profiles', 'mix_ceiling.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    return {'valu_per_simd_quadcycle': d['ceiling_valu_per_simd_quadcycle'], 'waves_per_simd': d['waves_per_simd'],
+            'source': 'profiles/mix_ceiling.json (%s)' % d['source']}
 
 
 def pmc_counters():

@@ -95,9 +95,17 @@ struct Shard {
   uint32_t* d_vbins = nullptr;  // work bins of the binned verification kernel (grow-only)
   size_t vbins_cap = 0;
   int cus = 0;                  // compute units of the device (the binned kernel: 4 bins per CU)
+  uint32_t resident = 0;        // bm_search_kernel workgroups resident on the device (occupancy x CUs)
+  unsigned long long* d_xb = nullptr;  // the cross-shard bound table as this device addresses it
 };
 
 std::vector<Shard> g_shards;
+// The cross-shard bound (bmpow_layout.h): BM_MAX_SHARDS rows of BM_XSLOTS words, host-pinned, coherent
+// and mapped into every device; allocated with the shard set.
+unsigned long long* g_xb = nullptr;
+// Columns a work item may get per shard (slice's `resident`): the device's resident workgroups over
+// the shards sharing it, so every shard's sweep is on the chip at once.
+uint32_t g_resident = 0;
 bool g_inited = false;
 bmpow_stats g_stats{};
 
@@ -162,6 +170,7 @@ int make_shard(int dev, Shard& s) {
   HIPTRY(hipEventCreate(&s.ev0));
   HIPTRY(hipEventCreate(&s.ev1));
   HIPTRY(hipDeviceGetAttribute(&s.cus, hipDeviceAttributeMultiprocessorCount, dev));
+  s.resident = (uint32_t)std::max(1, bm_search_resident_per_cu()) * (uint32_t)s.cus;
   HIPTRY(hipMalloc(&s.d_trials, sizeof(unsigned long long)));
   HIPTRY(hipHostMalloc(&s.h_trials, sizeof(unsigned long long), hipHostMallocDefault));
   return ensure_items(s, 1024);
@@ -182,6 +191,7 @@ std::vector<int> visible_gfx950() {
 int select_devices(const std::vector<int>& ids) {
   for (auto& s : g_shards) free_shard(s);
   g_shards.clear();
+  if (ids.size() > BM_MAX_SHARDS) return set_err(BMPOW_E_ARG, "more than BM_MAX_SHARDS shards");
   const auto vis = visible_gfx950();
   for (int id : ids) {
     if (std::find(vis.begin(), vis.end(), id) == vis.end())
@@ -191,6 +201,21 @@ int select_devices(const std::vector<int>& ids) {
   for (size_t i = 0; i < ids.size(); ++i) {
     int rc = make_shard(ids[i], g_shards[i]);
     if (rc < 0) return rc;
+  }
+  if (!g_xb) {
+    HIPTRY(hipHostMalloc(&g_xb, sizeof(unsigned long long) * BM_MAX_SHARDS * BM_XSLOTS,
+                         hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
+    for (size_t i = 0; i < (size_t)BM_MAX_SHARDS * BM_XSLOTS; ++i) g_xb[i] = ~0ULL;
+  }
+  g_resident = ~0u;
+  for (auto& sh : g_shards) {
+    HIPTRY(hipSetDevice(sh.dev));
+    void* dp = nullptr;
+    HIPTRY(hipHostGetDevicePointer(&dp, g_xb, 0));
+    sh.d_xb = (unsigned long long*)dp;
+    const uint32_t same = (uint32_t)std::count_if(g_shards.begin(), g_shards.end(),
+                                                  [&](const Shard& o) { return o.dev == sh.dev; });
+    g_resident = std::min<uint32_t>(g_resident, std::max<uint32_t>(1, sh.resident / same));
   }
   return (int)g_shards.size();
 }
@@ -385,8 +410,13 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
   const size_t S = g_shards.size();
   // 1-2. windows for the pending objects, sliced over the shards (bmpow_sched.cpp)
   bmsched::StepPlan plan;
-  if (!bmsched::plan_step(*b, budget, g_step_trials, S, plan)) return 0;
-  const uint32_t iters = plan.iters;
+  if (!bmsched::plan_step(*b, budget, g_step_trials, S, plan, g_resident)) return 0;
+  // windows split over the shards share a running minimum through the cross-shard bound: their
+  // slots start empty in every row, before any launch of the step
+  for (size_t s = 0; s < S; ++s)
+    for (uint32_t x = 0; x < plan.nx; ++x)
+      __atomic_store_n(&g_xb[s * BM_XSLOTS + x], ~0ULL, __ATOMIC_RELAXED);
+  if (plan.nx) __atomic_thread_fence(__ATOMIC_SEQ_CST);
   {
     int rc = stage_items(plan);
     if (rc == 0) rc = sync_vpool(b);
@@ -401,12 +431,18 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     HIPTRY(hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream));
     HIPTRY(hipMemsetAsync(sh.d_trials, 0, sizeof(unsigned long long), sh.stream));
     HIPTRY(hipEventRecord(sh.ev0, sh.stream));
+    bm_xbound xb;
+    if (plan.nx) {
+      xb.table = sh.d_xb;
+      xb.row = (uint32_t)s;
+      xb.rows = (uint32_t)S;
+    }
     if (sh.nmain)
-      HIPTRY(bm_launch_search(sh.stream, sh.chmain, iters, b->dev[s].d_obj, sh.d_items, sh.nmain,
-                              b->dev[s].d_best, b->dev[s].d_found, sh.d_trials));
+      HIPTRY(bm_launch_search(sh.stream, sh.chmain, b->dev[s].d_obj, sh.d_items, sh.nmain, b->dev[s].d_best,
+                              b->dev[s].d_found, sh.d_trials, xb));
     if (sh.nitems > sh.nmain)
-      HIPTRY(bm_launch_search_var(sh.stream, sh.nchunks - sh.chmain, iters, b->dev[s].d_obj, sh.d_items + sh.nmain,
-                                  sh.nitems - sh.nmain, b->dev[s].d_best, b->dev[s].d_found, sh.d_trials,
+      HIPTRY(bm_launch_search_var(sh.stream, sh.nchunks - sh.chmain, b->dev[s].d_obj, sh.d_items + sh.nmain,
+                                  sh.nitems - sh.nmain, b->dev[s].d_best, b->dev[s].d_found, sh.d_trials, xb,
                                   b->dev[s].d_vpool));
     HIPTRY(hipEventRecord(sh.ev1, sh.stream));
     HIPTRY(bm_launch_resolve(sh.stream, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best,
@@ -507,7 +543,7 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
     uint64_t C = 0;
     if (!mt.plan(total_chunks, plan.wins, C)) break;
     bmsched::slice(plan.wins, C, BM_CHUNK, S, plan);
-    bmsched::split_kinds(objs, BM_CHUNK, any_var, plan);
+    bmsched::split_kinds(objs, any_var, plan);
     rc = stage_items(plan);
     if (rc < 0) break;
     for (size_t s = 0; s < S && rc == 0; ++s) {
@@ -520,9 +556,9 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
         e = hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream);
       if (e == hipSuccess) e = hipEventRecord(sh.ev0, sh.stream);
       if (e == hipSuccess && sh.nmain)
-        e = bm_launch_mintrial(sh.stream, sh.chmain, BM_ITERS, d_obj[s], sh.d_items, sh.nmain, sh.d_parts);
+        e = bm_launch_mintrial(sh.stream, sh.chmain, d_obj[s], sh.d_items, sh.nmain, sh.d_parts);
       if (e == hipSuccess && sh.nitems > sh.nmain)
-        e = bm_launch_mintrial_var(sh.stream, sh.nchunks - sh.chmain, BM_ITERS, d_obj[s], sh.d_items + sh.nmain,
+        e = bm_launch_mintrial_var(sh.stream, sh.nchunks - sh.chmain, d_obj[s], sh.d_items + sh.nmain,
                                    sh.nitems - sh.nmain, sh.d_parts + sh.chmain, d_vpool[s]);
       if (e == hipSuccess) e = hipEventRecord(sh.ev1, sh.stream);
       if (e == hipSuccess)
@@ -1160,6 +1196,8 @@ void bmpow_shutdown(void) {
   }
   for (auto& s : g_shards) free_shard(s);
   g_shards.clear();
+  if (g_xb) (void)hipHostFree(g_xb);
+  g_xb = nullptr;
   g_inited = false;
 }
 
@@ -1233,21 +1271,17 @@ int bmpow_search_len(const uint8_t* ih, size_t ih_len, uint64_t target, uint64_t
   if (rc < 0) return rc;
   bmpow_batch* b = g_scratch;
   uint64_t left = max_trials;
-  const uint64_t full = g_step_trials.load() * g_shards.size();
-  // The first step is sized to the object's expected trial count, 2^64 / (target + 1): an easy
-  // object does not launch (and drain) a full grid.  Steps then double up to the default; they
-  // cover consecutive windows, so exactness is unaffected.
-  const long double expect = 18446744073709551616.0L / ((long double)target + 1.0L);
-  const uint64_t floor_step = std::min<uint64_t>(full, (uint64_t)(1u << 23) * g_shards.size());
-  uint64_t step = expect * 2 >= (long double)full ? full : std::max<uint64_t>(floor_step, (uint64_t)(expect * 2));
-  step = (step + BM_CHUNK - 1) / BM_CHUNK * BM_CHUNK;
+  // Every step is a full one (2^28 trials per shard by default): the columns sweep the window as one
+  // front and stop one block row after the hit (bmpow_layout.h), so an easy object costs a row, not
+  // a drained grid -- no ramp of small first steps, no step tail.  Windows over several shards are
+  // capped near the expected trials by plan_step (expect_cap).
+  const uint64_t step = g_step_trials.load() * g_shards.size();
   while (left > 0) {
     // This step's window for the single object is `want` nonces rounded up to whole chunks;
     // a hit in the round-up tail lies beyond the caller's budget and is reported as
     // NOT_FOUND (the caller resumes at start + max_trials and finds it again: exactness
     // only needs every nonce below a reported hit to have been hashed).
     const uint64_t want = std::min(left, step);
-    step = std::min(full, step * 2);
     const uint64_t chunks = (want + BM_CHUNK - 1) / BM_CHUNK;
     const uint64_t st = b->next[0];
     rc = batch_step_locked(b, chunks * BM_CHUNK, nullptr);

@@ -5,15 +5,18 @@
 // src/bitmsghash/bitmsghash.cl:254-275 and the pthread loop bitmsghash.cpp:39-74.
 //
 // Execution model (one launch = one bounded "step" of the host scheduler, bmpow_host.hip):
-//   * the launch covers a list of work items; item = (object, contiguous nonce window);
-//   * each item is cut into CHUNKs of BM_BLOCK x BM_ITERS nonces; one workgroup per chunk;
-//     lane l of iteration i hashes nonce  chunk_first + i*BM_BLOCK + l;
+//   * the launch covers a list of work items; item = (object, nonce window, its columns);
+//   * the window is cut into blocks of BM_BLOCK nonces dealt round-robin to gn workgroup columns
+//     (bmpow_layout.h): column c, iteration i hashes block c + i*gn, lane l nonce
+//     start + (c + i*gn)*BM_BLOCK + l -- the columns sweep the window together, so the hashed set is
+//     always a prefix of the window plus at most one block row;
 //   * a hit does atomicMin(best[obj], nonce) -- the per-object minimum over the launch -- and
 //     sets found[obj]: best[] starts at UINT64_MAX, which is also a legal nonce (2^64-1), so
 //     "no hit" is found[obj] == 0, never a best[] value;
-//   * exact first-nonce semantics: a chunk whose first nonce is above best[obj] cannot
-//     hold the minimum, so it is skipped (checked at chunk start and after every iteration
-//     with an agent-scope load: the early exit never skips a nonce below the answer);
+//   * exact first-nonce semantics: a column whose next block starts above the running minimum
+//     cannot hold the answer, so it stops (checked at start and after every block with an
+//     agent-scope load: the early exit never skips a nonce below the answer); a window split over
+//     shards also reads the other shards' hits from the host-pinned cross-shard bound;
 //   * pure integer VALU -- no LDS, no MFMA, no HBM traffic beyond ~100 B per workgroup.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -34,15 +37,19 @@ using namespace bm;
 #ifndef BM_SEARCH_WAVES
 #define BM_SEARCH_WAVES 5
 #endif
+// kX: the launch holds windows split over shards (the cross-shard bound is read and written); the
+// other instantiation -- every step of one shard, every step with as many objects as shards -- carries
+// none of it in its loop.
+template <bool kX>
 __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(const bm_obj* __restrict__ objs,
                                                              const bm_item* __restrict__ items,
                                                              uint32_t nitems,
                                                              unsigned long long* __restrict__ best,
                                                              uint32_t* __restrict__ found,
                                                              unsigned long long* __restrict__ trials_done,
-                                                             uint32_t iters) {
+                                                             unsigned long long* __restrict__ xb,
+                                                             uint32_t xrow, uint32_t xrows) {
   const uint32_t b = blockIdx.x;
-  const uint64_t chunk = (uint64_t)BM_BLOCK * iters;  // nonces per workgroup in this launch
   // largest item index with chunk_base <= b (items sorted by chunk_base, uniform search)
   uint32_t lo = 0, hi = nitems;
   while (hi - lo > 1) {
@@ -50,12 +57,13 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
     if (items[mid].chunk_base <= b) lo = mid; else hi = mid;
   }
   const bm_item it = items[lo];
-  const uint64_t off = (uint64_t)(b - it.chunk_base) * chunk;
-  if (off >= it.count) return;
-  const uint64_t cnt = (it.count - off < chunk) ? (it.count - off) : chunk;
-  const uint64_t first = it.start + off;
+  const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;  // blocks of the window
+  const uint64_t gn = it.gn;
+  uint64_t blk = (uint64_t)it.g0 + (b - it.chunk_base);        // this workgroup's column
+  if (blk >= nblk) return;
   unsigned long long* bestp = best + it.obj;
-  if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < first) return;
+  const bool xs = kX && it.xslot != BM_NO_XSLOT;               // a window split over shards
+  if (bm_bound(bestp, xs, xb, it.xslot, xrows) < it.start + blk * BM_BLOCK) return;
 
 #ifdef BM_PRIO_MOD
   if (b % BM_PRIO_MOD == 0) __builtin_amdgcn_s_setprio(2);  // A/B knob: a share of the waves issue first
@@ -78,22 +86,23 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
   const uint64_t target = o->target;
 
   uint32_t done = 0;
-  for (uint32_t i = 0; i < iters; ++i) {
-    const uint64_t base = (uint64_t)i * BM_BLOCK;
-    if (base >= cnt) break;
-    // Early exit, one iteration of granularity at no stall: the running minimum is read
-    // before this iteration's hashing (its latency hides behind ~6,500 VALU instructions)
-    // and tested after it.  A value older by one iteration is only conservative.
-    const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t j = base + threadIdx.x;
-    const uint64_t nonce = first + j;
+  for (; blk < nblk; blk += gn) {
+    const uint64_t off = blk * BM_BLOCK;
+    const uint64_t first = it.start + off;
+    // Early exit, one block row of granularity at no stall: the running minimum is read before
+    // this block's hashing (its latency -- a PCIe round trip for the cross-shard bound -- hides
+    // behind ~6,500 VALU instructions) and tested after it.  A value older by one row is only
+    // conservative.
+    const uint64_t seen = bm_bound(bestp, xs, xb, it.xslot, xrows);
+    const uint64_t nonce = first + threadIdx.x;
     const uint64_t tv = trial_of(ihw, nonce);
-    if (j < cnt && tv <= target) {
-      atomicMin(bestp, (unsigned long long)nonce);
+    if (off + threadIdx.x < it.count && tv <= target) {
+      const unsigned long long prev = atomicMin(bestp, (unsigned long long)nonce);
       __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (kX && xs) bm_publish(bestp, xb + (size_t)xrow * BM_XSLOTS + it.xslot, prev < nonce ? prev : nonce);
     }
-    done += (cnt - base < BM_BLOCK) ? (uint32_t)(cnt - base) : BM_BLOCK;
-    if (seen < first + base + BM_BLOCK) break;  // every later nonce of this chunk is above it
+    done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
+    if (seen < first + gn * BM_BLOCK) break;  // every later block of this column is above it
   }
   if (threadIdx.x == 0) atomicAdd(trials_done, (unsigned long long)done);
 }
@@ -101,10 +110,20 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
 // ---------------------------------------------------------------------------------------
 // Launch wrappers (C++ linkage, used by bmpow_host.hip).
 // ---------------------------------------------------------------------------------------
-hipError_t bm_launch_search(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
-                            const bm_item* items, uint32_t nitems, unsigned long long* best, uint32_t* found,
-                            unsigned long long* trials_done) {
-  hipLaunchKernelGGL(bm_search_kernel, dim3(nchunks), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
-                     trials_done, iters);
+hipError_t bm_launch_search(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items, uint32_t nitems,
+                            unsigned long long* best, uint32_t* found, unsigned long long* trials_done,
+                            const bm_xbound& xb) {
+  if (xb.table)
+    hipLaunchKernelGGL(bm_search_kernel<true>, dim3(nwg), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
+                       trials_done, xb.table, xb.row, xb.rows);
+  else
+    hipLaunchKernelGGL(bm_search_kernel<false>, dim3(nwg), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
+                       trials_done, nullptr, 0u, 0u);
   return hipGetLastError();
+}
+
+int bm_search_resident_per_cu() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bm_search_kernel<false>, BM_BLOCK, 0) != hipSuccess) return 0;
+  return n;
 }

@@ -41,14 +41,37 @@ inline uint64_t bm_var_words(uint64_t len) { return 16 + 80 * (bm_var_blocks(len
 #define BMPOW_MAX_IH_LEN (1u << 20)  // longest initialHash the library accepts (1 MiB)
 #endif
 
-// Work item = one object's contiguous nonce window inside one launch (32 B).
+// Work item = one object's nonce window [start, start + count) inside one launch (48 B), cut into
+// blocks of BM_BLOCK nonces (one per lane).  The window's blocks are dealt to `gn` workgroup
+// COLUMNS: column c hashes blocks c, c + gn, c + 2 gn, ... in ascending order, so the columns sweep
+// the window together, one block row at a time, and a hit at nonce n leaves at most one row above
+// n in flight (each column stops at its next block above the running minimum).  This item runs
+// columns [g0, g0 + nwg) as its nwg workgroups; a window cut over several items (shards) has one
+// item per piece, each with its own g0 and the common gn.
+//   * a window on one shard: one item, g0 = 0, gn = nwg (capped at the shard's resident workgroups,
+//     so every column of the window is on the chip at once -- a persistent sweep);
+//   * a window split over the S shards (fewer pending objects than shards): one item per shard, all
+//     covering the whole window, interleaved: shard s runs columns [g0_s, g0_s + nwg_s) of gn = sum
+//     nwg_s -- so every device sweeps the same front -- and the shards share the window's running
+//     minimum through the cross-shard bound (xslot, below).
 struct bm_item {
   uint64_t start;       // first nonce of the window
-  uint64_t count;       // trials in the window (> 0; start + count - 1 <= 2^64 - 1)
+  uint64_t count;       // nonces in the window (> 0; start + count - 1 <= 2^64 - 1)
   uint32_t obj;         // object index (into bm_obj[] and best[])
-  uint32_t chunk_base;  // first chunk (workgroup) index of this item in the launch
+  uint32_t chunk_base;  // first workgroup of this item in its launch
+  uint32_t g0;          // first column of this item
+  uint32_t gn;          // columns of the window (over every item of the window)
+  uint32_t nwg;         // workgroups (columns) of this item
+  uint32_t xslot;       // cross-shard bound slot of a split window, or BM_NO_XSLOT
   uint64_t pad;
 };
+static_assert(sizeof(bm_item) == 48, "bm_item is 48 B");
+#define BM_NO_XSLOT 0xffffffffu
+// Cross-shard bound table: host-pinned, coherent, mapped into every device; row s (BM_XSLOTS words)
+// belongs to shard s, which stores its hits there (any hit of the window is a valid bound); every
+// shard's kernel reads all rows' slot of the window.  Split windows number fewer than the shards.
+#define BM_XSLOTS 64
+#define BM_MAX_SHARDS 64
 
 struct bm_result {
   uint64_t nonce;  // the object's minimum hit so far (meaningful only when found)

@@ -5,9 +5,9 @@
 // (src/proofofwork.py:100-111) iff trial(n) <= target and min{trial(m) : 1 <= m < n} > target.
 // It hashes every nonce of its range (no early exit, no target) and reduces instead of searching,
 // so it shares the trial function with bm_search_kernel but none of its hit/exit logic: a search
-// bug cannot hide behind the probe.  Layout and chunking are the search kernel's (bm_item list,
-// one workgroup per chunk of BM_BLOCK x iters nonces); each workgroup writes one bm_minpart and
-// the host reduces the parts per item.
+// bug cannot hide behind the probe.  Layout is the search kernel's (bm_item list, one workgroup per
+// column of an item, bmpow_layout.h); each workgroup writes one bm_minpart and the host reduces the
+// parts per item.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -32,31 +32,27 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int mask) {
 
 __global__ __launch_bounds__(BM_BLOCK) void bm_mintrial_kernel(const bm_obj* __restrict__ objs,
                                                                const bm_item* __restrict__ items,
-                                                               uint32_t nitems, bm_minpart* __restrict__ parts,
-                                                               uint32_t iters) {
+                                                               uint32_t nitems, bm_minpart* __restrict__ parts) {
   const uint32_t b = blockIdx.x;
-  const uint64_t chunk = (uint64_t)BM_BLOCK * iters;
   uint32_t lo = 0, hi = nitems;
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
     if (items[mid].chunk_base <= b) lo = mid; else hi = mid;
   }
   const bm_item it = items[lo];
-  const uint64_t off = (uint64_t)(b - it.chunk_base) * chunk;
+  const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
+  uint64_t blk = (uint64_t)it.g0 + (b - it.chunk_base);  // this workgroup's column (bmpow_layout.h)
   uint64_t bt = ~0ULL, bn = ~0ULL;  // no nonce of this lane (yet): sorts after every real pair
-  if (off < it.count) {
-    const uint64_t cnt = (it.count - off < chunk) ? (it.count - off) : chunk;
-    const uint64_t first = it.start + off;
+  if (blk < nblk) {
     const bm_obj* o = objs + it.obj;
     uint64_t ihw[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) ihw[i] = o->w[i];
-    for (uint32_t i = 0; i < iters; ++i) {
-      const uint64_t j = (uint64_t)i * BM_BLOCK + threadIdx.x;
-      if ((uint64_t)i * BM_BLOCK >= cnt) break;
-      const uint64_t nonce = first + j;
+    for (; blk < nblk; blk += it.gn) {
+      const uint64_t j = blk * BM_BLOCK + threadIdx.x;
+      const uint64_t nonce = it.start + j;
       const uint64_t tv = trial_of(ihw, nonce);
-      if (j < cnt && tv < bt) {  // ascending nonces per lane: strict < keeps the first
+      if (j < it.count && tv < bt) {  // ascending nonces per lane: strict < keeps the first
         bt = tv;
         bn = nonce;
       }
@@ -91,8 +87,8 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_mintrial_kernel(const bm_obj* __r
   }
 }
 
-hipError_t bm_launch_mintrial(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
-                              const bm_item* items, uint32_t nitems, bm_minpart* parts) {
-  hipLaunchKernelGGL(bm_mintrial_kernel, dim3(nchunks), dim3(BM_BLOCK), 0, st, objs, items, nitems, parts, iters);
+hipError_t bm_launch_mintrial(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items, uint32_t nitems,
+                              bm_minpart* parts) {
+  hipLaunchKernelGGL(bm_mintrial_kernel, dim3(nwg), dim3(BM_BLOCK), 0, st, objs, items, nitems, parts);
   return hipGetLastError();
 }

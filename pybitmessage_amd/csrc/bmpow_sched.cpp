@@ -231,12 +231,38 @@ void set_pending(BatchState& b, size_t first, size_t count, bool pending) {
 // ---------------------------------------------------------------------------------------
 // search steps
 // ---------------------------------------------------------------------------------------
-void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p) {
-  std::vector<uint64_t> cut(S + 1);
-  for (size_t s = 0; s <= S; ++s) cut[s] = C * s / S;
+void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident,
+           bool split) {
   p.items.assign(S, std::vector<bm_item>());
   p.nchunks.assign(S, 0);
-  for (size_t s = 0; s < S; ++s) p.nchunks[s] = (uint32_t)(cut[s + 1] - cut[s]);
+  p.nx = 0;
+  p.C = C;
+  if (split && S > 1) {
+    // every shard sweeps every window: G columns per shard and window, at least 4 blocks per column
+    const uint64_t share = resident ? std::max<uint64_t>(1, resident / std::max<size_t>(wins.size(), 1)) : ~0ULL;
+    for (const Win& w : wins) {
+      const uint64_t nblk = (w.count + BM_BLOCK - 1) / BM_BLOCK;
+      const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(share, (nblk + 4 * S - 1) / (4 * S)));
+      for (size_t s = 0; s < S; ++s) {
+        bm_item it;
+        std::memset(&it, 0, sizeof it);
+        it.start = w.start;
+        it.count = w.count;
+        it.obj = w.obj;
+        it.chunk_base = p.nchunks[s];
+        it.g0 = (uint32_t)(G * s);
+        it.gn = (uint32_t)(G * S);
+        it.nwg = (uint32_t)G;
+        it.xslot = p.nx < BM_XSLOTS ? p.nx : BM_NO_XSLOT;
+        p.items[s].push_back(it);
+        p.nchunks[s] += (uint32_t)G;
+      }
+      if (p.nx < BM_XSLOTS) ++p.nx;
+    }
+    return;
+  }
+  std::vector<uint64_t> cut(S + 1);
+  for (size_t s = 0; s <= S; ++s) cut[s] = C * s / S;
   size_t s = 0;
   for (const Win& w : wins) {
     uint64_t c = w.chunk0;
@@ -245,13 +271,21 @@ void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, S
       while (s < S && cut[s + 1] <= c) ++s;
       const uint64_t seg_end = std::min(cend, cut[s + 1]);
       bm_item it;
+      std::memset(&it, 0, sizeof it);
       const uint64_t off = (c - w.chunk0) * chunk;
       it.start = w.start + off;
       it.count = std::min<uint64_t>(w.count - off, (seg_end - c) * chunk);
       it.obj = w.obj;
-      it.chunk_base = (uint32_t)(c - cut[s]);
-      it.pad = 0;
+      it.chunk_base = p.nchunks[s];
+      const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
+      uint64_t G = std::min<uint64_t>(seg_end - c, nblk);
+      if (resident) G = std::min<uint64_t>(G, resident);
+      it.g0 = 0;
+      it.gn = (uint32_t)G;
+      it.nwg = (uint32_t)G;
+      it.xslot = BM_NO_XSLOT;
       p.items[s].push_back(it);
+      p.nchunks[s] += (uint32_t)G;
       c = seg_end;
     }
   }
@@ -266,7 +300,7 @@ uint64_t expect_cap(uint64_t target, size_t S, uint64_t chunk) {
   return cap < (double)floor_ ? floor_ : (cap >= 1.8e19 ? kU64Max : (uint64_t)cap);
 }
 
-bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p) {
+bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p, uint32_t resident) {
   while (b.first_pending < b.n && b.done[b.first_pending] != BMPOW_PENDING) ++b.first_pending;
   if (b.pending == 0) return false;
   if (budget == 0) budget = step_trials * S;
@@ -295,13 +329,12 @@ bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, S
     p.wins.push_back({(uint32_t)i, st, want, ch, acc});
     acc += ch;
   }
-  p.C = acc;
-  slice(p.wins, p.C, p.chunk, S, p);
-  split_kinds(b.objs, p.chunk, b.nvar_slots > 0, p);
+  slice(p.wins, acc, p.chunk, S, p, resident, split);
+  split_kinds(b.objs, b.nvar_slots > 0, p);
   return true;
 }
 
-void split_kinds(const std::vector<bm_obj>& objs, uint64_t chunk, bool any_var, StepPlan& p) {
+void split_kinds(const std::vector<bm_obj>& objs, bool any_var, StepPlan& p) {
   const size_t S = p.items.size();
   p.nmain.assign(S, 0);
   p.chmain.assign(S, 0);
@@ -318,7 +351,7 @@ void split_kinds(const std::vector<bm_obj>& objs, uint64_t chunk, bool any_var, 
     uint64_t cm = 0, cv = 0;
     for (const bm_item& it0 : v) {
       bm_item it = it0;
-      const uint64_t nch = (it.count + chunk - 1) / chunk;
+      const uint64_t nch = it.nwg;
       if (objs[it.obj].ihlen == BM_IH_MAIN) {
         it.chunk_base = (uint32_t)cm;
         cm += nch;
@@ -417,9 +450,8 @@ bool MinTrial::plan(uint64_t total_chunks, std::vector<Win>& wins, uint64_t& C) 
 
 void MinTrial::reduce_parts(const std::vector<bm_item>& items, const bm_minpart* parts, uint64_t* min_out,
                             uint64_t* argmin_out) {
-  const uint64_t chunk = BM_CHUNK;
   for (const bm_item& it : items) {
-    const uint64_t nch = (it.count + chunk - 1) / chunk;
+    const uint64_t nch = it.nwg;
     uint64_t& mt = min_out[it.obj];
     uint64_t& mn = argmin_out[it.obj];
     for (uint64_t c = it.chunk_base; c < it.chunk_base + nch; ++c) {

@@ -88,39 +88,49 @@ struct Win {
 };
 
 struct StepPlan {
-  uint32_t iters = 0;   // workgroup iterations (chunk = BM_BLOCK x iters nonces)
+  uint32_t iters = 0;   // planning unit: chunk = BM_BLOCK x iters nonces (a window is whole chunks)
   uint64_t chunk = 0;
-  uint64_t C = 0;       // chunks in the step
+  uint64_t C = 0;       // chunks planned in the step
   std::vector<Win> wins;                    // ascending object order
   std::vector<std::vector<bm_item>> items;  // per shard, ascending chunk_base
   std::vector<uint32_t> nchunks;            // per shard: workgroups of its launch(es)
   // after split_kinds: per shard, items[s][0, nmain[s]) are 64-byte objects (bm_search_kernel, chunk_base
-  // from 0, chmain[s] chunks) and the rest var-form objects (bm_search_var_kernel, chunk_base again from 0)
+  // from 0, chmain[s] workgroups) and the rest var-form objects (bm_search_var_kernel, chunk_base again
+  // from 0)
   std::vector<uint32_t> nmain, chmain;
+  uint32_t nx = 0;  // windows split over the shards: cross-shard bound slots [0, nx) (bmpow_layout.h)
 };
 
 // Reorder each shard's items into the two kernels' launches (see StepPlan); with any_var false every
 // item is 64-byte and nothing moves.
-void split_kinds(const std::vector<bm_obj>& objs, uint64_t chunk, bool any_var, StepPlan& p);
+void split_kinds(const std::vector<bm_obj>& objs, bool any_var, StepPlan& p);
 
-// Cut C chunks of windows (ascending chunk0) into S contiguous per-shard slices: big windows are
-// nonce-sharded, small ones object-sharded; each item's chunk_base is relative to its shard.
-void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p);
+// Deal the step's windows (C chunks, ascending chunk0) to S shards as work items (bmpow_layout.h).
+//   * default: the flattened chunk list is cut into S contiguous slices -- big windows are
+//     nonce-sharded, small ones object-sharded -- and each (window, shard) piece is one item whose
+//     columns sweep its sub-range; a piece gets at most `resident` workgroups (0 = no cap: one per
+//     chunk), the workgroups its shard keeps on the chip at once, so its sweep is one front;
+//   * split (fewer pending objects than shards, S > 1): every shard gets an item over each whole
+//     window, interleaved column by column (shard s runs columns [g0_s, g0_s + G) of S x G), so all
+//     devices sweep the same front, and the window's cross-shard bound slot (p.nx of them) lets a hit
+//     on one device stop the columns above it on every other.
+// chunk_base of each item is relative to its shard's launch.
+void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident = 0,
+           bool split = false);
 
-// With fewer pending objects than shards, each window is cut into contiguous per-shard slices, and a
-// shard whose slice lies above the object's first hit cannot know it: it hashes its slice up to a hit
-// of its own (~E trials) or its end.  So such a window is capped at kExpectWindows x E nonces (E =
-// 2^64 / (target + 1), the expected trials to a hit; at least one chunk per shard): a C1-sized object
-// (E ~ 1.3e7) over 8 GPUs takes a step of 2E / 8 nonces per GPU (13.5 % of the time a second one)
-// instead of 2^28-nonce slices.  With as many objects as shards or more, objects are object-sharded
-// and a shard's own early exit already stops at its object's hit: no cap (it would only add steps).
+// A window split over the shards is capped at kExpectWindows x E nonces (E = 2^64 / (target + 1), the
+// expected trials to a hit; at least one chunk per shard): a step then lasts about as long as the
+// object, and with the cross-shard bound the shards above a hit stop within a block row of it.  With
+// as many objects as shards or more, objects are object-sharded and a shard's own early exit stops at
+// its object's hit: no cap (it would only add steps).
 constexpr double kExpectWindows = 2.0;
 uint64_t expect_cap(uint64_t target, size_t S, uint64_t chunk);
 
 // Windows for the next step over S shards with about `budget` trials (0 = step_trials x S): pending
-// objects in slot order, k chunks each (capped by expect_cap when fewer than S are pending).
-// Returns false (p untouched) when nothing is pending.
-bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p);
+// objects in slot order, k chunks each (capped by expect_cap when fewer than S are pending), dealt by
+// slice (split mode when fewer than S objects are pending).  resident: as slice.  Returns false (p
+// untouched) when nothing is pending.
+bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p, uint32_t resident = 0);
 
 // Fold the step's per-shard results (res[s][k] for p.items[s][k]) into the state: the min over
 // shards of each object's hits is final (every lower nonce of its window was hashed); no hit moves

@@ -3,7 +3,7 @@
 // src/proofofwork.py:100-111; every caller in the reference passes a 64-byte digest, which
 // bm_search_kernel serves).
 //
-// Same execution model as bm_search_kernel (bmpow_kernels.hip): one workgroup per chunk of an
+// Same execution model as bm_search_kernel (bmpow_kernels.hip): workgroup columns sweeping an
 // item's nonce window, atomicMin of hits into best[obj], early exit above the running minimum.
 // Per object the message words come from the batch's var pool (bmsched::pack_var): block 0's
 // W1..W15 are loaded once per workgroup (loop-invariant, so their sigma terms are hoisted out of
@@ -45,39 +45,39 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_var_kernel(const bm_obj* _
                                                                  unsigned long long* __restrict__ best,
                                                                  uint32_t* __restrict__ found,
                                                                  unsigned long long* __restrict__ trials_done,
-                                                                 uint32_t iters,
+                                                                 unsigned long long* __restrict__ xb,
+                                                                 uint32_t xrow, uint32_t xrows,
                                                                  const uint64_t* __restrict__ vpool) {
-  const uint32_t b = blockIdx.x;
-  const uint64_t chunk = (uint64_t)BM_BLOCK * iters;
-  const bm_item it = items[item_of(items, nitems, b)];
-  const uint64_t off = (uint64_t)(b - it.chunk_base) * chunk;
-  if (off >= it.count) return;
-  const uint64_t cnt = (it.count - off < chunk) ? (it.count - off) : chunk;
-  const uint64_t first = it.start + off;
+  const bm_item it = items[item_of(items, nitems, blockIdx.x)];
+  const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
+  const uint64_t gn = it.gn;
+  uint64_t blk = (uint64_t)it.g0 + (blockIdx.x - it.chunk_base);
+  if (blk >= nblk) return;
   unsigned long long* bestp = best + it.obj;
-  if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < first) return;
+  const bool xs = xb != nullptr && it.xslot != BM_NO_XSLOT;
+  if (bm_bound(bestp, xs, xb, it.xslot, xrows) < it.start + blk * BM_BLOCK) return;
   const bm_obj* o = objs + it.obj;
   const uint64_t* m = vpool + o->vword;
-  const uint32_t nblk = o->nblk;
+  const uint32_t nb = o->nblk;
   const uint64_t target = o->target;
   uint64_t mw[16];
   mw[0] = 0;
 #pragma unroll
   for (int i = 1; i < 16; ++i) mw[i] = m[i];
   uint32_t done = 0;
-  for (uint32_t i = 0; i < iters; ++i) {
-    const uint64_t base = (uint64_t)i * BM_BLOCK;
-    if (base >= cnt) break;
-    const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t j = base + threadIdx.x;
-    const uint64_t nonce = first + j;
-    const uint64_t tv = trial_var(mw, m + 16, nblk, nonce);
-    if (j < cnt && tv <= target) {
-      atomicMin(bestp, (unsigned long long)nonce);
+  for (; blk < nblk; blk += gn) {
+    const uint64_t off = blk * BM_BLOCK;
+    const uint64_t first = it.start + off;
+    const uint64_t seen = bm_bound(bestp, xs, xb, it.xslot, xrows);
+    const uint64_t nonce = first + threadIdx.x;
+    const uint64_t tv = trial_var(mw, m + 16, nb, nonce);
+    if (off + threadIdx.x < it.count && tv <= target) {
+      const unsigned long long prev = atomicMin(bestp, (unsigned long long)nonce);
       __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (xs) bm_publish(bestp, xb + (size_t)xrow * BM_XSLOTS + it.xslot, prev < nonce ? prev : nonce);
     }
-    done += (cnt - base < BM_BLOCK) ? (uint32_t)(cnt - base) : BM_BLOCK;
-    if (seen < first + base + BM_BLOCK) break;
+    done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
+    if (seen < first + gn * BM_BLOCK) break;
   }
   if (threadIdx.x == 0) atomicAdd(trials_done, (unsigned long long)done);
 }
@@ -86,29 +86,25 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_var_kernel(const bm_obj* _
 __global__ __launch_bounds__(BM_BLOCK) void bm_mintrial_var_kernel(const bm_obj* __restrict__ objs,
                                                                    const bm_item* __restrict__ items,
                                                                    uint32_t nitems, bm_minpart* __restrict__ parts,
-                                                                   uint32_t iters,
                                                                    const uint64_t* __restrict__ vpool) {
   const uint32_t b = blockIdx.x;
-  const uint64_t chunk = (uint64_t)BM_BLOCK * iters;
   const bm_item it = items[item_of(items, nitems, b)];
-  const uint64_t off = (uint64_t)(b - it.chunk_base) * chunk;
+  const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
+  uint64_t blk = (uint64_t)it.g0 + (b - it.chunk_base);
   uint64_t bt = ~0ULL, bn = ~0ULL;
-  if (off < it.count) {
-    const uint64_t cnt = (it.count - off < chunk) ? (it.count - off) : chunk;
-    const uint64_t first = it.start + off;
+  if (blk < nblk) {
     const bm_obj* o = objs + it.obj;
     const uint64_t* m = vpool + o->vword;
-    const uint32_t nblk = o->nblk;
+    const uint32_t nb = o->nblk;
     uint64_t mw[16];
     mw[0] = 0;
 #pragma unroll
     for (int i = 1; i < 16; ++i) mw[i] = m[i];
-    for (uint32_t i = 0; i < iters; ++i) {
-      const uint64_t j = (uint64_t)i * BM_BLOCK + threadIdx.x;
-      if ((uint64_t)i * BM_BLOCK >= cnt) break;
-      const uint64_t nonce = first + j;
-      const uint64_t tv = trial_var(mw, m + 16, nblk, nonce);
-      if (j < cnt && tv < bt) {
+    for (; blk < nblk; blk += it.gn) {
+      const uint64_t j = blk * BM_BLOCK + threadIdx.x;
+      const uint64_t nonce = it.start + j;
+      const uint64_t tv = trial_var(mw, m + 16, nb, nonce);
+      if (j < it.count && tv < bt) {
         bt = tv;
         bn = nonce;
       }
@@ -142,17 +138,16 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_mintrial_var_kernel(const bm_obj*
   }
 }
 
-hipError_t bm_launch_search_var(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
-                                const bm_item* items, uint32_t nitems, unsigned long long* best, uint32_t* found,
-                                unsigned long long* trials_done, const uint64_t* vpool) {
-  hipLaunchKernelGGL(bm_search_var_kernel, dim3(nchunks), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
-                     trials_done, iters, vpool);
+hipError_t bm_launch_search_var(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items,
+                                uint32_t nitems, unsigned long long* best, uint32_t* found,
+                                unsigned long long* trials_done, const bm_xbound& xb, const uint64_t* vpool) {
+  hipLaunchKernelGGL(bm_search_var_kernel, dim3(nwg), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
+                     trials_done, xb.table, xb.row, xb.rows, vpool);
   return hipGetLastError();
 }
 
-hipError_t bm_launch_mintrial_var(hipStream_t st, uint32_t nchunks, uint32_t iters, const bm_obj* objs,
-                                  const bm_item* items, uint32_t nitems, bm_minpart* parts, const uint64_t* vpool) {
-  hipLaunchKernelGGL(bm_mintrial_var_kernel, dim3(nchunks), dim3(BM_BLOCK), 0, st, objs, items, nitems, parts, iters,
-                     vpool);
+hipError_t bm_launch_mintrial_var(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items,
+                                  uint32_t nitems, bm_minpart* parts, const uint64_t* vpool) {
+  hipLaunchKernelGGL(bm_mintrial_var_kernel, dim3(nwg), dim3(BM_BLOCK), 0, st, objs, items, nitems, parts, vpool);
   return hipGetLastError();
 }

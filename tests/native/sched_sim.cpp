@@ -117,6 +117,25 @@ static uint64_t sim_trial(const bm_obj& o, const std::vector<uint64_t>& vpool, u
   return bmo_trial(ih, nonce);
 }
 
+// The nonces an item's workgroups hash (bmpow_layout.h): columns [g0, g0 + nwg) of gn, column c taking
+// blocks c, c + gn, ... of BM_BLOCK nonces -- visited here in ascending nonce order (row by row), so
+// the first hit is the item's minimum, whatever the device's early exit skips above it.
+template <typename F>
+static void for_each_block(const bm_item& it, F&& fn) {
+  const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
+  for (uint64_t row = 0;; ++row) {
+    bool any = false;
+    for (uint64_t c = it.g0; c < (uint64_t)it.g0 + it.nwg; ++c) {
+      const uint64_t blk = row * it.gn + c;
+      if (blk >= nblk) continue;
+      any = true;
+      const uint64_t lo = blk * BM_BLOCK, hi = std::min<uint64_t>(it.count, lo + BM_BLOCK);
+      if (!fn(c - it.g0, it.start + lo, hi - lo)) return;
+    }
+    if (!any) return;
+  }
+}
+
 static void sim_step_shard(const std::vector<bm_obj>& objs, const std::vector<uint64_t>& vpool,
                            const std::vector<bm_item>& items, SimShard& sh) {
   if (sh.best.size() < objs.size()) {
@@ -124,14 +143,17 @@ static void sim_step_shard(const std::vector<bm_obj>& objs, const std::vector<ui
     sh.found.resize(objs.size(), 0);
   }
   for (const bm_item& it : items) {
-    for (uint64_t j = 0; j < it.count; ++j) {
-      const uint64_t n = it.start + j;
-      if (sim_trial(objs[it.obj], vpool, n) <= objs[it.obj].target) {
-        if (!sh.found[it.obj] || n < sh.best[it.obj]) sh.best[it.obj] = n;
-        sh.found[it.obj] = 1;
-        break;
+    for_each_block(it, [&](uint64_t, uint64_t first, uint64_t cnt) {
+      for (uint64_t j = 0; j < cnt; ++j) {
+        const uint64_t n = first + j;
+        if (sim_trial(objs[it.obj], vpool, n) <= objs[it.obj].target) {
+          if (!sh.found[it.obj] || n < sh.best[it.obj]) sh.best[it.obj] = n;
+          sh.found[it.obj] = 1;
+          return false;
+        }
       }
-    }
+      return true;
+    });
   }
   sh.res.resize(items.size());
   for (size_t k = 0; k < items.size(); ++k) {
@@ -150,12 +172,31 @@ static void sim_step_shard(const std::vector<bm_obj>& objs, const std::vector<ui
 }
 
 // One bounded step over S shards, one host thread per shard (as one stream per device).
-static bool sim_step(BatchState& b, std::vector<SimShard>& shards, uint64_t budget, uint64_t step_trials) {
+static bool sim_step(BatchState& b, std::vector<SimShard>& shards, uint64_t budget, uint64_t step_trials,
+                     uint32_t resident = 24) {
   StepPlan p;
-  if (!plan_step(b, budget, step_trials, shards.size(), p)) return false;
-  uint64_t chunks = 0;
-  for (size_t s = 0; s < shards.size(); ++s) chunks += p.nchunks[s];
-  CHECK(chunks == p.C, "shard chunks %llu != step chunks %llu", (unsigned long long)chunks, (unsigned long long)p.C);
+  if (!plan_step(b, budget, step_trials, shards.size(), p, resident)) return false;
+  // every window's columns [0, gn) are covered exactly once over the shards' items; a window split
+  // over the shards has one item per shard and a cross-shard bound slot of its own
+  for (size_t wi = 0; wi < p.wins.size(); ++wi) {
+    std::vector<std::pair<uint64_t, uint64_t>> cols;  // (start of the item's sub-range, column)
+    for (size_t s = 0; s < shards.size(); ++s)
+      for (const bm_item& it : p.items[s])
+        if (it.obj == p.wins[wi].obj) {
+          CHECK(it.nwg >= 1 && it.g0 + it.nwg <= it.gn && it.gn >= 1, "item columns");
+          CHECK(resident == 0 || it.nwg <= resident || it.xslot != BM_NO_XSLOT, "item above the resident cap");
+          for (uint32_t c = it.g0; c < it.g0 + it.nwg; ++c) cols.push_back({it.start, c});
+          if (it.xslot != BM_NO_XSLOT) CHECK(it.xslot < p.nx, "xslot %u of %u", it.xslot, p.nx);
+        }
+    std::sort(cols.begin(), cols.end());
+    CHECK(std::adjacent_find(cols.begin(), cols.end()) == cols.end(), "a column dealt twice (window %zu)", wi);
+  }
+  uint64_t wgs = 0, items_wg = 0;
+  for (size_t s = 0; s < shards.size(); ++s) {
+    wgs += p.nchunks[s];
+    for (const bm_item& it : p.items[s]) items_wg += it.nwg;
+  }
+  CHECK(wgs == items_wg, "launch workgroups %llu != items' %llu", (unsigned long long)wgs, (unsigned long long)items_wg);
   for (size_t s = 0; s < shards.size(); ++s) {
     // two launches per shard (split_kinds): 64-byte objects, then var-form ones, chunk_base from 0 in each
     uint64_t cm = 0, cv = 0;
@@ -165,7 +206,7 @@ static bool sim_step(BatchState& b, std::vector<SimShard>& shards, uint64_t budg
       CHECK(main_kind == (b.objs[it.obj].ihlen == BM_IH_MAIN), "item %zu of shard %zu in the wrong launch", k, s);
       uint64_t& c = main_kind ? cm : cv;
       CHECK(it.chunk_base == c, "chunk_base %u, want %llu", it.chunk_base, (unsigned long long)c);
-      c += (it.count + p.chunk - 1) / p.chunk;
+      c += it.nwg;
     }
     CHECK(cm == p.chmain[s] && cm + cv == p.nchunks[s], "shard %zu chunk totals", s);
   }
@@ -498,7 +539,7 @@ static void scenario_min_trial() {
     StepPlan p;
     uint64_t C = 0;
     while (mt.plan(9, p.wins, C)) {  // 9 chunks of BM_CHUNK per step: ranges span steps and shards
-      slice(p.wins, C, BM_CHUNK, S, p);
+      slice(p.wins, C, BM_CHUNK, S, p, S == 4 ? 3 : 0);  // with and without a column cap
       std::vector<std::thread> th;
       std::vector<std::vector<bm_minpart>> parts(S);
       for (size_t s = 0; s < S; ++s)
@@ -507,11 +548,14 @@ static void scenario_min_trial() {
           uint8_t ih[64];
           for (const bm_item& it : p.items[s]) {
             ih_of(ob[it.obj], ih);
-            for (uint64_t j = 0; j < it.count; ++j) {
-              bm_minpart& q = parts[s][it.chunk_base + j / BM_CHUNK];
-              const uint64_t t = bmo_trial(ih, it.start + j);
-              if (t < q.trial || (t == q.trial && it.start + j < q.nonce)) q = {t, it.start + j};
-            }
+            for_each_block(it, [&](uint64_t w, uint64_t first, uint64_t cnt) {
+              bm_minpart& q = parts[s][it.chunk_base + w];
+              for (uint64_t j = 0; j < cnt; ++j) {
+                const uint64_t t = bmo_trial(ih, first + j);
+                if (t < q.trial || (t == q.trial && first + j < q.nonce)) q = {t, first + j};
+              }
+              return true;
+            });
           }
         });
       for (auto& t : th) t.join();

@@ -1,7 +1,11 @@
 #!/usr/bin/env python3
 """Summarise tools/profile_pmc.sh output for bm_search_kernel (per launch, averaged).
 
-    python tools/pmc_summary.py gpurun_out/pmc_r01 [trials_per_launch]
+    python tools/pmc_summary.py gpurun_out/pmc_r01 [trials_per_launch] > profiles/pmc_latest.json
+
+The summary is stamped with the build it measured ("build"): the md5 of the libbmpow_hip.so the GPU
+box ran (OUTDIR/lib.md5, written by tools/profile_pmc.sh), the library's version string from the
+bench line, and the git commit checked out here when summarising.
 
 Derived (MI355X_MICROARCH.md conventions):
   * issued VALU instructions per trial = SQ_INSTS_VALU x 64 / trials
@@ -19,6 +23,7 @@ import collections
 import csv
 import json
 import os
+import subprocess
 import sys
 
 KERNEL = 'bm_search_kernel'
@@ -85,7 +90,23 @@ def main():
         res['write_kb_per_launch'] = out['WRITE_SIZE']
     if out.get('FETCH_SIZE') is not None and out.get('WRITE_SIZE') is not None:
         res['hbm_bytes_per_launch_upper'] = (2 * out['FETCH_SIZE'] + out['WRITE_SIZE']) * 1024
-    print(json.dumps({'raw': out, 'derived': res}, indent=1))
+    build = {}
+    md5 = os.path.join(root, 'lib.md5')
+    if os.path.exists(md5):
+        build['lib_md5'] = open(md5).read().split()[0]
+    for p in ['instr', 'kt']:
+        bj = os.path.join(root, p + '.bench.json')
+        if os.path.exists(bj):
+            lines = [l for l in open(bj) if l.startswith('{')]
+            if lines:
+                build['lib_version'] = json.loads(lines[-1]).get('config', {}).get('lib')
+                break
+    try:
+        build['git_head'] = subprocess.check_output(['git', 'rev-parse', '--short=12', 'HEAD'], text=True).strip()
+    except (OSError, subprocess.CalledProcessError):
+        pass
+    build['outdir'] = root
+    print(json.dumps({'build': build, 'raw': out, 'derived': res}, indent=1))
 
 
 if __name__ == '__main__':

@@ -8,6 +8,7 @@ OUT=${1:?outdir}
 LOG2=${2:-33}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
+md5sum pybitmessage_amd/lib/libbmpow_hip.so > "$OUT/lib.md5"
 CMD=(python3 bench.py --config c3 --c3-log2 "$LOG2" --steps 1 --warmup 0 --no-cpu-baseline)
 if [ -n "${PMC_DEFAULT_BENCH:-}" ]; then CMD=(python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline); fi
 pass() {
