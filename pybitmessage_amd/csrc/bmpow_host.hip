@@ -171,7 +171,7 @@ int make_shard(int dev, Shard& s) {
   HIPTRY(hipEventCreate(&s.ev1));
   HIPTRY(hipDeviceGetAttribute(&s.cus, hipDeviceAttributeMultiprocessorCount, dev));
   s.resident = (uint32_t)std::max(1, bm_search_resident_per_cu()) * (uint32_t)s.cus;
-  HIPTRY(hipMalloc(&s.d_trials, sizeof(unsigned long long)));
+  HIPTRY(hipMalloc(&s.d_trials, 2 * sizeof(unsigned long long)));  // trials, relay's finished columns
   HIPTRY(hipHostMalloc(&s.h_trials, sizeof(unsigned long long), hipHostMallocDefault));
   return ensure_items(s, 1024);
 }
@@ -429,7 +429,7 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     if (sh.nitems == 0) continue;
     HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream));
-    HIPTRY(hipMemsetAsync(sh.d_trials, 0, sizeof(unsigned long long), sh.stream));
+    HIPTRY(hipMemsetAsync(sh.d_trials, 0, 2 * sizeof(unsigned long long), sh.stream));
     HIPTRY(hipEventRecord(sh.ev0, sh.stream));
     bm_xbound xb;
     if (plan.nx) {
@@ -440,6 +440,8 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     if (sh.nmain)
       HIPTRY(bm_launch_search(sh.stream, sh.chmain, b->dev[s].d_obj, sh.d_items, sh.nmain, b->dev[s].d_best,
                               b->dev[s].d_found, sh.d_trials, xb));
+    if (sh.nitems > sh.nmain && sh.nmain && xb.table)  // the var launch's relay counts its own columns
+      HIPTRY(hipMemsetAsync(sh.d_trials + 1, 0, sizeof(unsigned long long), sh.stream));
     if (sh.nitems > sh.nmain)
       HIPTRY(bm_launch_search_var(sh.stream, sh.nchunks - sh.chmain, b->dev[s].d_obj, sh.d_items + sh.nmain,
                                   sh.nitems - sh.nmain, b->dev[s].d_best, b->dev[s].d_found, sh.d_trials, xb,

@@ -17,38 +17,56 @@ struct bm_xbound {
   uint32_t row = 0, rows = 0;
 };
 
-// Running minimum hit of an item's object as a column sees it: the device's own (agent scope: other
-// CUs' atomics through L2), and for a window split over shards every shard's published hit (system
-// scope: host-pinned memory, written by other devices).  Every value read is a real hit of the window
-// or UINT64_MAX, so it only ever stops columns above an answer.
-__device__ __forceinline__ uint64_t bm_bound(unsigned long long* bestp, bool xs, unsigned long long* xb,
-                                             uint32_t xslot, uint32_t xrows) {
-  uint64_t m = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (xs) {
-    for (uint32_t r = 0; r < xrows; ++r) {
-      const uint64_t v = __hip_atomic_load(xb + (size_t)r * BM_XSLOTS + xslot, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_SYSTEM);
-      m = v < m ? v : m;
-    }
-  }
-  return m;
-}
-
-// Publish this shard's running minimum of a split window to its slot of the cross-shard bound: a plain
-// system-scope store (no PCIe atomics), then re-read the device minimum and store again while it is
-// lower, so the last writer leaves the true minimum even when stores of two hits cross.
-__device__ __forceinline__ void bm_publish(unsigned long long* bestp, unsigned long long* slot, uint64_t v) {
+// Publish a hit of a split window: store this device's running minimum into the window's slot of
+// EVERY shard's row (plain system-scope vector stores, no PCIe atomics; a hit is rare, so the S stores
+// are too), then re-read the device minimum and store again while it is lower, so the last writer
+// leaves a value no larger than its device's minimum when stores of two hits cross.  Any value stored
+// is a real hit of the window, so a stale larger one only stops fewer columns.
+__device__ __forceinline__ void bm_publish(unsigned long long* bestp, unsigned long long* xb, uint32_t xslot,
+                                           uint32_t xrows, uint64_t v) {
   for (;;) {
-    __hip_atomic_store(slot, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    for (uint32_t r = 0; r < xrows; ++r)
+      __hip_atomic_store(xb + (size_t)r * BM_XSLOTS + xslot, (unsigned long long)v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
     const uint64_t now = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (now >= v) break;
     v = now;
   }
 }
 
+// The launch's relay of the cross-shard bound (workgroup 0 of a launch with split windows; one wave):
+// while the launch's columns run, it polls this shard's row of the table -- one system-scope load per
+// split window every few microseconds, not one per column and block -- and folds what the other shards
+// published into the device's own running minimum (atomicMin on best[obj]), which every column already
+// reads once per block from L2.  A value it folds in is a real hit of the window: the columns above it
+// stop, and the found[] flag stays the device's own, so the step's results are unchanged.  Exit: every
+// column has finished (cols_done, counted by each column workgroup as it ends), or 2^24 polls.
+__device__ __forceinline__ void bm_relay(const bm_item* __restrict__ items, uint32_t nitems,
+                                         unsigned long long* __restrict__ best, unsigned long long* xb,
+                                         uint32_t xrow, unsigned long long* cols_done, uint32_t ncols) {
+  if (threadIdx.x >= 64) return;
+  uint64_t seen = ~0ULL;  // lane k's last folded value for item k (k < 64)
+  for (uint32_t spin = 0; spin < (1u << 24); ++spin) {
+    if (__hip_atomic_load(cols_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ncols) break;
+    for (uint32_t k = threadIdx.x; k < nitems; k += 64) {
+      const bm_item& it = items[k];
+      if (it.xslot == BM_NO_XSLOT) continue;
+      const uint64_t v = __hip_atomic_load(xb + (size_t)xrow * BM_XSLOTS + it.xslot, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_SYSTEM);
+      if (v < seen || k >= 64) {
+        atomicMin(best + it.obj, (unsigned long long)v);
+        if (k < 64) seen = v;
+      }
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
 hipError_t bm_launch_search(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                             unsigned long long* best, uint32_t* found, unsigned long long* trials_done,
                             const bm_xbound& xb);
+// trials_done points at two counters: [0] trials hashed, [1] column workgroups finished (the relay's
+// exit; both zeroed before each launch).  With xb.table set, the grid is nwg + 1 workgroups (the relay).
 // workgroups of bm_search_kernel resident per CU (its occupancy): the columns a shard's window
 // gets at most, so a sweep is on the chip at once
 int bm_search_resident_per_cu();

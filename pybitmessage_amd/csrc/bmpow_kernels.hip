@@ -15,8 +15,9 @@
 //     "no hit" is found[obj] == 0, never a best[] value;
 //   * exact first-nonce semantics: a column whose next block starts above the running minimum
 //     cannot hold the answer, so it stops (checked at start and after every block with an
-//     agent-scope load: the early exit never skips a nonce below the answer); a window split over
-//     shards also reads the other shards' hits from the host-pinned cross-shard bound;
+//     agent-scope load: the early exit never skips a nonce below the answer); for a window split
+//     over shards the launch's relay workgroup folds the other shards' hits (the host-pinned
+//     cross-shard bound) into that running minimum;
 //   * pure integer VALU -- no LDS, no MFMA, no HBM traffic beyond ~100 B per workgroup.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -37,19 +38,13 @@ using namespace bm;
 #ifndef BM_SEARCH_WAVES
 #define BM_SEARCH_WAVES 5
 #endif
-// kX: the launch holds windows split over shards (the cross-shard bound is read and written); the
-// other instantiation -- every step of one shard, every step with as many objects as shards -- carries
-// none of it in its loop.
+// One column workgroup of a launch (bmpow_layout.h): the sweep of its item's blocks c, c + gn, ...
+// kX: the launch holds windows split over shards, whose hits are published to the cross-shard bound.
 template <bool kX>
-__global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(const bm_obj* __restrict__ objs,
-                                                             const bm_item* __restrict__ items,
-                                                             uint32_t nitems,
-                                                             unsigned long long* __restrict__ best,
-                                                             uint32_t* __restrict__ found,
-                                                             unsigned long long* __restrict__ trials_done,
-                                                             unsigned long long* __restrict__ xb,
-                                                             uint32_t xrow, uint32_t xrows) {
-  const uint32_t b = blockIdx.x;
+__device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
+                                              uint32_t nitems, unsigned long long* __restrict__ best,
+                                              uint32_t* __restrict__ found, unsigned long long* __restrict__ trials_done,
+                                              unsigned long long* __restrict__ xb, uint32_t xrows, uint32_t b) {
   // largest item index with chunk_base <= b (items sorted by chunk_base, uniform search)
   uint32_t lo = 0, hi = nitems;
   while (hi - lo > 1) {
@@ -62,8 +57,7 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
   uint64_t blk = (uint64_t)it.g0 + (b - it.chunk_base);        // this workgroup's column
   if (blk >= nblk) return;
   unsigned long long* bestp = best + it.obj;
-  const bool xs = kX && it.xslot != BM_NO_XSLOT;               // a window split over shards
-  if (bm_bound(bestp, xs, xb, it.xslot, xrows) < it.start + blk * BM_BLOCK) return;
+  if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it.start + blk * BM_BLOCK) return;
 
 #ifdef BM_PRIO_MOD
   if (b % BM_PRIO_MOD == 0) __builtin_amdgcn_s_setprio(2);  // A/B knob: a share of the waves issue first
@@ -89,22 +83,46 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
   for (; blk < nblk; blk += gn) {
     const uint64_t off = blk * BM_BLOCK;
     const uint64_t first = it.start + off;
-    // Early exit, one block row of granularity at no stall: the running minimum is read before
-    // this block's hashing (its latency -- a PCIe round trip for the cross-shard bound -- hides
-    // behind ~6,500 VALU instructions) and tested after it.  A value older by one row is only
-    // conservative.
-    const uint64_t seen = bm_bound(bestp, xs, xb, it.xslot, xrows);
+    // Early exit, one block row of granularity at no stall: the running minimum (for a split window
+    // also the other shards' hits, folded in by the launch's relay) is read before this block's
+    // hashing -- its latency hides behind ~6,500 VALU instructions -- and tested after it.  A value
+    // older by one row is only conservative.
+    const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t nonce = first + threadIdx.x;
     const uint64_t tv = trial_of(ihw, nonce);
     if (off + threadIdx.x < it.count && tv <= target) {
       const unsigned long long prev = atomicMin(bestp, (unsigned long long)nonce);
       __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (kX && xs) bm_publish(bestp, xb + (size_t)xrow * BM_XSLOTS + it.xslot, prev < nonce ? prev : nonce);
+      if (kX && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
     }
     done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
     if (seen < first + gn * BM_BLOCK) break;  // every later block of this column is above it
   }
   if (threadIdx.x == 0) atomicAdd(trials_done, (unsigned long long)done);
+}
+
+// kX = false: every launch without split windows (one shard; as many objects as shards) -- the hot
+// loop carries nothing of the cross-shard bound.  kX = true: workgroup 0 is the relay (bm_relay),
+// columns are workgroups 1.., and each column counts itself in trials_done[1] as it ends.
+template <bool kX>
+__global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(const bm_obj* __restrict__ objs,
+                                                             const bm_item* __restrict__ items,
+                                                             uint32_t nitems,
+                                                             unsigned long long* __restrict__ best,
+                                                             uint32_t* __restrict__ found,
+                                                             unsigned long long* __restrict__ trials_done,
+                                                             unsigned long long* __restrict__ xb,
+                                                             uint32_t xrow, uint32_t xrows) {
+  if constexpr (kX) {
+    if (blockIdx.x == 0) {
+      bm_relay(items, nitems, best, xb, xrow, trials_done + 1, gridDim.x - 1);
+      return;
+    }
+    search_column<true>(objs, items, nitems, best, found, trials_done, xb, xrows, blockIdx.x - 1);
+    if (threadIdx.x == 0) atomicAdd(trials_done + 1, 1ull);
+  } else {
+    search_column<false>(objs, items, nitems, best, found, trials_done, nullptr, 0, blockIdx.x);
+  }
 }
 
 // ---------------------------------------------------------------------------------------
@@ -114,7 +132,7 @@ hipError_t bm_launch_search(hipStream_t st, uint32_t nwg, const bm_obj* objs, co
                             unsigned long long* best, uint32_t* found, unsigned long long* trials_done,
                             const bm_xbound& xb) {
   if (xb.table)
-    hipLaunchKernelGGL(bm_search_kernel<true>, dim3(nwg), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
+    hipLaunchKernelGGL(bm_search_kernel<true>, dim3(nwg + 1), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
                        trials_done, xb.table, xb.row, xb.rows);
   else
     hipLaunchKernelGGL(bm_search_kernel<false>, dim3(nwg), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,

@@ -238,8 +238,10 @@ void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, S
   p.nx = 0;
   p.C = C;
   if (split && S > 1) {
-    // every shard sweeps every window: G columns per shard and window, at least 4 blocks per column
-    const uint64_t share = resident ? std::max<uint64_t>(1, resident / std::max<size_t>(wins.size(), 1)) : ~0ULL;
+    // every shard sweeps every window: G columns per shard and window, at least 4 blocks per column;
+    // one resident workgroup per shard is the launch's relay of the cross-shard bound (bm_relay)
+    const uint64_t share =
+        resident ? std::max<uint64_t>(1, (resident > 1 ? resident - 1 : 1) / std::max<size_t>(wins.size(), 1)) : ~0ULL;
     for (const Win& w : wins) {
       const uint64_t nblk = (w.count + BM_BLOCK - 1) / BM_BLOCK;
       const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(share, (nblk + 4 * S - 1) / (4 * S)));

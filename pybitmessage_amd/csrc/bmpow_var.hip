@@ -39,23 +39,19 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int mask) {
 
 }  // namespace
 
-__global__ __launch_bounds__(BM_BLOCK) void bm_search_var_kernel(const bm_obj* __restrict__ objs,
-                                                                 const bm_item* __restrict__ items,
-                                                                 uint32_t nitems,
-                                                                 unsigned long long* __restrict__ best,
-                                                                 uint32_t* __restrict__ found,
-                                                                 unsigned long long* __restrict__ trials_done,
-                                                                 unsigned long long* __restrict__ xb,
-                                                                 uint32_t xrow, uint32_t xrows,
-                                                                 const uint64_t* __restrict__ vpool) {
-  const bm_item it = items[item_of(items, nitems, blockIdx.x)];
+__device__ __forceinline__ void search_var_column(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
+                                                  uint32_t nitems, unsigned long long* __restrict__ best,
+                                                  uint32_t* __restrict__ found,
+                                                  unsigned long long* __restrict__ trials_done,
+                                                  unsigned long long* __restrict__ xb, uint32_t xrows,
+                                                  const uint64_t* __restrict__ vpool, uint32_t b) {
+  const bm_item it = items[item_of(items, nitems, b)];
   const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
   const uint64_t gn = it.gn;
-  uint64_t blk = (uint64_t)it.g0 + (blockIdx.x - it.chunk_base);
+  uint64_t blk = (uint64_t)it.g0 + (b - it.chunk_base);
   if (blk >= nblk) return;
   unsigned long long* bestp = best + it.obj;
-  const bool xs = xb != nullptr && it.xslot != BM_NO_XSLOT;
-  if (bm_bound(bestp, xs, xb, it.xslot, xrows) < it.start + blk * BM_BLOCK) return;
+  if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it.start + blk * BM_BLOCK) return;
   const bm_obj* o = objs + it.obj;
   const uint64_t* m = vpool + o->vword;
   const uint32_t nb = o->nblk;
@@ -68,18 +64,41 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_var_kernel(const bm_obj* _
   for (; blk < nblk; blk += gn) {
     const uint64_t off = blk * BM_BLOCK;
     const uint64_t first = it.start + off;
-    const uint64_t seen = bm_bound(bestp, xs, xb, it.xslot, xrows);
+    const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t nonce = first + threadIdx.x;
     const uint64_t tv = trial_var(mw, m + 16, nb, nonce);
     if (off + threadIdx.x < it.count && tv <= target) {
       const unsigned long long prev = atomicMin(bestp, (unsigned long long)nonce);
       __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (xs) bm_publish(bestp, xb + (size_t)xrow * BM_XSLOTS + it.xslot, prev < nonce ? prev : nonce);
+      if (xb && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
     }
     done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
     if (seen < first + gn * BM_BLOCK) break;
   }
   if (threadIdx.x == 0) atomicAdd(trials_done, (unsigned long long)done);
+}
+
+// xb set (split windows): workgroup 0 is the relay and columns are workgroups 1.., as in
+// bm_search_kernel<true>.
+__global__ __launch_bounds__(BM_BLOCK) void bm_search_var_kernel(const bm_obj* __restrict__ objs,
+                                                                 const bm_item* __restrict__ items,
+                                                                 uint32_t nitems,
+                                                                 unsigned long long* __restrict__ best,
+                                                                 uint32_t* __restrict__ found,
+                                                                 unsigned long long* __restrict__ trials_done,
+                                                                 unsigned long long* __restrict__ xb,
+                                                                 uint32_t xrow, uint32_t xrows,
+                                                                 const uint64_t* __restrict__ vpool) {
+  if (xb) {
+    if (blockIdx.x == 0) {
+      bm_relay(items, nitems, best, xb, xrow, trials_done + 1, gridDim.x - 1);
+      return;
+    }
+    search_var_column(objs, items, nitems, best, found, trials_done, xb, xrows, vpool, blockIdx.x - 1);
+    if (threadIdx.x == 0) atomicAdd(trials_done + 1, 1ull);
+  } else {
+    search_var_column(objs, items, nitems, best, found, trials_done, nullptr, 0, vpool, blockIdx.x);
+  }
 }
 
 // Min-trial probe over var-form objects: bm_mintrial_kernel (bmpow_mintrial.hip) with trial_var.
@@ -141,8 +160,8 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_mintrial_var_kernel(const bm_obj*
 hipError_t bm_launch_search_var(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items,
                                 uint32_t nitems, unsigned long long* best, uint32_t* found,
                                 unsigned long long* trials_done, const bm_xbound& xb, const uint64_t* vpool) {
-  hipLaunchKernelGGL(bm_search_var_kernel, dim3(nwg), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
-                     trials_done, xb.table, xb.row, xb.rows, vpool);
+  hipLaunchKernelGGL(bm_search_var_kernel, dim3(nwg + (xb.table ? 1 : 0)), dim3(BM_BLOCK), 0, st, objs, items, nitems,
+                     best, found, trials_done, xb.table, xb.row, xb.rows, vpool);
   return hipGetLastError();
 }
 

@@ -119,6 +119,31 @@ def test_c5_default_difficulty_slice(gpulib, shards, coracle):
     oracle_sample(coracle, objs, res, rng.sample(range(len(objs)), 20))
 
 
+# bm_search_kernel workgroups resident on one MI355X (5 per CU at 96 VGPRs x 256 CUs): the columns
+# of a window's sweep (bmpow_layout.h), one block row = ROW nonces
+ROW = 1280 * 256
+
+
+@pytest.mark.parametrize('nshards', [1, 8])
+def test_c1_sweep_stops_within_rows_of_the_hit(gpulib, shards, golden, nshards):
+    """One C1 object (1 KB msg at defaults, golden nonce 10,909,138) on one shard, and nonce-split
+    over 8 shards (8 streams on this device, the slicing of 8 GPUs): the window's columns sweep it
+    as one front, and over 8 shards the host-pinned cross-shard bound stops every shard's columns
+    at the first hit of any, so the trials hashed past the answer stay within a few block rows of
+    the sweep -- round 2, with contiguous per-shard slices and no cross-shard bound, hashed 24 M
+    trials over 8 shards for the 10.9 M useful ones (profiles/r02/expect_cap/capped.json)."""
+    shards([0] * nshards)
+    k = [k for k in golden('first_nonce_kats.json')['kats'] if k['nonce'] == 10909138][0]
+    ih = bytes.fromhex(k['ih'])
+    for _ in range(3):
+        gpulib.bmpow_reset_stats()
+        assert proofofwork.run(k['target'], ih) == [k['trial'], k['nonce']]
+        st = _lib.BmpowStats()
+        gpulib.bmpow_get_stats(ctypes.byref(st))
+        assert st.trials >= k['nonce'] - 1
+        assert st.trials - k['nonce'] <= 4 * ROW, (st.trials, st.steps)
+
+
 @pytest.mark.slow
 def test_c3_sweep_2_38_no_hit(gpulib):
     """C3: fixed initialHash, target 0, 2^38 nonces: no hit, and the device hashes exactly 2^38
