@@ -76,6 +76,12 @@ BMPOW_API int bmpow_set_device_count(int ndev);
 /* Copy the active shard -> device map into ids[0..cap); returns the shard count. */
 BMPOW_API int bmpow_get_devices(int *ids, int cap);
 
+/* Per-shard search throughput the step planner weights its slices by (trials per ms, an
+ * exponential average over launches of >= 2^24 trials; 0 = no sample yet) into rates[0..cap);
+ * returns the shard count.  A shard's share of a multi-shard step is its rate over the mean,
+ * clamped to [1/2, 2], once every shard has a sample (equal shares before). */
+BMPOW_API int bmpow_get_shard_rates(double *rates, int cap);
+
 /* Release all device memory and streams (bmpow_init may be called again). */
 BMPOW_API void bmpow_shutdown(void);
 

@@ -73,6 +73,7 @@ SIGNATURES = [
     ('bmpow_set_devices', ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ('bmpow_set_device_count', ctypes.c_int, [ctypes.c_int]),
     ('bmpow_get_devices', ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ('bmpow_get_shard_rates', ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ('bmpow_shutdown', None, []),
     ('bmpow_last_error', ctypes.c_char_p, []),
     ('bmpow_version', ctypes.c_char_p, []),

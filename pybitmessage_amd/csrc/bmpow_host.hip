@@ -64,6 +64,7 @@ struct Shard {
   bm_item* d_items = nullptr;
   bm_result* d_res = nullptr;
   unsigned long long* d_trials = nullptr;
+  unsigned long long* d_queue = nullptr;  // per item: the next block of its window to hand out (bmpow_kernels.h)
   bm_item* h_items = nullptr;      // pinned
   bm_result* h_res = nullptr;      // pinned
   unsigned long long* h_trials = nullptr;  // pinned
@@ -106,6 +107,8 @@ unsigned long long* g_xb = nullptr;
 // Columns a work item may get per shard (slice's `resident`): the device's resident workgroups over
 // the shards sharing it, so every shard's sweep is on the chip at once.
 uint32_t g_resident = 0;
+// per-shard throughput of the search launches: the weights of the next step's slices (bmpow_sched.h)
+bmsched::ShardRates g_rates;
 bool g_inited = false;
 bmpow_stats g_stats{};
 
@@ -126,9 +129,11 @@ int ensure_items(Shard& s, size_t n) {
   if (s.d_items) {
     HIPTRY(hipFree(s.d_items));
     HIPTRY(hipFree(s.d_res));
+    HIPTRY(hipFree(s.d_queue));
     HIPTRY(hipHostFree(s.h_res));
   }
   HIPTRY(hipMalloc(&s.d_items, cap * sizeof(bm_item)));
+  HIPTRY(hipMalloc(&s.d_queue, cap * sizeof(unsigned long long)));
   HIPTRY(hipMalloc(&s.d_res, cap * sizeof(bm_result)));
   HIPTRY(hipHostMalloc(&s.h_res, cap * sizeof(bm_result), hipHostMallocDefault));
   s.item_cap = cap;
@@ -140,6 +145,7 @@ void free_shard(Shard& s) {
   (void)hipSetDevice(s.dev);
   if (s.d_items) (void)hipFree(s.d_items);
   if (s.d_res) (void)hipFree(s.d_res);
+  if (s.d_queue) (void)hipFree(s.d_queue);
   if (s.d_trials) (void)hipFree(s.d_trials);
   if (s.h_items) (void)hipHostFree(s.h_items);
   if (s.h_res) (void)hipHostFree(s.h_res);
@@ -171,6 +177,8 @@ int make_shard(int dev, Shard& s) {
   HIPTRY(hipEventCreate(&s.ev1));
   HIPTRY(hipDeviceGetAttribute(&s.cus, hipDeviceAttributeMultiprocessorCount, dev));
   s.resident = (uint32_t)std::max(1, bm_search_resident_per_cu()) * (uint32_t)s.cus;
+  if (const char* e = std::getenv("BMPOW_COLUMNS"))  // A/B knob: columns per shard and window
+    if (std::atoi(e) > 0) s.resident = (uint32_t)std::atoi(e);
   HIPTRY(hipMalloc(&s.d_trials, 2 * sizeof(unsigned long long)));  // trials, relay's finished columns
   HIPTRY(hipHostMalloc(&s.h_trials, sizeof(unsigned long long), hipHostMallocDefault));
   return ensure_items(s, 1024);
@@ -208,6 +216,7 @@ int select_devices(const std::vector<int>& ids) {
     for (size_t i = 0; i < (size_t)BM_MAX_SHARDS * BM_XSLOTS; ++i) g_xb[i] = ~0ULL;
   }
   g_resident = ~0u;
+  g_rates.reset(g_shards.size());
   for (auto& sh : g_shards) {
     HIPTRY(hipSetDevice(sh.dev));
     void* dp = nullptr;
@@ -410,7 +419,9 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
   const size_t S = g_shards.size();
   // 1-2. windows for the pending objects, sliced over the shards (bmpow_sched.cpp)
   bmsched::StepPlan plan;
-  if (!bmsched::plan_step(*b, budget, g_step_trials, S, plan, g_resident)) return 0;
+  std::vector<double> w;
+  const bool weighted = S > 1 && g_rates.weights(w);
+  if (!bmsched::plan_step(*b, budget, g_step_trials, S, plan, g_resident, weighted ? w.data() : nullptr)) return 0;
   // windows split over the shards share a running minimum through the cross-shard bound: their
   // slots start empty in every row, before any launch of the step
   for (size_t s = 0; s < S; ++s)
@@ -423,13 +434,20 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     if (rc < 0) return rc;
   }
 
-  // 3. launch on every shard, then collect
+  // 3. stage every shard's items and counters, then launch on every shard back to back (the shards of a
+  // split window sweep the same rows, so their kernels should start together), then collect
   for (size_t s = 0; s < S; ++s) {
     Shard& sh = g_shards[s];
     if (sh.nitems == 0) continue;
     HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream));
     HIPTRY(hipMemsetAsync(sh.d_trials, 0, 2 * sizeof(unsigned long long), sh.stream));
+    HIPTRY(hipMemsetAsync(sh.d_queue, 0, sh.nitems * sizeof(unsigned long long), sh.stream));
+  }
+  for (size_t s = 0; s < S; ++s) {
+    Shard& sh = g_shards[s];
+    if (sh.nitems == 0) continue;
+    HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(hipEventRecord(sh.ev0, sh.stream));
     bm_xbound xb;
     if (plan.nx) {
@@ -439,14 +457,19 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     }
     if (sh.nmain)
       HIPTRY(bm_launch_search(sh.stream, sh.chmain, b->dev[s].d_obj, sh.d_items, sh.nmain, b->dev[s].d_best,
-                              b->dev[s].d_found, sh.d_trials, xb));
+                              b->dev[s].d_found, sh.d_trials, sh.d_queue, xb));
     if (sh.nitems > sh.nmain && sh.nmain && xb.table)  // the var launch's relay counts its own columns
       HIPTRY(hipMemsetAsync(sh.d_trials + 1, 0, sizeof(unsigned long long), sh.stream));
     if (sh.nitems > sh.nmain)
       HIPTRY(bm_launch_search_var(sh.stream, sh.nchunks - sh.chmain, b->dev[s].d_obj, sh.d_items + sh.nmain,
-                                  sh.nitems - sh.nmain, b->dev[s].d_best, b->dev[s].d_found, sh.d_trials, xb,
-                                  b->dev[s].d_vpool));
+                                  sh.nitems - sh.nmain, b->dev[s].d_best, b->dev[s].d_found, sh.d_trials,
+                                  sh.d_queue + sh.nmain, xb, b->dev[s].d_vpool));
     HIPTRY(hipEventRecord(sh.ev1, sh.stream));
+  }
+  for (size_t s = 0; s < S; ++s) {
+    Shard& sh = g_shards[s];
+    if (sh.nitems == 0) continue;
+    HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(bm_launch_resolve(sh.stream, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best,
                              b->dev[s].d_found, sh.d_res, b->dev[s].d_vpool));
     HIPTRY(hipMemcpyAsync(sh.h_res, sh.d_res, sh.nitems * sizeof(bm_result), hipMemcpyDeviceToHost, sh.stream));
@@ -466,6 +489,7 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     g_stats.launches++;
     step_max_ms = std::max<double>(step_max_ms, ms);
     step_trials += *sh.h_trials;
+    g_rates.sample(s, *sh.h_trials, ms);
   }
   g_stats.trials += step_trials;
   g_stats.steps++;
@@ -1186,6 +1210,13 @@ int bmpow_set_device_count(int ndev) {
 int bmpow_get_devices(int* ids, int cap) {
   std::lock_guard<std::mutex> lk(g_mu);
   for (int i = 0; i < (int)g_shards.size() && i < cap; ++i) ids[i] = g_shards[i].dev;
+  return (int)g_shards.size();
+}
+
+int bmpow_get_shard_rates(double* rates, int cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (int i = 0; i < (int)g_shards.size() && i < cap; ++i)
+    rates[i] = i < (int)g_rates.ema.size() ? g_rates.ema[i] : 0.0;
   return (int)g_shards.size();
 }
 

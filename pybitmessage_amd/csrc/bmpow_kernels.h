@@ -62,9 +62,30 @@ __device__ __forceinline__ void bm_relay(const bm_item* __restrict__ items, uint
   }
 }
 
+// The block queue of a work item (round 3).  A static column layout (column c hashing blocks c,
+// c + gn, ...) keeps the columns in step only while every column progresses at the same rate, and
+// they do not: the SIMD's arbiter favours its older waves, so of five column workgroups sharing a
+// SIMD the oldest runs several times faster than the youngest.  A lone C1 object on one shard
+// (1,280 columns) hashed 29 M trials for its 10.9 M useful, and 62.7 M with 1,024 columns
+// (profiles/r03/c1_columns_static.jsonl): the column holding the answer lagged dozens of rows behind the
+// fast ones.  So an item's workgroups now take its blocks IN ORDER from a per-item counter
+// (queue[item], zeroed before each launch): the k-th block taken is the k-th block of the item's
+// own columns, row by row, and the hashed set is always a prefix of the item's blocks plus the
+// blocks in flight, however unevenly the workgroups run.  A workgroup fetches its next block while
+// it hashes the current one (lane 0's atomicAdd, ~1 per 256 trials: 26 M/s device-wide for one
+// item, against 83 M/s measured for one address, profiles/r03/atomic_rate.jsonl) and shares it
+// through LDS at one barrier per block.
+// A window on one shard (every item with gn == nwg has g0 == 0) takes its blocks as they come; only a
+// window split over shards maps through its columns (a uniform 64-bit division, once per block).
+__device__ __forceinline__ uint64_t bm_block_of(const bm_item& it, uint64_t k) {
+  if (it.gn == it.nwg) return k;
+  const uint64_t row = k / it.nwg;
+  return row * it.gn + it.g0 + (k - row * it.nwg);
+}
+
 hipError_t bm_launch_search(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                             unsigned long long* best, uint32_t* found, unsigned long long* trials_done,
-                            const bm_xbound& xb);
+                            unsigned long long* queue, const bm_xbound& xb);
 // trials_done points at two counters: [0] trials hashed, [1] column workgroups finished (the relay's
 // exit; both zeroed before each launch).  With xb.table set, the grid is nwg + 1 workgroups (the relay).
 // workgroups of bm_search_kernel resident per CU (its occupancy): the columns a shard's window
@@ -72,7 +93,8 @@ hipError_t bm_launch_search(hipStream_t st, uint32_t nwg, const bm_obj* objs, co
 int bm_search_resident_per_cu();
 hipError_t bm_launch_search_var(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items,
                                 uint32_t nitems, unsigned long long* best, uint32_t* found,
-                                unsigned long long* trials_done, const bm_xbound& xb, const uint64_t* vpool);
+                                unsigned long long* trials_done, unsigned long long* queue, const bm_xbound& xb,
+                                const uint64_t* vpool);
 // vpool: the batch's var pool (may be null when no object of the launch is var-form)
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                              const unsigned long long* best, const uint32_t* found, bm_result* res,

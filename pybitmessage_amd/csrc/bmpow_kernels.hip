@@ -38,13 +38,15 @@ using namespace bm;
 #ifndef BM_SEARCH_WAVES
 #define BM_SEARCH_WAVES 5
 #endif
-// One column workgroup of a launch (bmpow_layout.h): the sweep of its item's blocks c, c + gn, ...
+// One workgroup of a launch: it takes blocks of its item from the item's queue (bm_block_of), in
+// order, until the window ends or the next block lies above the running minimum.
 // kX: the launch holds windows split over shards, whose hits are published to the cross-shard bound.
 template <bool kX>
 __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
                                               uint32_t nitems, unsigned long long* __restrict__ best,
                                               uint32_t* __restrict__ found, unsigned long long* __restrict__ trials_done,
-                                              unsigned long long* __restrict__ xb, uint32_t xrows, uint32_t b) {
+                                              unsigned long long* __restrict__ queue, unsigned long long* __restrict__ xb,
+                                              uint32_t xrows, uint32_t b) {
   // largest item index with chunk_base <= b (items sorted by chunk_base, uniform search)
   uint32_t lo = 0, hi = nitems;
   while (hi - lo > 1) {
@@ -53,10 +55,13 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
   }
   const bm_item it = items[lo];
   const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;  // blocks of the window
-  const uint64_t gn = it.gn;
-  uint64_t blk = (uint64_t)it.g0 + (b - it.chunk_base);        // this workgroup's column
-  if (blk >= nblk) return;
   unsigned long long* bestp = best + it.obj;
+  unsigned long long* qp = queue + lo;
+  __shared__ unsigned long long s_k[2];  // the block taken, alternating slots (one barrier per block)
+  if (threadIdx.x == 0) s_k[0] = atomicAdd(qp, 1ull);
+  __syncthreads();
+  uint64_t blk = bm_block_of(it, s_k[0]);
+  if (blk >= nblk) return;
   if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it.start + blk * BM_BLOCK) return;
 
 #ifdef BM_PRIO_MOD
@@ -80,13 +85,16 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
   const uint64_t target = o->target;
 
   uint32_t done = 0;
-  for (; blk < nblk; blk += gn) {
+  for (uint32_t slot = 1;; slot ^= 1) {
+    // the next block, taken while this one is hashed (its latency hides behind ~6,500 VALU
+    // instructions)
+    unsigned long long kn = 0;
+    if (threadIdx.x == 0) kn = atomicAdd(qp, 1ull);
     const uint64_t off = blk * BM_BLOCK;
     const uint64_t first = it.start + off;
-    // Early exit, one block row of granularity at no stall: the running minimum (for a split window
-    // also the other shards' hits, folded in by the launch's relay) is read before this block's
-    // hashing -- its latency hides behind ~6,500 VALU instructions -- and tested after it.  A value
-    // older by one row is only conservative.
+    // Early exit at no stall: the running minimum (for a split window also the other shards' hits,
+    // folded in by the launch's relay) is read before this block's hashing and tested against the
+    // next block after it.  A value older by one block is only conservative.
     const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t nonce = first + threadIdx.x;
     const uint64_t tv = trial_of(ihw, nonce);
@@ -96,7 +104,13 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
       if (kX && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
     }
     done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
-    if (seen < first + gn * BM_BLOCK) break;  // every later block of this column is above it
+    if (threadIdx.x == 0) s_k[slot] = kn;
+    __syncthreads();
+    const uint64_t nb = bm_block_of(it, s_k[slot]);
+    // a block taken and not hashed lies past the window or above a hit: no nonce below the answer
+    // is skipped
+    if (nb >= nblk || seen < it.start + nb * BM_BLOCK) break;
+    blk = nb;
   }
   if (threadIdx.x == 0) atomicAdd(trials_done, (unsigned long long)done);
 }
@@ -111,6 +125,7 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
                                                              unsigned long long* __restrict__ best,
                                                              uint32_t* __restrict__ found,
                                                              unsigned long long* __restrict__ trials_done,
+                                                             unsigned long long* __restrict__ queue,
                                                              unsigned long long* __restrict__ xb,
                                                              uint32_t xrow, uint32_t xrows) {
   if constexpr (kX) {
@@ -118,10 +133,10 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
       bm_relay(items, nitems, best, xb, xrow, trials_done + 1, gridDim.x - 1);
       return;
     }
-    search_column<true>(objs, items, nitems, best, found, trials_done, xb, xrows, blockIdx.x - 1);
+    search_column<true>(objs, items, nitems, best, found, trials_done, queue, xb, xrows, blockIdx.x - 1);
     if (threadIdx.x == 0) atomicAdd(trials_done + 1, 1ull);
   } else {
-    search_column<false>(objs, items, nitems, best, found, trials_done, nullptr, 0, blockIdx.x);
+    search_column<false>(objs, items, nitems, best, found, trials_done, queue, nullptr, 0, blockIdx.x);
   }
 }
 
@@ -130,13 +145,13 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
 // ---------------------------------------------------------------------------------------
 hipError_t bm_launch_search(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                             unsigned long long* best, uint32_t* found, unsigned long long* trials_done,
-                            const bm_xbound& xb) {
+                            unsigned long long* queue, const bm_xbound& xb) {
   if (xb.table)
     hipLaunchKernelGGL(bm_search_kernel<true>, dim3(nwg + 1), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
-                       trials_done, xb.table, xb.row, xb.rows);
+                       trials_done, queue, xb.table, xb.row, xb.rows);
   else
     hipLaunchKernelGGL(bm_search_kernel<false>, dim3(nwg), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
-                       trials_done, nullptr, 0u, 0u);
+                       trials_done, queue, nullptr, 0u, 0u);
   return hipGetLastError();
 }
 

@@ -232,7 +232,7 @@ void set_pending(BatchState& b, size_t first, size_t count, bool pending) {
 // search steps
 // ---------------------------------------------------------------------------------------
 void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident,
-           bool split) {
+           bool split, const double* weights) {
   p.items.assign(S, std::vector<bm_item>());
   p.nchunks.assign(S, 0);
   p.nx = 0;
@@ -264,7 +264,19 @@ void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, S
     return;
   }
   std::vector<uint64_t> cut(S + 1);
-  for (size_t s = 0; s <= S; ++s) cut[s] = C * s / S;
+  if (weights) {
+    double tot = 0;
+    for (size_t s = 0; s < S; ++s) tot += weights[s];
+    double acc = 0;
+    cut[0] = 0;
+    for (size_t s = 1; s < S; ++s) {
+      acc += weights[s - 1];
+      cut[s] = std::max(cut[s - 1], std::min<uint64_t>(C, (uint64_t)((double)C * acc / tot + 0.5)));
+    }
+    cut[S] = C;
+  } else {
+    for (size_t s = 0; s <= S; ++s) cut[s] = C * s / S;
+  }
   size_t s = 0;
   for (const Win& w : wins) {
     uint64_t c = w.chunk0;
@@ -302,7 +314,27 @@ uint64_t expect_cap(uint64_t target, size_t S, uint64_t chunk) {
   return cap < (double)floor_ ? floor_ : (cap >= 1.8e19 ? kU64Max : (uint64_t)cap);
 }
 
-bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p, uint32_t resident) {
+void ShardRates::sample(size_t s, uint64_t trials, double ms) {
+  if (s >= ema.size() || trials < kRateMinTrials || !(ms > 0)) return;
+  const double r = (double)trials / ms;
+  ema[s] = ema[s] > 0 ? (1 - kRateAlpha) * ema[s] + kRateAlpha * r : r;
+}
+
+bool ShardRates::weights(std::vector<double>& w) const {
+  w.assign(ema.size(), 1.0);
+  double mean = 0;
+  for (double r : ema) {
+    if (!(r > 0)) return false;
+    mean += r;
+  }
+  if (ema.empty()) return false;
+  mean /= (double)ema.size();
+  for (size_t s = 0; s < ema.size(); ++s) w[s] = std::min(2.0, std::max(0.5, ema[s] / mean));
+  return true;
+}
+
+bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p, uint32_t resident,
+               const double* weights) {
   while (b.first_pending < b.n && b.done[b.first_pending] != BMPOW_PENDING) ++b.first_pending;
   if (b.pending == 0) return false;
   if (budget == 0) budget = step_trials * S;
@@ -331,7 +363,7 @@ bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, S
     p.wins.push_back({(uint32_t)i, st, want, ch, acc});
     acc += ch;
   }
-  slice(p.wins, acc, p.chunk, S, p, resident, split);
+  slice(p.wins, acc, p.chunk, S, p, resident, split, weights);
   split_kinds(b.objs, b.nvar_slots > 0, p);
   return true;
 }

@@ -115,8 +115,26 @@ void split_kinds(const std::vector<bm_obj>& objs, bool any_var, StepPlan& p);
 //     devices sweep the same front, and the window's cross-shard bound slot (p.nx of them) lets a hit
 //     on one device stop the columns above it on every other.
 // chunk_base of each item is relative to its shard's launch.
+//   * weights (null = equal): the default mode's slices are cut in proportion to w[s] (ShardRates), so a
+//     slower shard gets fewer chunks; split mode keeps equal columns (every shard sweeps the same rows).
 void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident = 0,
-           bool split = false);
+           bool split = false, const double* weights = nullptr);
+
+// Per-shard throughput, to weight a step's slices.  The in-process multi-device step is lockstep
+// (launch on every shard, wait for all, plan the next), so the slowest shard sets its length; a
+// shard's share of the next step is made proportional to its measured rate instead of 1/S: an
+// exponential average of trials per ms over its launches of at least kRateMinTrials trials (short
+// launches measure launch latency, not rate).  Weights are 1 until every shard has a sample and are
+// clamped to [1/2, 2] x the mean.
+constexpr uint64_t kRateMinTrials = (uint64_t)1 << 24;
+constexpr double kRateAlpha = 0.25;
+struct ShardRates {
+  std::vector<double> ema;  // trials per ms; 0 = no sample yet
+  void reset(size_t S) { ema.assign(S, 0.0); }
+  void sample(size_t s, uint64_t trials, double ms);
+  // w[s] with mean 1; false (w all 1) until every shard has a sample
+  bool weights(std::vector<double>& w) const;
+};
 
 // A window split over the shards is capped at kExpectWindows x E nonces (E = 2^64 / (target + 1), the
 // expected trials to a hit; at least one chunk per shard): a step then lasts about as long as the
@@ -128,9 +146,10 @@ uint64_t expect_cap(uint64_t target, size_t S, uint64_t chunk);
 
 // Windows for the next step over S shards with about `budget` trials (0 = step_trials x S): pending
 // objects in slot order, k chunks each (capped by expect_cap when fewer than S are pending), dealt by
-// slice (split mode when fewer than S objects are pending).  resident: as slice.  Returns false (p
+// slice (split mode when fewer than S objects are pending).  resident, weights: as slice.  Returns false (p
 // untouched) when nothing is pending.
-bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p, uint32_t resident = 0);
+bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p, uint32_t resident = 0,
+               const double* weights = nullptr);
 
 // Fold the step's per-shard results (res[s][k] for p.items[s][k]) into the state: the min over
 // shards of each object's hits is final (every lower nonce of its window was hashed); no hit moves

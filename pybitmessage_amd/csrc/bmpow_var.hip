@@ -3,8 +3,8 @@
 // src/proofofwork.py:100-111; every caller in the reference passes a 64-byte digest, which
 // bm_search_kernel serves).
 //
-// Same execution model as bm_search_kernel (bmpow_kernels.hip): workgroup columns sweeping an
-// item's nonce window, atomicMin of hits into best[obj], early exit above the running minimum.
+// Same execution model as bm_search_kernel (bmpow_kernels.hip): workgroups taking an item's blocks
+// in order from its queue, atomicMin of hits into best[obj], early exit above the running minimum.
 // Per object the message words come from the batch's var pool (bmsched::pack_var): block 0's
 // W1..W15 are loaded once per workgroup (loop-invariant, so their sigma terms are hoisted out of
 // the nonce loop), the K+W words of the further blocks are read per round with uniform loads.
@@ -43,14 +43,19 @@ __device__ __forceinline__ void search_var_column(const bm_obj* __restrict__ obj
                                                   uint32_t nitems, unsigned long long* __restrict__ best,
                                                   uint32_t* __restrict__ found,
                                                   unsigned long long* __restrict__ trials_done,
+                                                  unsigned long long* __restrict__ queue,
                                                   unsigned long long* __restrict__ xb, uint32_t xrows,
                                                   const uint64_t* __restrict__ vpool, uint32_t b) {
-  const bm_item it = items[item_of(items, nitems, b)];
+  const uint32_t li = item_of(items, nitems, b);
+  const bm_item it = items[li];
   const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
-  const uint64_t gn = it.gn;
-  uint64_t blk = (uint64_t)it.g0 + (b - it.chunk_base);
-  if (blk >= nblk) return;
   unsigned long long* bestp = best + it.obj;
+  unsigned long long* qp = queue + li;
+  __shared__ unsigned long long s_k[2];  // the item's block queue, as in bm_search_kernel (bmpow_kernels.h)
+  if (threadIdx.x == 0) s_k[0] = atomicAdd(qp, 1ull);
+  __syncthreads();
+  uint64_t blk = bm_block_of(it, s_k[0]);
+  if (blk >= nblk) return;
   if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it.start + blk * BM_BLOCK) return;
   const bm_obj* o = objs + it.obj;
   const uint64_t* m = vpool + o->vword;
@@ -61,7 +66,9 @@ __device__ __forceinline__ void search_var_column(const bm_obj* __restrict__ obj
 #pragma unroll
   for (int i = 1; i < 16; ++i) mw[i] = m[i];
   uint32_t done = 0;
-  for (; blk < nblk; blk += gn) {
+  for (uint32_t slot = 1;; slot ^= 1) {
+    unsigned long long kn = 0;
+    if (threadIdx.x == 0) kn = atomicAdd(qp, 1ull);
     const uint64_t off = blk * BM_BLOCK;
     const uint64_t first = it.start + off;
     const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -73,7 +80,11 @@ __device__ __forceinline__ void search_var_column(const bm_obj* __restrict__ obj
       if (xb && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
     }
     done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
-    if (seen < first + gn * BM_BLOCK) break;
+    if (threadIdx.x == 0) s_k[slot] = kn;
+    __syncthreads();
+    const uint64_t nxt = bm_block_of(it, s_k[slot]);
+    if (nxt >= nblk || seen < it.start + nxt * BM_BLOCK) break;
+    blk = nxt;
   }
   if (threadIdx.x == 0) atomicAdd(trials_done, (unsigned long long)done);
 }
@@ -86,6 +97,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_var_kernel(const bm_obj* _
                                                                  unsigned long long* __restrict__ best,
                                                                  uint32_t* __restrict__ found,
                                                                  unsigned long long* __restrict__ trials_done,
+                                                                 unsigned long long* __restrict__ queue,
                                                                  unsigned long long* __restrict__ xb,
                                                                  uint32_t xrow, uint32_t xrows,
                                                                  const uint64_t* __restrict__ vpool) {
@@ -94,10 +106,10 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_var_kernel(const bm_obj* _
       bm_relay(items, nitems, best, xb, xrow, trials_done + 1, gridDim.x - 1);
       return;
     }
-    search_var_column(objs, items, nitems, best, found, trials_done, xb, xrows, vpool, blockIdx.x - 1);
+    search_var_column(objs, items, nitems, best, found, trials_done, queue, xb, xrows, vpool, blockIdx.x - 1);
     if (threadIdx.x == 0) atomicAdd(trials_done + 1, 1ull);
   } else {
-    search_var_column(objs, items, nitems, best, found, trials_done, nullptr, 0, vpool, blockIdx.x);
+    search_var_column(objs, items, nitems, best, found, trials_done, queue, nullptr, 0, vpool, blockIdx.x);
   }
 }
 
@@ -159,9 +171,10 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_mintrial_var_kernel(const bm_obj*
 
 hipError_t bm_launch_search_var(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items,
                                 uint32_t nitems, unsigned long long* best, uint32_t* found,
-                                unsigned long long* trials_done, const bm_xbound& xb, const uint64_t* vpool) {
+                                unsigned long long* trials_done, unsigned long long* queue, const bm_xbound& xb,
+                                const uint64_t* vpool) {
   hipLaunchKernelGGL(bm_search_var_kernel, dim3(nwg + (xb.table ? 1 : 0)), dim3(BM_BLOCK), 0, st, objs, items, nitems,
-                     best, found, trials_done, xb.table, xb.row, xb.rows, vpool);
+                     best, found, trials_done, queue, xb.table, xb.row, xb.rows, vpool);
   return hipGetLastError();
 }
 

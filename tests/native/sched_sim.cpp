@@ -10,6 +10,7 @@
 //
 // Every answer is checked against the oracle's sequential _doSafePoW search
 // (src/proofofwork.py:100-111); exit status 0 = all scenarios passed.
+#include <cmath>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -173,9 +174,9 @@ static void sim_step_shard(const std::vector<bm_obj>& objs, const std::vector<ui
 
 // One bounded step over S shards, one host thread per shard (as one stream per device).
 static bool sim_step(BatchState& b, std::vector<SimShard>& shards, uint64_t budget, uint64_t step_trials,
-                     uint32_t resident = 24) {
+                     uint32_t resident = 24, const double* weights = nullptr) {
   StepPlan p;
-  if (!plan_step(b, budget, step_trials, shards.size(), p, resident)) return false;
+  if (!plan_step(b, budget, step_trials, shards.size(), p, resident, weights)) return false;
   // every window's columns [0, gn) are covered exactly once over the shards' items; a window split
   // over the shards has one item per shard and a cross-shard bound slot of its own
   for (size_t wi = 0; wi < p.wins.size(); ++wi) {
@@ -392,6 +393,54 @@ static void scenario_expect_cap() {
   plan_step(b, 0, 1 << 28, 8, p);
   for (const Win& w : p.wins)
     CHECK(w.chunks * p.chunk == ((uint64_t)1 << 28), "object-sharded window capped: %llu", (unsigned long long)w.count);
+}
+
+// ---- scenario 1d: slices weighted by the shards' measured rates (ShardRates) ----
+static void scenario_weights() {
+  ShardRates r;
+  r.reset(3);
+  std::vector<double> w;
+  CHECK(!r.weights(w) && w.size() == 3 && w[0] == 1.0, "no samples: equal weights");
+  r.sample(0, kRateMinTrials - 1, 1.0);  // too short a launch to measure
+  CHECK(r.ema[0] == 0.0, "short launch ignored");
+  r.sample(0, 1ull << 28, 40.0);
+  r.sample(1, 1ull << 28, 80.0);
+  CHECK(!r.weights(w), "weights need every shard sampled");
+  r.sample(2, 1ull << 28, 400.0);  // 10x slower than shard 0: clamped
+  CHECK(r.weights(w), "weights once every shard has a sample");
+  const double mean = ((1 << 28) / 40.0 + (1 << 28) / 80.0 + (1 << 28) / 400.0) / 3;
+  CHECK(std::fabs(w[0] - std::min(2.0, (1 << 28) / 40.0 / mean)) < 1e-12 && w[2] == 0.5, "clamped weights %f %f %f",
+        w[0], w[1], w[2]);
+  r.sample(1, 1ull << 28, 40.0);  // the average moves a quarter of the way
+  CHECK(std::fabs(r.ema[1] - (0.75 * (1 << 28) / 80.0 + 0.25 * (1 << 28) / 40.0)) < 1e-6, "ema step");
+
+  // a weighted step: each shard's chunks in proportion to its weight, and the answers still exact
+  std::mt19937_64 rng(31);
+  const double wt[4] = {1.0, 0.5, 2.0, 1.25};
+  const size_t n = 400;
+  std::vector<Obj> objs = random_objs(rng, n, 4000);
+  std::vector<uint8_t> ihs(64 * n);
+  std::vector<uint64_t> tg(n), st(n);
+  for (size_t i = 0; i < n; ++i) {
+    memcpy(&ihs[64 * i], objs[i].ih, 64);
+    tg[i] = objs[i].target;
+    st[i] = objs[i].start;
+  }
+  BatchState b;
+  init(b, n, ihs.data(), tg.data(), st.data());
+  StepPlan p;
+  CHECK(plan_step(b, (uint64_t)1 << 22, 1 << 20, 4, p, 0, wt), "weighted plan");
+  uint64_t tot = 0;
+  for (size_t s = 0; s < 4; ++s) tot += p.nchunks[s];
+  for (size_t s = 0; s < 4; ++s) {
+    const double share = (double)p.nchunks[s] / (double)tot, want = wt[s] / 4.75;
+    CHECK(std::fabs(share - want) < 0.02, "shard %zu share %.4f want %.4f", s, share, want);
+  }
+  std::vector<SimShard> shards(4);
+  while (sim_step(b, shards, (uint64_t)1 << 16, 1 << 14, 24, wt)) {
+  }
+  for (size_t i = 0; i < n; ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "weighted", i);
+  fprintf(stderr, "weights: rate averages, clamping, weighted slices exact over 4 shards\n");
 }
 
 // ---- scenario 2: windows clipped at the top of the nonce space ----
@@ -878,6 +927,7 @@ int main() {
   scenario_batches();
   scenario_var();
   scenario_expect_cap();
+  scenario_weights();
   scenario_top_of_space();
   scenario_session();
   scenario_min_trial();

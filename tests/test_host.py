@@ -42,9 +42,10 @@ def test_header_declares_the_boundary():
               'bmpow_min_trial_batch', 'bmpow_batch_add', 'bmpow_batch_take_done', 'bmpow_service_create',
               'bmpow_service_submit', 'bmpow_service_poll', 'bmpow_service_cancel', 'bmpow_service_outstanding',
               'bmpow_service_stop', 'bmpow_service_destroy', 'bmpow_set_device_count', 'bmpow_trials_len',
-              'bmpow_search_len', 'bmpow_min_trial_var', 'bmpow_batch_add_var', 'bmpow_service_submit_var']:
+              'bmpow_search_len', 'bmpow_min_trial_var', 'bmpow_batch_add_var', 'bmpow_service_submit_var',
+              'bmpow_get_shard_rates']:
         assert s in syms
-    assert len(syms) == 53
+    assert len(syms) == 54
 
 
 def test_library_exports_every_declared_symbol(rawlib):
