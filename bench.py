@@ -918,8 +918,14 @@ def summarize(args, dist, r, lib_version):
                     line['roofline']['frac_vs_mix_ceiling'] = round(kernel_ghs / mceil, 4)
     if r.get('devices'):
         line['config']['parallelism'] = ('in-process nonce/object sharding over %d devices (bmpow_set_devices, '
-                                         'host min-reduction, no collective)' % r['devices'])
+                                         'rate-weighted slices, host min-reduction, no collective)' % r['devices'])
         line['n_gpus'] = r['devices']
+        import ctypes
+
+        from pybitmessage_amd import _lib
+        rates = (ctypes.c_double * 64)()
+        n = _lib.get().bmpow_get_shard_rates(rates, 64)
+        line['shard_rates_ghs'] = [round(rates[i] * 1e3 / 1e9, 4) for i in range(min(n, 64))]
     return line
 
 
@@ -949,8 +955,10 @@ def pmc_counters():
     if not os.path.exists(path):
         return None
     with open(path) as f:
-        d = json.load(f)['derived']
-    out = {'traffic': d.get('hbm_bytes_per_launch_upper'), 'source': 'profiles/pmc_latest.json (C3, 2^28-trial launches)'}
+        full = json.load(f)
+    d = full['derived']
+    out = {'traffic': d.get('hbm_bytes_per_launch_upper'), 'source': 'profiles/pmc_latest.json (C3, 2^28-trial launches)',
+           'build': full.get('build')}
     for k in ('valu_instr_per_trial', 'valu_issue_util', 'valu_instr_per_simd_quad_cycle', 'dual_issue_share',
               'simd_busy_frac', 'wave_issue_stall_share', 'wave_wait_share', 'eff_clock_ghz'):
         if d.get(k) is not None:

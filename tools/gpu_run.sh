@@ -1,0 +1,47 @@
+#!/bin/bash
+# One parameterised GPU-box runner (replaces the per-call one-off scripts): each STEP runs under
+# its own time limit, output under OUT/, and the first failing step ends the call.
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- 'bash tools/gpu_run.sh gpurun_out/NAME STEP...'
+# STEPS
+#   suite            pytest -m "gpu and not slow" (whole GPU suite, no -x: every failure listed)
+#   suite-slow       pytest -m "gpu and slow" (C3 at 2^38)
+#   tests:EXPR       pytest -m gpu -k EXPR over tests/
+#   bench            default bench line (C2, 20 steps, CPU baseline legs)
+#   bench-quick      C2, 3 steps, no CPU baseline
+#   c1 | c3 | c4 | c5 | verify | addrgen      bench.py --config X (short runs, no CPU baseline)
+#   rocprof-bench    rocprofv3 --kernel-trace --stats over the default bench (3 steps)
+#   pmc              tools/profile_pmc.sh OUT/pmc (C3 2^33, one counter group per pass)
+#   shard-latency    tools/shard_latency.py
+#   c1-columns       tools/diag/c1_columns.py (C1 waste by column count)
+#   atomic-rate      tools/diag/atomic_rate (single-address atomic rate)
+#   ubench-mix       tools/ubench_mix (the search kernel's instruction-mix issue ceiling)
+set -euo pipefail
+OUT=${1:?outdir}; shift
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+PYT=(python3 -u -m pytest --timeout 300 --timeout-method thread -v)
+for step in "$@"; do
+  echo "[gpu_run] $(date +%T) $step" >&2
+  case "$step" in
+    suite) timeout -k 10 1000 "${PYT[@]}" tests -m "gpu and not slow" > "$OUT/pytest_gpu.log" 2>&1 ;;
+    suite-slow) timeout -k 10 600 "${PYT[@]}" tests -m "gpu and slow" > "$OUT/pytest_gpu_slow.log" 2>&1 ;;
+    tests:*) timeout -k 10 900 "${PYT[@]}" -x tests -m gpu -k "${step#tests:}" > "$OUT/pytest_k.log" 2>&1 ;;
+    bench) timeout -k 10 600 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    bench-quick) timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/c2.json" 2> "$OUT/c2.err" ;;
+    c1) timeout -k 10 200 python3 bench.py --config c1 --steps 20 --warmup 2 --no-cpu-baseline > "$OUT/c1.json" 2> "$OUT/c1.err" ;;
+    c3) timeout -k 10 200 python3 bench.py --config c3 --c3-log2 36 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/c3.json" 2> "$OUT/c3.err" ;;
+    c4) timeout -k 10 300 python3 bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/c4.json" 2> "$OUT/c4.err" ;;
+    c5) timeout -k 10 300 python3 bench.py --config c5 --objects 4096 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/c5.json" 2> "$OUT/c5.err" ;;
+    verify) timeout -k 10 300 python3 bench.py --config verify --no-cpu-baseline > "$OUT/verify.json" 2> "$OUT/verify.err" ;;
+    addrgen) timeout -k 10 300 python3 bench.py --config addrgen --no-cpu-baseline > "$OUT/addrgen.json" 2> "$OUT/addrgen.err" ;;
+    rocprof-bench) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof" -o run -- \
+                     python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/rocprof_bench.json" 2> "$OUT/rocprof_bench.err" ;;
+    pmc) bash tools/profile_pmc.sh "$OUT/pmc" 33 > "$OUT/pmc.log" 2>&1 ;;
+    shard-latency) timeout -k 10 200 python3 tools/shard_latency.py > "$OUT/shard_latency.json" 2> "$OUT/shard_latency.err" ;;
+    c1-columns) timeout -k 10 300 python3 tools/diag/c1_columns.py parent 0 1024 512 > "$OUT/c1_columns.jsonl" 2> "$OUT/c1_columns.err" ;;
+    atomic-rate) timeout -k 10 120 ./tools/diag/atomic_rate > "$OUT/atomic_rate.jsonl" 2> "$OUT/atomic_rate.err" ;;
+    ubench-mix) timeout -k 10 300 ./tools/ubench_mix > "$OUT/ubench_mix.jsonl" 2> "$OUT/ubench_mix.err" ;;
+    *) echo "unknown step $step" >&2; exit 2 ;;
+  esac
+done
+echo "[gpu_run] $(date +%T) done" >&2
