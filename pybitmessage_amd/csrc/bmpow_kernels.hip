@@ -30,13 +30,14 @@ using namespace bm;
 // ---------------------------------------------------------------------------------------
 // Search kernel.
 // ---------------------------------------------------------------------------------------
-// Register budget for 5 waves per SIMD (<= 96 VGPRs; the allocator keeps 12 dwords of loop-invariant
-// per-object terms in scratch, 6 scratch_load_dwordx2 per iteration, L1-resident).  Same-box A/B, C3
-// 2^35 nonces, on three boxes: 6.53-6.59 GH/s against 6.30-6.39 at the 4 waves of 120 VGPRs
-// (profiles/r02/search_kernel_ab_waves*.txt).  The gain needs the per-object words in VGPRs too: with
-// them in SGPRs (BM_IHW_SGPR) 5 waves fit without scratch but run no faster than 4.
+// Register budget for 4 waves per SIMD (<= 128 VGPRs, no scratch).  With the static chunks of round 2,
+// 5 waves (96 VGPRs, 12 dwords of loop-invariant terms spilled to scratch) ran 3 % faster than 4
+// (profiles/r02/search_kernel_ab_waves*.txt); with the block queue the order reversed.  Same box, C3
+// 2^35 nonces, twice each (profiles/r03/waves_queue_ab/): 4 waves 6.7025 / 6.7026 GH/s, 5 waves
+// 6.691 / 6.684, 512-lane workgroups at 4 waves 6.695 / 6.691 and at 6 waves 6.662 / 6.666, 1,024-lane
+// workgroups 6.28 / 6.29 -- and 4 waves carry no scratch traffic.
 #ifndef BM_SEARCH_WAVES
-#define BM_SEARCH_WAVES 5
+#define BM_SEARCH_WAVES 4
 #endif
 // One workgroup of a launch: it takes blocks of its item from the item's queue (bm_block_of), in
 // order, until the window ends or the next block lies above the running minimum.

@@ -123,9 +123,9 @@ def test_c5_default_difficulty_slice(gpulib, shards, coracle):
     oracle_sample(coracle, objs, res, rng.sample(range(len(objs)), 20))
 
 
-# bm_search_kernel workgroups resident on one MI355X (5 per CU at 96 VGPRs x 256 CUs): the columns
-# of a window's sweep (bmpow_layout.h), one block row = ROW nonces
-ROW = 1280 * 256
+# bm_search_kernel workgroups resident on one MI355X (4 per CU at <= 128 VGPRs x 256 CUs): a window's
+# blocks in flight at once (bmpow_layout.h), one block row = ROW nonces
+ROW = 1024 * 256
 
 
 @pytest.mark.parametrize('nshards', [1, 4, 8])
