@@ -63,8 +63,11 @@ struct Shard {
   // per-step staging (capacity grows)
   bm_item* d_items = nullptr;
   bm_result* d_res = nullptr;
-  unsigned long long* d_trials = nullptr;
-  unsigned long long* d_queue = nullptr;  // per item: the next block of its window to hand out (bmpow_kernels.h)
+  // a step's counters, zeroed by one memset: [0] trials hashed, [1] the relay's finished workgroups,
+  // then per item the next block of its window to hand out (the block queue, bmpow_kernels.h)
+  unsigned long long* d_ctr = nullptr;
+  unsigned long long* d_trials = nullptr;  // d_ctr
+  unsigned long long* d_queue = nullptr;   // d_ctr + 2
   bm_item* h_items = nullptr;      // pinned
   bm_result* h_res = nullptr;      // pinned
   unsigned long long* h_trials = nullptr;  // pinned
@@ -129,11 +132,13 @@ int ensure_items(Shard& s, size_t n) {
   if (s.d_items) {
     HIPTRY(hipFree(s.d_items));
     HIPTRY(hipFree(s.d_res));
-    HIPTRY(hipFree(s.d_queue));
+    HIPTRY(hipFree(s.d_ctr));
     HIPTRY(hipHostFree(s.h_res));
   }
   HIPTRY(hipMalloc(&s.d_items, cap * sizeof(bm_item)));
-  HIPTRY(hipMalloc(&s.d_queue, cap * sizeof(unsigned long long)));
+  HIPTRY(hipMalloc(&s.d_ctr, (cap + 2) * sizeof(unsigned long long)));
+  s.d_trials = s.d_ctr;
+  s.d_queue = s.d_ctr + 2;
   HIPTRY(hipMalloc(&s.d_res, cap * sizeof(bm_result)));
   HIPTRY(hipHostMalloc(&s.h_res, cap * sizeof(bm_result), hipHostMallocDefault));
   s.item_cap = cap;
@@ -145,8 +150,7 @@ void free_shard(Shard& s) {
   (void)hipSetDevice(s.dev);
   if (s.d_items) (void)hipFree(s.d_items);
   if (s.d_res) (void)hipFree(s.d_res);
-  if (s.d_queue) (void)hipFree(s.d_queue);
-  if (s.d_trials) (void)hipFree(s.d_trials);
+  if (s.d_ctr) (void)hipFree(s.d_ctr);
   if (s.h_items) (void)hipHostFree(s.h_items);
   if (s.h_res) (void)hipHostFree(s.h_res);
   if (s.h_trials) (void)hipHostFree(s.h_trials);
@@ -179,7 +183,6 @@ int make_shard(int dev, Shard& s) {
   s.resident = (uint32_t)std::max(1, bm_search_resident_per_cu()) * (uint32_t)s.cus;
   if (const char* e = std::getenv("BMPOW_COLUMNS"))  // A/B knob: columns per shard and window
     if (std::atoi(e) > 0) s.resident = (uint32_t)std::atoi(e);
-  HIPTRY(hipMalloc(&s.d_trials, 2 * sizeof(unsigned long long)));  // trials, relay's finished columns
   HIPTRY(hipHostMalloc(&s.h_trials, sizeof(unsigned long long), hipHostMallocDefault));
   return ensure_items(s, 1024);
 }
@@ -441,8 +444,7 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     if (sh.nitems == 0) continue;
     HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream));
-    HIPTRY(hipMemsetAsync(sh.d_trials, 0, 2 * sizeof(unsigned long long), sh.stream));
-    HIPTRY(hipMemsetAsync(sh.d_queue, 0, sh.nitems * sizeof(unsigned long long), sh.stream));
+    HIPTRY(hipMemsetAsync(sh.d_ctr, 0, (2 + sh.nitems) * sizeof(unsigned long long), sh.stream));
   }
   for (size_t s = 0; s < S; ++s) {
     Shard& sh = g_shards[s];

@@ -93,10 +93,8 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
     if (threadIdx.x == 0) kn = atomicAdd(qp, 1ull);
     const uint64_t off = blk * BM_BLOCK;
     const uint64_t first = it.start + off;
-    // Early exit at no stall: the running minimum (for a split window also the other shards' hits,
-    // folded in by the launch's relay) is read before this block's hashing and tested against the
-    // next block after it.  A value older by one block is only conservative.
-    const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // Early exit: the running minimum (for a split window also the other shards' hits, folded in by
+    // the launch's relay) is tested against the next block.  A stale value is only conservative.
     const uint64_t nonce = first + threadIdx.x;
     const uint64_t tv = trial_of(ihw, nonce);
     if (off + threadIdx.x < it.count && tv <= target) {
@@ -104,6 +102,11 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
       __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (kX && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
     }
+    // The running minimum is read after the hash, so a hit published while this block was hashed
+    // stops the workgroup now rather than one block later; the load's latency overlaps the wait at
+    // the barrier below.  Same box (profiles/r03/fresh_bound_ab.txt): C1 waste 1.3-1.4 % against
+    // 2.1 % with the load issued before the hash; C3 6.705-6.707 against 6.703-6.708 GH/s.
+    const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
     if (threadIdx.x == 0) s_k[slot] = kn;
     __syncthreads();

@@ -71,7 +71,6 @@ __device__ __forceinline__ void search_var_column(const bm_obj* __restrict__ obj
     if (threadIdx.x == 0) kn = atomicAdd(qp, 1ull);
     const uint64_t off = blk * BM_BLOCK;
     const uint64_t first = it.start + off;
-    const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t nonce = first + threadIdx.x;
     const uint64_t tv = trial_var(mw, m + 16, nb, nonce);
     if (off + threadIdx.x < it.count && tv <= target) {
@@ -79,6 +78,7 @@ __device__ __forceinline__ void search_var_column(const bm_obj* __restrict__ obj
       __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (xb && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
     }
+    const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
     if (threadIdx.x == 0) s_k[slot] = kn;
     __syncthreads();
