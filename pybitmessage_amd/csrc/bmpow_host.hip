@@ -272,6 +272,9 @@ struct bmpow_batch : bmsched::BatchState {
     uint64_t* d_vpool = nullptr;           // copy of vpool (var-form objects' words), vcap words
   };
   std::vector<Dev> dev;  // one per shard (indexed like g_shards)
+  // a step was launched and not completed (an error mid-step): the devices' best/found may hold a
+  // hit the resolve kernel did not reset, so a reuse of the slots must reset them
+  bool dirty = false;
   size_t vcap = 0;         // words allocated per shard for the var pool
   size_t vsynced = 0;      // vpool words already on the devices (of epoch vepoch)
   uint64_t vepoch = ~0ULL;
@@ -437,6 +440,7 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     if (rc < 0) return rc;
   }
 
+  b->dirty = true;
   // 3. stage every shard's items and counters, then launch on every shard back to back (the shards of a
   // split window sweep the same rows, so their kernels should start together), then collect
   for (size_t s = 0; s < S; ++s) {
@@ -493,6 +497,7 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     step_trials += *sh.h_trials;
     g_rates.sample(s, *sh.h_trials, ms);
   }
+  b->dirty = false;  // every shard's resolve ran: best/found are (UINT64_MAX, 0) again
   g_stats.trials += step_trials;
   g_stats.steps++;
   double mx = 0;
@@ -639,9 +644,11 @@ int scratch_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, const u
       if (!n) continue;
       HIPTRY(hipMemcpyAsync(g_scratch->dev[s].d_obj, g_scratch->objs.data(), n * sizeof(bm_obj), hipMemcpyHostToDevice,
                             sh.stream));
+      if (!g_scratch->dirty) continue;  // the last steps' resolve left every slot at (UINT64_MAX, 0)
       HIPTRY(hipMemsetAsync(g_scratch->dev[s].d_best, 0xFF, n * sizeof(unsigned long long), sh.stream));
       HIPTRY(hipMemsetAsync(g_scratch->dev[s].d_found, 0, n * sizeof(uint32_t), sh.stream));
     }
+    g_scratch->dirty = false;
     // no host sync needed: the step's launches follow on the same streams
     return 0;
   }

@@ -96,8 +96,9 @@ hipError_t bm_launch_search_var(hipStream_t st, uint32_t nwg, const bm_obj* objs
                                 unsigned long long* trials_done, unsigned long long* queue, const bm_xbound& xb,
                                 const uint64_t* vpool);
 // vpool: the batch's var pool (may be null when no object of the launch is var-form)
+// Writes each item's result and puts its object's best/found back to (UINT64_MAX, 0).
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
-                             const unsigned long long* best, const uint32_t* found, bm_result* res,
+                             unsigned long long* best, uint32_t* found, bm_result* res,
                              const uint64_t* vpool);
 hipError_t bm_launch_mintrial(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                               bm_minpart* parts);

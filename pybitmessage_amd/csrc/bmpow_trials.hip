@@ -38,12 +38,12 @@ __device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce, const uint64_t* v
 // nonce (one thread per item).  res[k] = {nonce, trial, found = 1} or {UINT64_MAX, 0, found = 0}:
 // the found flag, not the nonce, says whether there is a hit (2^64-1 is a legal answer).
 __global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
-                                  uint32_t nitems, const unsigned long long* __restrict__ best,
-                                  const uint32_t* __restrict__ found, bm_result* __restrict__ res,
+                                  uint32_t nitems, unsigned long long* __restrict__ best,
+                                  uint32_t* __restrict__ found, bm_result* __restrict__ res,
                                   const uint64_t* __restrict__ vpool) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= nitems) return;
-  const uint32_t obj = items[k].obj;
+  const uint32_t obj = items[k].obj;  // at most one item per object in a shard's step
   bm_result r;
   r.nonce = best[obj];
   r.trial = 0;
@@ -51,6 +51,11 @@ __global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item
   r.pad = 0;
   if (r.found) r.trial = trial_obj(objs + obj, r.nonce, vpool);
   res[k] = r;
+  // Back to the "no hit" state: an object with a hit on any shard (its own, or one the relay folded
+  // in from another shard) is finished by this step, and a pending one is unchanged -- so between
+  // steps every slot reads (UINT64_MAX, 0) and a reused slot needs no reset (bmpow_host.hip).
+  best[obj] = ~0ULL;
+  found[obj] = 0;
 }
 
 // Trial values for an arbitrary list of nonces of one object, either form (parity probe).
@@ -67,7 +72,7 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_trials_kernel(const bm_obj* __res
 // Launch wrappers (C++ linkage, used by bmpow_host.hip).
 // ---------------------------------------------------------------------------------------
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
-                             const unsigned long long* best, const uint32_t* found, bm_result* res,
+                             unsigned long long* best, uint32_t* found, bm_result* res,
                              const uint64_t* vpool) {
   const uint32_t bs = 64;
   hipLaunchKernelGGL(bm_resolve_kernel, dim3((nitems + bs - 1) / bs), dim3(bs), 0, st, objs, items, nitems,

@@ -170,6 +170,11 @@ static void sim_step_shard(const std::vector<bm_obj>& objs, const std::vector<ui
     }
     sh.res[k] = r;
   }
+  // bm_resolve_kernel puts each item's object back to "no hit" after reading it
+  for (const bm_item& it : items) {
+    sh.best[it.obj] = kU64Max;
+    sh.found[it.obj] = 0;
+  }
 }
 
 // One bounded step over S shards, one host thread per shard (as one stream per device).
@@ -218,10 +223,11 @@ static bool sim_step(BatchState& b, std::vector<SimShard>& shards, uint64_t budg
   std::vector<const bm_result*> res(shards.size());
   for (size_t s = 0; s < shards.size(); ++s) res[s] = shards[s].res.data();
   apply_step(b, p, res);
-  // a pending object's device state is (UINT64_MAX, 0) between steps (bmpow_host.hip relies on it)
+  // every slot's device state is (UINT64_MAX, 0) between steps (bmpow_host.hip relies on it: a reused
+  // scratch slot is not reset)
   for (size_t s = 0; s < shards.size(); ++s)
     for (size_t i = 0; i < b.n && i < shards[s].found.size(); ++i)
-      if (b.done[i] == BMPOW_PENDING) CHECK(!shards[s].found[i], "pending object %zu has a hit on shard %zu", i, s);
+      CHECK(!shards[s].found[i] && shards[s].best[i] == kU64Max, "object %zu keeps a hit on shard %zu", i, s);
   return true;
 }
 
