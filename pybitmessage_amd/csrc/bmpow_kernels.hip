@@ -23,6 +23,9 @@
 #include <stdint.h>
 
 #include "bmpow_kernels.h"
+#ifdef BM_MID_SYNC  // A/B knob: a workgroup barrier between a trial's two compressions (wave phasing)
+#define BM_TRIAL_MID() __syncthreads()
+#endif
 #include "sha512_dev.h"
 
 using namespace bm;

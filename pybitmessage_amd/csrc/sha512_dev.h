@@ -266,6 +266,9 @@ BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
   // state after the folded round 0 (round 1 has A = 7: a=s7 b=s0 c=s1 d=s2 e=s3 f=s4 g=s5 h=s6)
   uint64_t s[8] = {IV(0), IV(1), IV(2), nonce + E1C, IV(4), IV(5), IV(6), nonce + A1C};
   rounds<1, 80, true>(s, w);
+#ifdef BM_TRIAL_MID
+  BM_TRIAL_MID();  // A/B hook of the search kernel (bmpow_kernels.hip), nothing elsewhere
+#endif
   // after 80 rounds A = 0: s[i] holds a..h in order
   uint64_t w2[16];
 #pragma unroll
