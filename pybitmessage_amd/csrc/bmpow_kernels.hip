@@ -39,6 +39,9 @@ using namespace bm;
 // 2^35 nonces, twice each (profiles/r03/waves_queue_ab/): 4 waves 6.7025 / 6.7026 GH/s, 5 waves
 // 6.691 / 6.684, 512-lane workgroups at 4 waves 6.695 / 6.691 and at 6 waves 6.662 / 6.666, 1,024-lane
 // workgroups 6.28 / 6.29 -- and 4 waves carry no scratch traffic.
+#ifndef BM_GRAB
+#define BM_GRAB 1
+#endif
 #ifndef BM_SEARCH_WAVES
 #define BM_SEARCH_WAVES 4
 #endif
@@ -59,14 +62,17 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
   }
   const bm_item it = items[lo];
   const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;  // blocks of the window
+  // the queue hands out units of BM_GRAB blocks (1 by default; larger is an A/B knob)
+  const uint64_t nunit = (nblk + BM_GRAB - 1) / BM_GRAB;
   unsigned long long* bestp = best + it.obj;
   unsigned long long* qp = queue + lo;
-  __shared__ unsigned long long s_k[2];  // the block taken, alternating slots (one barrier per block)
+  __shared__ unsigned long long s_k[2];  // the unit taken, alternating slots (one barrier per unit)
   if (threadIdx.x == 0) s_k[0] = atomicAdd(qp, 1ull);
   __syncthreads();
-  uint64_t blk = bm_block_of(it, s_k[0]);
-  if (blk >= nblk) return;
-  if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it.start + blk * BM_BLOCK) return;
+  uint64_t unit = bm_block_of(it, s_k[0]);
+  if (unit >= nunit) return;
+  if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it.start + unit * (BM_GRAB * BM_BLOCK))
+    return;
 
 #ifdef BM_PRIO_MOD
   if (b % BM_PRIO_MOD == 0) __builtin_amdgcn_s_setprio(2);  // A/B knob: a share of the waves issue first
@@ -90,34 +96,44 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
 
   uint32_t done = 0;
   for (uint32_t slot = 1;; slot ^= 1) {
-    // the next block, taken while this one is hashed (its latency hides behind ~6,500 VALU
-    // instructions)
+    // the next unit, taken while this one is hashed (its latency hides behind ~6,200 VALU
+    // instructions per block)
     unsigned long long kn = 0;
     if (threadIdx.x == 0) kn = atomicAdd(qp, 1ull);
-    const uint64_t off = blk * BM_BLOCK;
-    const uint64_t first = it.start + off;
-    // Early exit: the running minimum (for a split window also the other shards' hits, folded in by
-    // the launch's relay) is tested against the next block.  A stale value is only conservative.
-    const uint64_t nonce = first + threadIdx.x;
-    const uint64_t tv = trial_of(ihw, nonce);
-    if (off + threadIdx.x < it.count && tv <= target) {
-      const unsigned long long prev = atomicMin(bestp, (unsigned long long)nonce);
-      __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (kX && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
+#if BM_GRAB > 1
+#pragma unroll 1
+    for (uint32_t g = 0; g < BM_GRAB; ++g) {
+      const uint64_t blk = unit * BM_GRAB + g;
+      if (blk >= nblk) break;
+#else
+    {
+      const uint64_t blk = unit;
+#endif
+      const uint64_t off = blk * BM_BLOCK;
+      const uint64_t first = it.start + off;
+      const uint64_t nonce = first + threadIdx.x;
+      const uint64_t tv = trial_of(ihw, nonce);
+      if (off + threadIdx.x < it.count && tv <= target) {
+        const unsigned long long prev = atomicMin(bestp, (unsigned long long)nonce);
+        __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (kX && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
+      }
+      done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
     }
-    // The running minimum is read after the hash, so a hit published while this block was hashed
-    // stops the workgroup now rather than one block later; the load's latency overlaps the wait at
-    // the barrier below.  Same box (profiles/r03/fresh_bound_ab.txt): C1 waste 1.3-1.4 % against
-    // 2.1 % with the load issued before the hash; C3 6.705-6.707 against 6.703-6.708 GH/s.
+    // Early exit: the running minimum (for a split window also the other shards' hits, folded in by
+    // the launch's relay) is tested against the next unit.  It is read after the hash, so a hit
+    // published while this unit was hashed stops the workgroup now rather than one unit later; the
+    // load's latency overlaps the wait at the barrier below.  Same box (profiles/r03/fresh_bound_ab.txt):
+    // C1 waste 1.3-1.4 % against 2.1 % with the load issued before the hash; C3 6.705-6.707 against
+    // 6.703-6.708 GH/s.  A stale value is only conservative.
     const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
     if (threadIdx.x == 0) s_k[slot] = kn;
     __syncthreads();
-    const uint64_t nb = bm_block_of(it, s_k[slot]);
-    // a block taken and not hashed lies past the window or above a hit: no nonce below the answer
+    const uint64_t nu = bm_block_of(it, s_k[slot]);
+    // a unit taken and not hashed lies past the window or above a hit: no nonce below the answer
     // is skipped
-    if (nb >= nblk || seen < it.start + nb * BM_BLOCK) break;
-    blk = nb;
+    if (nu >= nunit || seen < it.start + nu * (BM_GRAB * BM_BLOCK)) break;
+    unit = nu;
   }
   if (threadIdx.x == 0) atomicAdd(trials_done, (unsigned long long)done);
 }
