@@ -61,16 +61,15 @@ struct Shard {
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // per-step staging (capacity grows)
+  // a step's upload, one copy: its items, then its counters (zeroed on the host) -- [0] trials hashed,
+  // [1] the relay's finished workgroups, then per item the next block of its window to hand out (the
+  // block queue, bmpow_kernels.h).  d_trials / d_queue point into it for the current step.
   bm_item* d_items = nullptr;
-  bm_result* d_res = nullptr;
-  // a step's counters, zeroed by one memset: [0] trials hashed, [1] the relay's finished workgroups,
-  // then per item the next block of its window to hand out (the block queue, bmpow_kernels.h)
-  unsigned long long* d_ctr = nullptr;
-  unsigned long long* d_trials = nullptr;  // d_ctr
-  unsigned long long* d_queue = nullptr;   // d_ctr + 2
-  bm_item* h_items = nullptr;      // pinned
+  bm_result* d_res = nullptr;      // nitems results, then the trials counter (bm_resolve_kernel)
+  unsigned long long* d_trials = nullptr;
+  unsigned long long* d_queue = nullptr;
+  bm_item* h_items = nullptr;      // pinned, the same layout
   bm_result* h_res = nullptr;      // pinned
-  unsigned long long* h_trials = nullptr;  // pinned
   size_t item_cap = 0;
   // step bookkeeping: items [0, nmain) / chunks [0, chmain) are 64-byte objects (bm_search_kernel),
   // the rest var-form objects (bm_search_var_kernel)
@@ -118,12 +117,15 @@ bmpow_stats g_stats{};
 // Grow the shard's item staging to hold n items.  Called while a step's item list is being
 // filled, so the host items already written (s.nitems of them) move to the new buffer; the device
 // copies and the results are (re)written after the fill.
+// Bytes of a step's upload for n items: the items, then 2 + n counters.
+size_t stage_bytes(size_t n) { return n * sizeof(bm_item) + (2 + n) * sizeof(unsigned long long); }
+
 int ensure_items(Shard& s, size_t n) {
   if (n <= s.item_cap) return 0;
   size_t cap = std::max<size_t>(n, 2 * s.item_cap);
   HIPTRY(hipSetDevice(s.dev));
   bm_item* h_items = nullptr;
-  HIPTRY(hipHostMalloc(&h_items, cap * sizeof(bm_item), hipHostMallocDefault));
+  HIPTRY(hipHostMalloc(&h_items, stage_bytes(cap), hipHostMallocDefault));
   if (s.h_items) {
     std::memcpy(h_items, s.h_items, std::min<size_t>(s.nitems, s.item_cap) * sizeof(bm_item));
     HIPTRY(hipHostFree(s.h_items));
@@ -132,15 +134,11 @@ int ensure_items(Shard& s, size_t n) {
   if (s.d_items) {
     HIPTRY(hipFree(s.d_items));
     HIPTRY(hipFree(s.d_res));
-    HIPTRY(hipFree(s.d_ctr));
     HIPTRY(hipHostFree(s.h_res));
   }
-  HIPTRY(hipMalloc(&s.d_items, cap * sizeof(bm_item)));
-  HIPTRY(hipMalloc(&s.d_ctr, (cap + 2) * sizeof(unsigned long long)));
-  s.d_trials = s.d_ctr;
-  s.d_queue = s.d_ctr + 2;
-  HIPTRY(hipMalloc(&s.d_res, cap * sizeof(bm_result)));
-  HIPTRY(hipHostMalloc(&s.h_res, cap * sizeof(bm_result), hipHostMallocDefault));
+  HIPTRY(hipMalloc(&s.d_items, stage_bytes(cap)));
+  HIPTRY(hipMalloc(&s.d_res, (cap + 1) * sizeof(bm_result)));
+  HIPTRY(hipHostMalloc(&s.h_res, (cap + 1) * sizeof(bm_result), hipHostMallocDefault));
   s.item_cap = cap;
   return 0;
 }
@@ -150,10 +148,8 @@ void free_shard(Shard& s) {
   (void)hipSetDevice(s.dev);
   if (s.d_items) (void)hipFree(s.d_items);
   if (s.d_res) (void)hipFree(s.d_res);
-  if (s.d_ctr) (void)hipFree(s.d_ctr);
   if (s.h_items) (void)hipHostFree(s.h_items);
   if (s.h_res) (void)hipHostFree(s.h_res);
-  if (s.h_trials) (void)hipHostFree(s.h_trials);
   if (s.d_parts) (void)hipFree(s.d_parts);
   if (s.h_parts) (void)hipHostFree(s.h_parts);
   for (int c = 0; c < 2; ++c)
@@ -183,7 +179,6 @@ int make_shard(int dev, Shard& s) {
   s.resident = (uint32_t)std::max(1, bm_search_resident_per_cu()) * (uint32_t)s.cus;
   if (const char* e = std::getenv("BMPOW_COLUMNS"))  // A/B knob: columns per shard and window
     if (std::atoi(e) > 0) s.resident = (uint32_t)std::atoi(e);
-  HIPTRY(hipHostMalloc(&s.h_trials, sizeof(unsigned long long), hipHostMallocDefault));
   return ensure_items(s, 1024);
 }
 
@@ -410,6 +405,10 @@ int stage_items(const bmsched::StepPlan& p) {
     if (rc < 0) return rc;
     if (!items.empty()) std::memcpy(sh.h_items, items.data(), items.size() * sizeof(bm_item));
     sh.nitems = (uint32_t)items.size();
+    // the counters after the items, zeroed here so the step's one upload resets them
+    std::memset(sh.h_items + sh.nitems, 0, (2 + (size_t)sh.nitems) * sizeof(unsigned long long));
+    sh.d_trials = reinterpret_cast<unsigned long long*>(sh.d_items + sh.nitems);
+    sh.d_queue = sh.d_trials + 2;
     sh.nchunks = p.nchunks[s];
     sh.nmain = p.nmain.empty() ? sh.nitems : p.nmain[s];
     sh.chmain = p.chmain.empty() ? sh.nchunks : p.chmain[s];
@@ -447,8 +446,7 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     Shard& sh = g_shards[s];
     if (sh.nitems == 0) continue;
     HIPTRY(hipSetDevice(sh.dev));
-    HIPTRY(hipMemcpyAsync(sh.d_items, sh.h_items, sh.nitems * sizeof(bm_item), hipMemcpyHostToDevice, sh.stream));
-    HIPTRY(hipMemsetAsync(sh.d_ctr, 0, (2 + sh.nitems) * sizeof(unsigned long long), sh.stream));
+    HIPTRY(hipMemcpyAsync(sh.d_items, sh.h_items, stage_bytes(sh.nitems), hipMemcpyHostToDevice, sh.stream));
   }
   for (size_t s = 0; s < S; ++s) {
     Shard& sh = g_shards[s];
@@ -477,9 +475,9 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     if (sh.nitems == 0) continue;
     HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(bm_launch_resolve(sh.stream, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best,
-                             b->dev[s].d_found, sh.d_res, b->dev[s].d_vpool));
-    HIPTRY(hipMemcpyAsync(sh.h_res, sh.d_res, sh.nitems * sizeof(bm_result), hipMemcpyDeviceToHost, sh.stream));
-    HIPTRY(hipMemcpyAsync(sh.h_trials, sh.d_trials, sizeof(unsigned long long), hipMemcpyDeviceToHost, sh.stream));
+                             b->dev[s].d_found, sh.d_res, b->dev[s].d_vpool, sh.d_trials));
+    HIPTRY(hipMemcpyAsync(sh.h_res, sh.d_res, (sh.nitems + 1) * sizeof(bm_result), hipMemcpyDeviceToHost,
+                          sh.stream));
   }
   uint64_t step_trials = 0;
   double step_max_ms = 0;
@@ -494,8 +492,9 @@ int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
     g_stats.kernel_ms += ms;
     g_stats.launches++;
     step_max_ms = std::max<double>(step_max_ms, ms);
-    step_trials += *sh.h_trials;
-    g_rates.sample(s, *sh.h_trials, ms);
+    const uint64_t tr = sh.h_res[sh.nitems].nonce;  // the trials counter, after the results
+    step_trials += tr;
+    g_rates.sample(s, tr, ms);
   }
   b->dirty = false;  // every shard's resolve ran: best/found are (UINT64_MAX, 0) again
   g_stats.trials += step_trials;

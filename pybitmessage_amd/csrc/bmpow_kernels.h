@@ -96,10 +96,11 @@ hipError_t bm_launch_search_var(hipStream_t st, uint32_t nwg, const bm_obj* objs
                                 unsigned long long* trials_done, unsigned long long* queue, const bm_xbound& xb,
                                 const uint64_t* vpool);
 // vpool: the batch's var pool (may be null when no object of the launch is var-form)
-// Writes each item's result and puts its object's best/found back to (UINT64_MAX, 0).
+// Writes each item's result and puts its object's best/found back to (UINT64_MAX, 0); res[nitems].nonce
+// = trials[0] (the step's trial count, so one copy brings both home).
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                              unsigned long long* best, uint32_t* found, bm_result* res,
-                             const uint64_t* vpool);
+                             const uint64_t* vpool, const unsigned long long* trials);
 hipError_t bm_launch_mintrial(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                               bm_minpart* parts);
 hipError_t bm_launch_mintrial_var(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items,

@@ -40,8 +40,17 @@ __device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce, const uint64_t* v
 __global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
                                   uint32_t nitems, unsigned long long* __restrict__ best,
                                   uint32_t* __restrict__ found, bm_result* __restrict__ res,
-                                  const uint64_t* __restrict__ vpool) {
+                                  const uint64_t* __restrict__ vpool,
+                                  const unsigned long long* __restrict__ trials) {
   const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k == 0) {  // the step's trial count rides home after the results (one copy)
+    bm_result t;
+    t.nonce = trials[0];
+    t.trial = 0;
+    t.found = 0;
+    t.pad = 0;
+    res[nitems] = t;
+  }
   if (k >= nitems) return;
   const uint32_t obj = items[k].obj;  // at most one item per object in a shard's step
   bm_result r;
@@ -73,10 +82,10 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_trials_kernel(const bm_obj* __res
 // ---------------------------------------------------------------------------------------
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                              unsigned long long* best, uint32_t* found, bm_result* res,
-                             const uint64_t* vpool) {
+                             const uint64_t* vpool, const unsigned long long* trials) {
   const uint32_t bs = 64;
-  hipLaunchKernelGGL(bm_resolve_kernel, dim3((nitems + bs - 1) / bs), dim3(bs), 0, st, objs, items, nitems,
-                     best, found, res, vpool);
+  hipLaunchKernelGGL(bm_resolve_kernel, dim3((nitems + bs) / bs), dim3(bs), 0, st, objs, items, nitems,
+                     best, found, res, vpool, trials);
   return hipGetLastError();
 }
 

@@ -15,6 +15,8 @@
 #   c1-columns       tools/diag/c1_columns.py (C1 waste by column count)
 #   atomic-rate      tools/diag/atomic_rate (single-address atomic rate)
 #   ubench-mix       tools/ubench_mix (the search kernel's instruction-mix issue ceiling)
+#   rehearse-n2 | rehearse-n8   the driver's N-rank bench command with every rank on GPU 0
+#                    (--share-device: launch, claiming, barriers, one JSON line; not a scaling number)
 set -euo pipefail
 OUT=${1:?outdir}; shift
 mkdir -p "$OUT"
@@ -41,6 +43,10 @@ for step in "$@"; do
     c1-columns) timeout -k 10 300 python3 tools/diag/c1_columns.py parent 0 1024 512 > "$OUT/c1_columns.jsonl" 2> "$OUT/c1_columns.err" ;;
     atomic-rate) timeout -k 10 120 ./tools/diag/atomic_rate > "$OUT/atomic_rate.jsonl" 2> "$OUT/atomic_rate.err" ;;
     ubench-mix) timeout -k 10 300 ./tools/ubench_mix > "$OUT/ubench_mix.jsonl" 2> "$OUT/ubench_mix.err" ;;
+    rehearse-n*) n=${step#rehearse-n}
+      timeout -k 10 500 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
+        --master-port $((29500 + n)) bench.py --gpus "$n" --steps 1 --warmup 1 --share-device \
+        > "$OUT/bench_n$n.json" 2> "$OUT/bench_n$n.err" ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
 done
