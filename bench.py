@@ -51,6 +51,8 @@ BASELINE_MD_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
 #: pair in it (SQ_ACTIVE_INST_VALU2); bm_search_kernel's mix is 73 % half-rate VOP3 (v_alignbit_b32,
 #: v_lshl_add_u64, v_lshrrev_b64), so its ceiling is one instruction per SIMD per quad-cycle.
 SIMDS = 256 * 4
+#: v_bitop3_b32 per trial in bm_search_kernel's nonce loop (tools/isa_census.py): the pairable share
+BITOP3_PER_TRIAL = 1716
 
 
 def object_target(L, ttl, ntpb=1000, extra=1000):
@@ -911,8 +913,19 @@ def summarize(args, dist, r, lib_version):
                     'ghs': round(ceil, 4), 'frac': round(kernel_ghs / ceil, 4),
                     'basis': '1,024 SIMDs x one VALU instruction per quad-cycle x 64 lanes / VALU instructions '
                              'per trial (SQ_INSTS_VALU), at the PMC run clock (GRBM_GUI_ACTIVE / 8 / kernel time)'}
+                # every v_bitop3_b32 paired with another wave's: the hard issue bound of this
+                # instruction mix (the other 73 % issue one per quad-cycle)
+                slots = pmc['valu_instr_per_trial'] - BITOP3_PER_TRIAL / 2
+                pceil = SIMDS * pmc['eff_clock_ghz'] * 1e9 / 4 * 64 / slots / 1e9
+                line['roofline']['all_pairs_bound'] = {
+                    'ghs': round(pceil, 4), 'frac': round(kernel_ghs / pceil, 4),
+                    'basis': 'one issue slot per quad-cycle for each VALU instruction but a pair of v_bitop3_b32 '
+                             '(%d per trial, tools/isa_census.py) sharing one: (VALU per trial - %d / 2) slots'
+                             % (BITOP3_PER_TRIAL, BITOP3_PER_TRIAL)}
                 mix = mix_ceiling()
                 if mix:
+                    # the free-running instruction-mix microbenchmark: measured, but below what the
+                    # kernel issues since round 3 (the queue's barrier phases the waves better)
                     mceil = ceil * mix['valu_per_simd_quadcycle']
                     line['roofline']['mix_ceiling'] = dict(mix, ghs=round(mceil, 4))
                     line['roofline']['frac_vs_mix_ceiling'] = round(kernel_ghs / mceil, 4)

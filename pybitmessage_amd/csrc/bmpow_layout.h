@@ -42,18 +42,21 @@ inline uint64_t bm_var_words(uint64_t len) { return 16 + 80 * (bm_var_blocks(len
 #endif
 
 // Work item = one object's nonce window [start, start + count) inside one launch (48 B), cut into
-// blocks of BM_BLOCK nonces (one per lane).  The window's blocks are dealt to `gn` workgroup
-// COLUMNS: column c hashes blocks c, c + gn, c + 2 gn, ... in ascending order, so the columns sweep
-// the window together, one block row at a time, and a hit at nonce n leaves at most one row above
-// n in flight (each column stops at its next block above the running minimum).  This item runs
-// columns [g0, g0 + nwg) as its nwg workgroups; a window cut over several items (shards) has one
-// item per piece, each with its own g0 and the common gn.
-//   * a window on one shard: one item, g0 = 0, gn = nwg (capped at the shard's resident workgroups,
-//     so every column of the window is on the chip at once -- a persistent sweep);
+// blocks of BM_BLOCK nonces (one per lane).  The item's workgroups take its blocks IN ORDER from a
+// per-item counter (the block queue, bmpow_kernels.h: the k-th block taken is bm_block_of(item, k)),
+// so the hashed set is a prefix of the item's blocks plus those in flight, and a workgroup stops at
+// its next block above the running minimum.  The order is that of the item's COLUMNS: the window's
+// blocks are dealt round-robin to gn columns (column c: blocks c, c + gn, c + 2 gn, ...), this item
+// owns columns [g0, g0 + nwg) and runs nwg workgroups, and its k-th block is row k / nwg of column
+// g0 + k % nwg.
+//   * a window on one shard: one item, g0 = 0, gn = nwg (capped at the shard's resident workgroups),
+//     so the k-th block is simply block k;
 //   * a window split over the S shards (fewer pending objects than shards): one item per shard, all
 //     covering the whole window, interleaved: shard s runs columns [g0_s, g0_s + nwg_s) of gn = sum
-//     nwg_s -- so every device sweeps the same front -- and the shards share the window's running
+//     nwg_s -- so every device sweeps the same rows -- and the shards share the window's running
 //     minimum through the cross-shard bound (xslot, below).
+// The min-trial probe (no early exit) runs the same items as static columns: workgroup c of the item
+// hashes column g0 + c top to bottom.
 struct bm_item {
   uint64_t start;       // first nonce of the window
   uint64_t count;       // nonces in the window (> 0; start + count - 1 <= 2^64 - 1)
