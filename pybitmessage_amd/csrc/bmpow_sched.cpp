@@ -231,6 +231,8 @@ void set_pending(BatchState& b, size_t first, size_t count, bool pending) {
 // ---------------------------------------------------------------------------------------
 // search steps
 // ---------------------------------------------------------------------------------------
+uint32_t g_chunks_per_worker = 1;
+
 void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident,
            bool split, const double* weights) {
   p.items.assign(S, std::vector<bm_item>());
@@ -292,7 +294,8 @@ void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, S
       it.obj = w.obj;
       it.chunk_base = p.nchunks[s];
       const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
-      uint64_t G = std::min<uint64_t>(seg_end - c, nblk);
+      const uint64_t cpw = std::max<uint32_t>(1, g_chunks_per_worker);
+      uint64_t G = std::min<uint64_t>((seg_end - c + cpw - 1) / cpw, nblk);
       if (resident) G = std::min<uint64_t>(G, resident);
       it.g0 = 0;
       it.gn = (uint32_t)G;

@@ -119,6 +119,11 @@ void split_kinds(const std::vector<bm_obj>& objs, bool any_var, StepPlan& p);
 //     slower shard gets fewer chunks; split mode keeps equal columns (every shard sweeps the same rows).
 void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident = 0,
            bool split = false, const double* weights = nullptr);
+// Chunks of a piece per workgroup in the default mode (a piece of c chunks gets ceil(c / this)
+// workgroups, at most `resident`): each workgroup then takes that many chunks' blocks from the
+// item's queue before it ends, so fewer workgroups pay the start-up (the item search, the object's
+// words).  Set once by the library (bmpow_host.hip) before any step.
+extern uint32_t g_chunks_per_worker;
 
 // Per-shard throughput, to weight a step's slices.  The in-process multi-device step is lockstep
 // (launch on every shard, wait for all, plan the next), so the slowest shard sets its length; a
