@@ -232,8 +232,8 @@ int init_locked() {
   const auto vis = visible_gfx950();
   if (vis.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
   std::vector<int> ids = vis;
-  if (const char* e = std::getenv("BMPOW_CHUNKS_PER_WORKER"))  // A/B knob
-    if (std::atoi(e) > 0) bmsched::g_chunks_per_worker = (uint32_t)std::atoi(e);
+  if (const char* e = std::getenv("BMPOW_BLOCKS_PER_WORKER"))  // A/B knob
+    if (std::atoi(e) > 0) bmsched::g_blocks_per_worker = (uint32_t)std::atoi(e);
   if (const char* env = std::getenv("BMPOW_DEVICES")) {
     ids.clear();
     std::string e(env);

@@ -231,7 +231,7 @@ void set_pending(BatchState& b, size_t first, size_t count, bool pending) {
 // ---------------------------------------------------------------------------------------
 // search steps
 // ---------------------------------------------------------------------------------------
-uint32_t g_chunks_per_worker = 1;
+uint32_t g_blocks_per_worker = 0;
 
 void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident,
            bool split, const double* weights) {
@@ -294,8 +294,9 @@ void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, S
       it.obj = w.obj;
       it.chunk_base = p.nchunks[s];
       const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
-      const uint64_t cpw = std::max<uint32_t>(1, g_chunks_per_worker);
-      uint64_t G = std::min<uint64_t>((seg_end - c + cpw - 1) / cpw, nblk);
+      const uint64_t bpw =
+          g_blocks_per_worker ? g_blocks_per_worker : std::max<uint64_t>(1, std::min<uint64_t>(kBlocksPerWorker, chunk / BM_BLOCK));
+      uint64_t G = std::max<uint64_t>(1, (nblk + bpw - 1) / bpw);
       if (resident) G = std::min<uint64_t>(G, resident);
       it.g0 = 0;
       it.gn = (uint32_t)G;

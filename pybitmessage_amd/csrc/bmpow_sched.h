@@ -119,11 +119,16 @@ void split_kinds(const std::vector<bm_obj>& objs, bool any_var, StepPlan& p);
 //     slower shard gets fewer chunks; split mode keeps equal columns (every shard sweeps the same rows).
 void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident = 0,
            bool split = false, const double* weights = nullptr);
-// Chunks of a piece per workgroup in the default mode (a piece of c chunks gets ceil(c / this)
-// workgroups, at most `resident`): each workgroup then takes that many chunks' blocks from the
-// item's queue before it ends, so fewer workgroups pay the start-up (the item search, the object's
-// words).  Set once by the library (bmpow_host.hip) before any step.
-extern uint32_t g_chunks_per_worker;
+// Blocks of a piece per workgroup in the default mode: a piece of n blocks gets ceil(n / this)
+// workgroups, at most `resident`.  Each workgroup takes about that many blocks from the item's queue
+// before the item runs dry, so this sets how long the workgroups live, and the launch's tail with it.
+// Same box, twice each (profiles/r03/waves_queue_ab/blocks_per_worker_ab.txt): 16 blocks 6.644 /
+// 6.654 GH/s on the C5 sample and 6.656 / 6.661 on C2, against 6.633 / 6.634 and 6.648 / 6.649 at 32
+// (one workgroup per chunk) and 6.633 / 6.642, 6.648 / 6.646 at 8; 128 and 512 were 2 % and 9 %
+// slower.  g_blocks_per_worker (0 = kBlocksPerWorker, at most a chunk) is set once by the library
+// (bmpow_host.hip, BMPOW_BLOCKS_PER_WORKER for A/B runs).
+constexpr uint64_t kBlocksPerWorker = 16;
+extern uint32_t g_blocks_per_worker;
 
 // Per-shard throughput, to weight a step's slices.  The in-process multi-device step is lockstep
 // (launch on every shard, wait for all, plan the next), so the slowest shard sets its length; a
