@@ -114,12 +114,12 @@ bmsched::ShardRates g_rates;
 bool g_inited = false;
 bmpow_stats g_stats{};
 
-// Grow the shard's item staging to hold n items.  Called while a step's item list is being
-// filled, so the host items already written (s.nitems of them) move to the new buffer; the device
-// copies and the results are (re)written after the fill.
 // Bytes of a step's upload for n items: the items, then 2 + n counters.
 size_t stage_bytes(size_t n) { return n * sizeof(bm_item) + (2 + n) * sizeof(unsigned long long); }
 
+// Grow the shard's item staging to hold n items.  Called while a step's item list is being
+// filled, so the host items already written (s.nitems of them) move to the new buffer; the device
+// copies and the results are (re)written after the fill.
 int ensure_items(Shard& s, size_t n) {
   if (n <= s.item_cap) return 0;
   size_t cap = std::max<size_t>(n, 2 * s.item_cap);
@@ -1225,6 +1225,7 @@ int bmpow_get_devices(int* ids, int cap) {
 
 int bmpow_get_shard_rates(double* rates, int cap) {
   std::lock_guard<std::mutex> lk(g_mu);
+  if (!rates && cap > 0) return set_err(BMPOW_E_ARG, "null pointer");
   for (int i = 0; i < (int)g_shards.size() && i < cap; ++i)
     rates[i] = i < (int)g_rates.ema.size() ? g_rates.ema[i] : 0.0;
   return (int)g_shards.size();

@@ -108,8 +108,8 @@ void split_kinds(const std::vector<bm_obj>& objs, bool any_var, StepPlan& p);
 // Deal the step's windows (C chunks, ascending chunk0) to S shards as work items (bmpow_layout.h).
 //   * default: the flattened chunk list is cut into S contiguous slices -- big windows are
 //     nonce-sharded, small ones object-sharded -- and each (window, shard) piece is one item whose
-//     columns sweep its sub-range; a piece gets at most `resident` workgroups (0 = no cap: one per
-//     chunk), the workgroups its shard keeps on the chip at once, so its sweep is one front;
+//     workgroups take its blocks in order; a piece gets one workgroup per g_blocks_per_worker blocks,
+//     at most `resident` (0 = no cap), the workgroups its shard keeps on the chip at once;
 //   * split (fewer pending objects than shards, S > 1): every shard gets an item over each whole
 //     window, interleaved column by column (shard s runs columns [g0_s, g0_s + G) of S x G), so all
 //     devices sweep the same front, and the window's cross-shard bound slot (p.nx of them) lets a hit
