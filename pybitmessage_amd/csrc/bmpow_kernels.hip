@@ -126,6 +126,15 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
     // load's latency overlaps the wait at the barrier below.  Same box (profiles/r03/fresh_bound_ab.txt):
     // C1 waste 1.3-1.4 % against 2.1 % with the load issued before the hash; C3 6.705-6.707 against
     // 6.703-6.708 GH/s.  A stale value is only conservative.
+    //
+    // Each wave reads it itself, so two waves of the workgroup may see different values and part:
+    // one stops, another goes on.  That is safe.  The one that stops saw a real hit below the next
+    // block, so the lanes it leaves unhashed lie above an answer; the one that goes on finds its
+    // slots no longer refreshed by thread 0 and re-hashes blocks it already hashed (their hits are
+    // real ones) until its own read shows the hit -- within two blocks, since the last slot written
+    // holds the block the other wave stopped at.  Sharing thread 0's read through LDS instead keeps
+    // the waves in step but exposes the load's latency before the barrier: 4.7 % slower (C3 6.39
+    // against 6.70 GH/s, same box, profiles/r03/steal_ab/lds_bound_ab.txt).
     const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0) s_k[slot] = kn;
     __syncthreads();

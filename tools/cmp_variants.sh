@@ -1,12 +1,24 @@
 #!/bin/bash
-# C3 kernel rate of alternative builds of libbmpow_hip.so (BMPOW_LIB) on the same box.
-#   usage: tools/cmp_variants.sh OUTDIR variant...   (variant = default | build/<name>)
+# Kernel rate of alternative builds of libbmpow_hip.so (BMPOW_LIB) on the same box.
+#   usage: [CONFIGS="c3 c2 c5"] tools/cmp_variants.sh OUTDIR variant...   (variant = default | variants/<name>)
+# c3: 2^35 nonces, 2 steps; c2: the default bench, 2 steps; c5: a 4,096-object sample, 1 step.
 set -e
 OUT=${1:?outdir}; shift
 mkdir -p "$OUT"
+CONFIGS=${CONFIGS:-c3}
+i=0
 for v in "$@"; do
   if [ "$v" = default ]; then L=pybitmessage_amd/lib/libbmpow_hip.so; else L=$v/libbmpow_hip.so; fi
-  n=$(basename "$v")
-  BMPOW_LIB=$L timeout -k 10 120 python3 bench.py --config c3 --c3-log2 35 --steps 2 --warmup 1 --no-cpu-baseline > "$OUT/c3_$n.json"
-  python3 -c "import json;d=json.load(open('$OUT/c3_$n.json'));r=d['roofline'];print('$n', r['kernel_ghs'], r['avg_launch_ms'])"
+  n=$(basename "$v")_$i; i=$((i + 1))
+  line="$n"
+  for c in $CONFIGS; do
+    case $c in
+      c3) args=(--config c3 --c3-log2 35 --steps 2 --warmup 1) ;;
+      c2) args=(--steps 2 --warmup 1) ;;
+      c5) args=(--config c5 --objects 4096 --steps 1 --warmup 0) ;;
+    esac
+    BMPOW_LIB=$L timeout -k 10 200 python3 bench.py "${args[@]}" --no-cpu-baseline > "$OUT/${c}_$n.json"
+    line="$line $(python3 -c "import json;d=json.load(open('$OUT/${c}_$n.json'));r=d['roofline'];print('$c', d['value'], r['kernel_ghs'])")"
+  done
+  echo "$line"
 done
