@@ -65,6 +65,18 @@ def test_load_binds_all_signatures(rawlib):
 
 
 @pytest.mark.skipif(os.path.exists('/dev/kfd'), reason='a GPU is present')
+def test_shard_rates_without_devices():
+    """bmpow_get_shard_rates reads host state only: no shard selected yet, and a null buffer with a
+    positive capacity is an argument error rather than a crash."""
+    lib = _lib.load()
+    rates = (ctypes.c_double * 4)(-1, -1, -1, -1)
+    assert lib.bmpow_get_shard_rates(rates, 4) == 0
+    assert list(rates) == [-1, -1, -1, -1]
+    assert lib.bmpow_get_shard_rates(None, 4) == _lib.E_ARG
+    assert lib.bmpow_get_shard_rates(None, 0) == 0
+
+
+@pytest.mark.skipif(os.path.exists('/dev/kfd'), reason='a GPU is present')
 def test_no_device_fails_loudly():
     lib = _lib.load()
     assert lib.bmpow_device_count() == 0
