@@ -186,3 +186,19 @@ def test_nonce_sharding_over_every_device(gpulib, shards, coracle, golden):
     objs, _ = bench.make_objects('c4', 0, 2)
     res = proofofwork.run_batch(objs)
     assert_exact_first_nonces(gpulib, objs, res)
+
+
+def test_device_count_selector(gpulib, shards, golden):
+    """SURVEY 8(b)'s `int bmpow_set_devices(int ndev)` form (bmpow_set_device_count): the first ndev
+    visible devices, rejected below 1 or above the visible count, and the search exact after it."""
+    ndev = gpulib.bmpow_device_count()
+    assert ndev >= 1
+    assert gpulib.bmpow_set_device_count(1) == 1
+    ids = (ctypes.c_int * 64)()
+    assert gpulib.bmpow_get_devices(ids, 64) == 1 and ids[0] == 0
+    assert gpulib.bmpow_set_device_count(0) == _lib.E_ARG
+    assert gpulib.bmpow_set_device_count(ndev + 1) == _lib.E_ARG
+    assert gpulib.bmpow_set_devices(None, ndev) == ndev  # the NULL-list spelling of the same
+    assert gpulib.bmpow_get_devices(ids, 64) == ndev and list(ids[:ndev]) == list(range(ndev))
+    k = [k for k in golden('first_nonce_kats.json')['kats'] if k['nonce'] == 10909138][0]
+    assert proofofwork.run(k['target'], bytes.fromhex(k['ih'])) == [k['trial'], k['nonce']]
