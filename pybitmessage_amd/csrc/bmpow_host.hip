@@ -37,7 +37,11 @@
 namespace {
 
 constexpr uint64_t kU64Max = ~0ULL;
-constexpr uint64_t kDefaultStepTrials = 1ULL << 28;  // per shard per step, ~40-60 ms on MI355X
+// Per shard per step: ~80 ms on one MI355X, the interrupt granularity of a batch.  Against 2^28, the
+// launch's tail and the host's planning between launches cost half as much: C2 6.683 / 6.679 against
+// 6.668 / 6.658 GH/s, the C5 sample 6.667 / 6.674 against 6.662 / 6.664 (same box, twice each;
+// 2^30 no better; profiles/r03/step_trials_ab.txt).
+constexpr uint64_t kDefaultStepTrials = 1ULL << 29;
 
 thread_local std::string g_err;
 std::mutex g_mu;

@@ -434,7 +434,7 @@ class PowService(object):
     it waits; the library re-hashes each found nonce on the host inside that call, the check
     ``_doGPUPoW`` makes with hashlib) and resolves the futures,
     overlapping the Python work with the device's next step.  An object submitted mid-flight joins
-    the next step (~40 ms on one MI355X) instead of waiting for the objects ahead of it, and
+    the next step (~80 ms on one MI355X) instead of waiting for the objects ahead of it, and
     producers never contend for the device.  Replaces concurrent blocking ``run`` calls from the
     worker and API threads (``class_singleWorker.py:236,1276``, ``api.py:1304,1350``)."""
 

@@ -19,6 +19,8 @@ import random
 import numpy as np
 import pytest
 
+from conftest import default_step_trials
+
 import bench
 from pybitmessage_amd import _lib, proofofwork
 
@@ -116,7 +118,7 @@ def test_c5_default_difficulty_slice(gpulib, shards, coracle):
     kinds = {t for t, _ in objs}
     assert len(kinds) == 2 and min(kinds) > 4e11  # default difficulty, both object kinds
     res = proofofwork.run_batch(objs)
-    gpulib.bmpow_set_step_trials(1 << 28)
+    gpulib.bmpow_set_step_trials(default_step_trials(gpulib))
     hashed = assert_exact_first_nonces(gpulib, objs, res)
     assert hashed > 1e11
     rng = random.Random(55)
@@ -163,7 +165,7 @@ def test_c1_sweep_stops_within_rows_of_the_hit(gpulib, shards, golden, nshards):
 @pytest.mark.slow
 def test_c3_sweep_2_38_no_hit(gpulib):
     """C3: fixed initialHash, target 0, 2^38 nonces: no hit, and the device hashes exactly 2^38
-    trials (no window lost or repeated across 1,024 steps)."""
+    trials (no window lost or repeated across the 512 steps of 2^29)."""
     ih = hashlib.sha512(b'bmpow-sweep').digest()
     gpulib.bmpow_reset_stats()
     n, t = ctypes.c_uint64(), ctypes.c_uint64()

@@ -1,7 +1,8 @@
 #!/bin/bash
 # PMC passes for bm_search_kernel on the GPU box (one counter group per rocprofv3 run, no
 # tracing domains beside --pmc).  Workload: C3 sweep (target 0, fixed initialHash) of
-# 2^LOG2 nonces = 2^(LOG2-28) full launches of 2^28 trials each.
+# 2^LOG2 nonces = 2^(LOG2-28) full launches of 2^28 trials each (--step-trials: the PMC method
+# stays at 2^28-trial launches whatever the library default).
 #   usage: tools/profile_pmc.sh OUTDIR [LOG2]
 set -euo pipefail
 OUT=${1:?outdir}
@@ -9,7 +10,7 @@ LOG2=${2:-33}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 md5sum pybitmessage_amd/lib/libbmpow_hip.so > "$OUT/lib.md5"
-CMD=(python3 bench.py --config c3 --c3-log2 "$LOG2" --steps 1 --warmup 0 --no-cpu-baseline)
+CMD=(python3 bench.py --config c3 --c3-log2 "$LOG2" --steps 1 --warmup 0 --no-cpu-baseline --step-trials 268435456)
 if [ -n "${PMC_DEFAULT_BENCH:-}" ]; then CMD=(python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline); fi
 pass() {
   local name=$1; shift
