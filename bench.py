@@ -904,7 +904,16 @@ def summarize(args, dist, r, lib_version):
         }
         pmc = pmc_counters()
         if pmc:
-            line['roofline']['traffic'] = pmc.pop('traffic')
+            # PMC bytes per 2^28-trial launch, scaled to this run's launches (the traffic -- the block
+            # queue's atomics and the item loads -- grows with the trials a launch hashes)
+            pmc_traffic, pmc_trials = pmc.pop('traffic'), pmc.pop('trials_per_launch', None)
+            per_launch = st.trials / max(launches, 1)
+            if pmc_traffic is not None and pmc_trials:
+                line['roofline']['traffic'] = round(pmc_traffic * per_launch / pmc_trials)
+                line['roofline']['traffic_basis'] = ('%.0f B per %d-trial PMC launch x %.0f trials per launch here'
+                                                     % (pmc_traffic, pmc_trials, per_launch))
+            else:
+                line['roofline']['traffic'] = pmc_traffic
             line['roofline']['counters'] = pmc
             if pmc.get('valu_instr_per_trial') and pmc.get('eff_clock_ghz'):
                 # one wave64 VALU instruction per SIMD per quad-cycle, at the PMC run's clock
@@ -971,7 +980,7 @@ def pmc_counters():
         full = json.load(f)
     d = full['derived']
     out = {'traffic': d.get('hbm_bytes_per_launch_upper'), 'source': 'profiles/pmc_latest.json (C3, 2^28-trial launches)',
-           'build': full.get('build')}
+           'build': full.get('build'), 'trials_per_launch': full.get('raw', {}).get('trials_per_launch')}
     for k in ('valu_instr_per_trial', 'valu_issue_util', 'valu_instr_per_simd_quad_cycle', 'dual_issue_share',
               'simd_busy_frac', 'wave_issue_stall_share', 'wave_wait_share', 'eff_clock_ghz'):
         if d.get(k) is not None:

@@ -92,6 +92,10 @@ def test_two_rank_aggregation(tmp_path):
     assert line['objects_per_s'] == round(16 / 2.0, 3)
     assert line['performed_ghs'] == round(3000 / 2.0 / 1e9, 4)
     assert r1['line']['value'] == line['value']  # every rank sees the same reduction
+    # the committed PMC traffic (per 2^28-trial launch) scaled to this rank's trials per launch
+    pmc = json.load(open(os.path.join(bench.ROOT, 'profiles', 'pmc_latest.json')))
+    want = pmc['derived']['hbm_bytes_per_launch_upper'] * (1000 / 2) / pmc['raw']['trials_per_launch']
+    assert line['roofline']['traffic'] == round(want) and 'traffic_basis' in line['roofline']
     # each rank works on its own batch (seed + rank): no object is solved twice
     assert r0['first_ih'] != r1['first_ih']
 
