@@ -113,11 +113,28 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
       const uint64_t first = it.start + off;
       const uint64_t nonce = first + threadIdx.x;
       const uint64_t tv = trial_of(ihw, nonce);
+#ifndef BM_LANE_ATOMICS
+      // Wavefront min-reduction of the hits: a wave's 64 nonces are consecutive, so its smallest hit
+      // is its lowest hitting lane -- one atomicMin per wave instead of one per hitting lane.  Same
+      // box (profiles/r03/waves_queue_ab/wave_min_ab.txt): C3 6.713-6.718 against 6.709-6.718 GH/s
+      // with lane atomics (BM_LANE_ATOMICS), C2 6.674-6.681 against 6.678, and the hit-heavy C5
+      // flood at test-mode difficulty 5.816-5.837 against 5.761-5.835.
+      const uint64_t hits = __builtin_amdgcn_ballot_w64(off + threadIdx.x < it.count && tv <= target);
+      if (hits) {
+        const uint64_t wmin = first + (threadIdx.x & ~63u) + (uint64_t)__builtin_ctzll(hits);
+        if ((threadIdx.x & 63) == 0) {
+          const unsigned long long prev = atomicMin(bestp, (unsigned long long)wmin);
+          __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (kX && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < wmin ? prev : wmin);
+        }
+      }
+#else
       if (off + threadIdx.x < it.count && tv <= target) {
         const unsigned long long prev = atomicMin(bestp, (unsigned long long)nonce);
         __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (kX && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
       }
+#endif
       done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
     }
     // Early exit: the running minimum (for a split window also the other shards' hits, folded in by

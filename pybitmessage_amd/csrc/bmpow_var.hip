@@ -73,10 +73,15 @@ __device__ __forceinline__ void search_var_column(const bm_obj* __restrict__ obj
     const uint64_t first = it.start + off;
     const uint64_t nonce = first + threadIdx.x;
     const uint64_t tv = trial_var(mw, m + 16, nb, nonce);
-    if (off + threadIdx.x < it.count && tv <= target) {
-      const unsigned long long prev = atomicMin(bestp, (unsigned long long)nonce);
-      __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (xb && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
+    // the wave's smallest hit is its lowest hitting lane (consecutive nonces): one atomicMin per wave
+    const uint64_t hits = __builtin_amdgcn_ballot_w64(off + threadIdx.x < it.count && tv <= target);
+    if (hits) {
+      const uint64_t wmin = first + (threadIdx.x & ~63u) + (uint64_t)__builtin_ctzll(hits);
+      if ((threadIdx.x & 63) == 0) {
+        const unsigned long long prev = atomicMin(bestp, (unsigned long long)wmin);
+        __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (xb && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < wmin ? prev : wmin);
+      }
     }
     const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
