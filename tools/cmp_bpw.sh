@@ -1,6 +1,6 @@
 #!/bin/bash
 # C5 (4,096-object sample) and C2 kernel rate at several BMPOW_BLOCKS_PER_WORKER values, same box.
-#   usage: tools/cmp_cpw.sh OUTDIR value...
+#   usage: tools/cmp_bpw.sh OUTDIR value...
 set -e
 OUT=${1:?outdir}; shift
 mkdir -p "$OUT"
