@@ -222,7 +222,12 @@ def run_batch_bench(args, dist):
     tg = np.array([t for t, _ in objs], dtype=np.uint64)
     p64 = ctypes.POINTER(ctypes.c_uint64)
     chunk = n if dist.world == 1 else max(1, min(8, per_gpu // 8))
-    low_water = max(chunk, min(128, per_gpu // 4))
+    # Objects a rank keeps pending (N > 1).  When the global batch runs out each rank still has these
+    # to finish, and an object's remaining work is ~E whatever it has hashed (the hit is memoryless),
+    # so the spread between ranks' tails grows as the square root of this count: 32 (C2: ~0.8 % of a
+    # step at 8 GPUs by that estimate, against ~1.7 % at 128) still gives one GPU thousands of
+    # workgroups per step, since a single window already fills the chip (the block queue).
+    low_water = max(chunk, min(32, per_gpu // 4))
     claimer = Claimer(dist, n, chunk)
     h = lib.bmpow_batch_create(n, ihs, tg.ctypes.data_as(p64), None)
     if not h:
