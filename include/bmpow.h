@@ -355,7 +355,8 @@ typedef struct bmpow_stats {
 BMPOW_API int bmpow_get_stats(bmpow_stats *out);
 BMPOW_API void bmpow_reset_stats(void);
 
-/* Default per-shard trial budget of one step (one kernel launch); settable for tests. */
+/* Per-shard trial budget of one step (one kernel launch), default 2^29 (~80 ms on one MI355X: the
+ * interrupt granularity of a batch); set 0 to restore the default.  At least one chunk (8,192). */
 BMPOW_API uint64_t bmpow_get_step_trials(void);
 BMPOW_API void bmpow_set_step_trials(uint64_t trials_per_shard);
 

@@ -1856,7 +1856,7 @@ uint64_t bmpow_get_step_trials(void) { return g_step_trials.load(); }
 
 void bmpow_set_step_trials(uint64_t t) {
   std::lock_guard<std::mutex> lk(g_mu);
-  g_step_trials.store(std::max<uint64_t>(t, BM_CHUNK));
+  g_step_trials.store(t ? std::max<uint64_t>(t, BM_CHUNK) : kDefaultStepTrials);
 }
 
 unsigned long long BitmessagePOW(unsigned char* starthash, unsigned long long target) {

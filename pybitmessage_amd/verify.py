@@ -131,7 +131,7 @@ def isProofOfWorkSufficient_batch(objects, nonceTrialsPerByte=0, payloadLengthEx
         _lib.check(lib, rc, 'bmpow_verify_batch_ptrs')
         if 2 in ok:
             raise struct.error('unpack requires a buffer of 8 bytes')
-        return np.frombuffer(ok, dtype=np.uint8).view(np.bool_).tolist()
+        return fast.verdicts(ok)
     if set(map(type, objs)) - {bytes}:  # bytearray / memoryview: one bytes copy each
         objs = [o if type(o) is bytes else bytes(o) for o in objs]
     ptrs = _pointers(objs)

@@ -35,23 +35,11 @@ def coracle():
     return oracle.COracle()
 
 
-_DEFAULT_STEP = []
-
-
-def default_step_trials(lib):
-    """The library's own per-step trial budget, as it was before any test changed it."""
-    if not _DEFAULT_STEP:
-        _DEFAULT_STEP.append(lib.bmpow_get_step_trials())
-    return _DEFAULT_STEP[0]
-
-
 @pytest.fixture(scope='session')
 def gpulib():
     """libbmpow_hip.so initialised on the GPU (gpu tests only)."""
     from pybitmessage_amd import _lib
-    lib = _lib.get()
-    default_step_trials(lib)
-    return lib
+    return _lib.get()
 
 
 @pytest.fixture
@@ -64,7 +52,7 @@ def shards(gpulib):
         assert gpulib.bmpow_set_devices(arr, len(ids)) == len(ids)
     yield use
     gpulib.bmpow_set_devices(None, 0)
-    gpulib.bmpow_set_step_trials(default_step_trials(gpulib))
+    gpulib.bmpow_set_step_trials(0)  # the library's default
 
 
 @pytest.fixture(autouse=True)

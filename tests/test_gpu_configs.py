@@ -19,7 +19,6 @@ import random
 import numpy as np
 import pytest
 
-from conftest import default_step_trials
 
 import bench
 from pybitmessage_amd import _lib, proofofwork
@@ -118,7 +117,7 @@ def test_c5_default_difficulty_slice(gpulib, shards, coracle):
     kinds = {t for t, _ in objs}
     assert len(kinds) == 2 and min(kinds) > 4e11  # default difficulty, both object kinds
     res = proofofwork.run_batch(objs)
-    gpulib.bmpow_set_step_trials(default_step_trials(gpulib))
+    gpulib.bmpow_set_step_trials(0)  # the library's default
     hashed = assert_exact_first_nonces(gpulib, objs, res)
     assert hashed > 1e11
     rng = random.Random(55)

@@ -9,7 +9,6 @@ import time
 import numpy as np
 import pytest
 
-from conftest import default_step_trials
 
 from pybitmessage_amd import _lib, proofofwork, state
 
@@ -230,7 +229,7 @@ def test_min_trial_large_range(gpulib, coracle):
         ih = hashlib.sha512(b'min-trial').digest()
         assert gpu_min_trial(gpulib, [ih], [12345], [2000000]) == [coracle.min_trial(ih, 12345, 2000000)]
     finally:
-        gpulib.bmpow_set_step_trials(default_step_trials(gpulib))
+        gpulib.bmpow_set_step_trials(0)  # the library's default
 
 
 def test_search_batch_stateless_resume(gpulib, coracle):
@@ -405,7 +404,7 @@ def test_session_add_and_take_done(gpulib, coracle):
                 got[sid] = (o, (int(trial_b[j]), int(nonce_b[j])))
     finally:
         gpulib.bmpow_batch_destroy(h)
-        gpulib.bmpow_set_step_trials(default_step_trials(gpulib))
+        gpulib.bmpow_set_step_trials(0)  # the library's default
     assert len(got) == serial
     for (t, ih), res in got.values():
         assert res == coracle.search(ih, t)
@@ -487,4 +486,4 @@ def test_native_service_producers_cancel_abort(gpulib, coracle):
     finally:
         gpulib.bmpow_clear_abort()
         gpulib.bmpow_service_destroy(s)
-        gpulib.bmpow_set_step_trials(default_step_trials(gpulib))
+        gpulib.bmpow_set_step_trials(0)  # the library's default

@@ -64,6 +64,19 @@ def test_load_binds_all_signatures(rawlib):
     assert lib.bmpow_get_step_trials() > 0
 
 
+def test_step_trials_setting():
+    """The per-step budget (host state only): at least one chunk, and 0 restores the default."""
+    lib = _lib.load()
+    default = lib.bmpow_get_step_trials()
+    assert default == 1 << 29
+    lib.bmpow_set_step_trials(1 << 20)
+    assert lib.bmpow_get_step_trials() == 1 << 20
+    lib.bmpow_set_step_trials(5)
+    assert lib.bmpow_get_step_trials() == 8192
+    lib.bmpow_set_step_trials(0)
+    assert lib.bmpow_get_step_trials() == default
+
+
 @pytest.mark.skipif(os.path.exists('/dev/kfd'), reason='a GPU is present')
 def test_shard_rates_without_devices():
     """bmpow_get_shard_rates reads host state only: no shard selected yet, and a null buffer with a

@@ -58,6 +58,30 @@ def test_host_verdict_arithmetic_matches_reference(hostlib, kats):
             assert targets.isProofOfWorkSufficient(obj, c['ntpb'], c['extra'], c['recvTime']) == c['ok']
 
 
+def test_fast_verdict_list():
+    """_bmpow_fast.verdicts: bytes of 0/1 -> list of bools, with the singletons' reference counts
+    balanced (added in two sums, released one by one when the list goes)."""
+    import sys
+
+    from pybitmessage_amd import verify
+    fast = verify._fast()
+    assert fast is not None, 'the CPython marshalling module is built by build()'
+    rng = random.Random(3)
+    ok = bytes(rng.getrandbits(1) for _ in range(10001))
+    nt = sum(ok)
+    assert 4000 < nt < 6000
+    rt, rf = sys.getrefcount(True), sys.getrefcount(False)
+    got = fast.verdicts(ok)
+    dt, df = sys.getrefcount(True) - rt, sys.getrefcount(False) - rf
+    assert abs(dt - nt) <= 2 and abs(df - (len(ok) - nt)) <= 2, (dt, df, nt)  # +-2: interpreter temporaries
+    assert got == [bool(b) for b in ok] and all(type(v) is bool for v in got)
+    del got
+    assert abs(sys.getrefcount(True) - rt) <= 2 and abs(sys.getrefcount(False) - rf) <= 2
+    assert fast.verdicts(b'') == []
+    with pytest.raises(TypeError):
+        fast.verdicts(bytearray(b'\x01'))
+
+
 def test_host_verdict_random_vs_restatement(hostlib):
     rng = random.Random(11)
     for _ in range(3000):
