@@ -112,7 +112,11 @@ static PyObject *verify_list(PyObject *self, PyObject *args) {
     rc = ((verify_ptrs_fn)(uintptr_t)fn_addr)((size_t)n, sc->ptrs, sc->lens, vn, ve, vr,
                                               (uint8_t *)PyBytes_AS_STRING(ok));
     Py_END_ALLOW_THREADS
-    for (Py_ssize_t i = 0; i < n; ++i) Py_DECREF(sc->held[i]);
+    /* the headers were evicted by the payload pass meanwhile: ask for them ahead again */
+    for (Py_ssize_t i = 0; i < n; ++i) {
+        if (i + 16 < n) __builtin_prefetch(sc->held[i + 16], 1);
+        Py_DECREF(sc->held[i]);
+    }
     sc->busy = 0;
     scratch_free(&own);
     PyObject *res = Py_BuildValue("(iO)", rc, ok);
