@@ -140,7 +140,9 @@ static PyObject *verdicts(PyObject *self, PyObject *arg) {
         nt += t;
         items[i] = t ? Py_True : Py_False;
     }
-    /* one reference per slot, added in two sums instead of n increments of two shared counters */
+    /* one reference per slot, added in two sums instead of n increments of two shared counters (on
+     * an interpreter with immortal singletons, 3.12+, Py_SET_REFCNT leaves them alone, as Py_INCREF
+     * would) */
     Py_SET_REFCNT(Py_True, Py_REFCNT(Py_True) + nt);
     Py_SET_REFCNT(Py_False, Py_REFCNT(Py_False) + (n - nt));
     return list;
