@@ -6,19 +6,20 @@
 //
 // Execution model (one launch = one bounded "step" of the host scheduler, bmpow_host.hip):
 //   * the launch covers a list of work items; item = (object, nonce window, its columns);
-//   * the window is cut into blocks of BM_BLOCK nonces dealt round-robin to gn workgroup columns
-//     (bmpow_layout.h): column c, iteration i hashes block c + i*gn, lane l nonce
-//     start + (c + i*gn)*BM_BLOCK + l -- the columns sweep the window together, so the hashed set is
-//     always a prefix of the window plus at most one block row;
-//   * a hit does atomicMin(best[obj], nonce) -- the per-object minimum over the launch -- and
-//     sets found[obj]: best[] starts at UINT64_MAX, which is also a legal nonce (2^64-1), so
-//     "no hit" is found[obj] == 0, never a best[] value;
-//   * exact first-nonce semantics: a column whose next block starts above the running minimum
-//     cannot hold the answer, so it stops (checked at start and after every block with an
-//     agent-scope load: the early exit never skips a nonce below the answer); for a window split
-//     over shards the launch's relay workgroup folds the other shards' hits (the host-pinned
-//     cross-shard bound) into that running minimum;
-//   * pure integer VALU -- no LDS, no MFMA, no HBM traffic beyond ~100 B per workgroup.
+//   * the window is cut into blocks of BM_BLOCK nonces, one per lane; the item's workgroups take them
+//     IN ORDER from the item's block queue (a per-item counter, bm_block_of in bmpow_kernels.h), so
+//     the hashed set is always a prefix of the window plus the blocks in flight, however unevenly
+//     the workgroups progress (the SIMD arbiter favours older waves);
+//   * each wave reduces its hits to its lowest hitting lane (its 64 nonces are consecutive) and does
+//     one atomicMin(best[obj], nonce) -- the per-object minimum over the launch -- and sets
+//     found[obj]: best[] starts at UINT64_MAX, which is also a legal nonce (2^64-1), so "no hit" is
+//     found[obj] == 0, never a best[] value;
+//   * exact first-nonce semantics: a workgroup whose next block starts above the running minimum
+//     stops (an agent-scope load after each block: the early exit never skips a nonce below the
+//     answer); for a window split over shards the launch's relay workgroup folds the other shards'
+//     hits (the host-pinned cross-shard bound) into that running minimum;
+//   * pure integer VALU -- no MFMA, 16 B of LDS (the block index), and memory traffic of one queue
+//     atomic per 256 trials plus ~100 B per workgroup.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
