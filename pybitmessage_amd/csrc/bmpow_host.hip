@@ -4,17 +4,18 @@
 //   BitmessagePOW          src/bitmsghash/bitmsghash.cpp:127-165  (pthreads + OpenSSL)
 //   do_opencl_pow/initCL   src/openclpow.py:31-111                (pyopencl window loop)
 //
-// Scheduler ("step" = one kernel launch per shard, bounded so the caller can poll its
-// shutdown flag between steps, dev/powinterrupttest.py:22-37):
-//   1. take the pending objects in index order; give each k chunks (k*BM_CHUNK nonces,
-//      contiguous from its next_start) so that the step totals ~budget trials;
-//   2. flatten all windows into one chunk list and cut it into S contiguous slices, one per
-//      shard (device/stream): large objects are nonce-sharded, small ones object-sharded;
-//   3. per shard: upload the item list, launch bm_search_kernel (+ bm_resolve_kernel),
-//      read back per-item {min hit nonce, trial};
-//   4. host min-reduction over shards per object -- the only cross-device exchange (no
-//      RCCL: no data moves between GPUs).  An object with a hit in this step is final
-//      (its whole window below the hit has been hashed); otherwise next_start += window.
+// Scheduler (round 4: per-device stepping, bmsched::Engine in bmpow_sched.cpp).  One stepper thread
+// and stream per shard (device, or a stream of one).  Whenever a shard has fewer than two launches
+// in flight, its stepper claims windows from the objects' frontiers under the engine's mutex --
+// its fair share of the objects, each a window of its step's budget, or one piece each of windows
+// split over every shard when fewer objects than shards are pending -- and enqueues the launch
+// behind the running one: items up, bm_search_kernel (+ the var-form kernel), bm_resolve_kernel,
+// results home.  When a launch completes, its per-item minima are folded into the objects (the host
+// min-reduction over shards; no RCCL: no data moves between GPUs); an object is final once every
+// window below its least hit has completed on whichever shard ran it.  No shard waits for another.
+// The entry points (bounded searches, batch steps, the service) let the steppers claim a trial
+// budget and wait for what they need, so the caller polls its shutdown flag between bounded calls
+// (dev/powinterrupttest.py:22-37).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -37,14 +38,14 @@
 namespace {
 
 constexpr uint64_t kU64Max = ~0ULL;
-// Per shard per step: ~80 ms on one MI355X, the interrupt granularity of a batch.  Against 2^28, the
+// Per shard per launch: ~80 ms on one MI355X, the interrupt granularity of a batch.  Against 2^28, the
 // launch's tail and the host's planning between launches cost half as much: C2 6.683 / 6.679 against
 // 6.668 / 6.658 GH/s, the C5 sample 6.667 / 6.674 against 6.662 / 6.664 (same box, twice each;
 // 2^30 no better; profiles/r03/step_trials_ab.txt).
 constexpr uint64_t kDefaultStepTrials = 1ULL << 29;
 
 thread_local std::string g_err;
-std::mutex g_mu;
+std::mutex g_mu;  // one entry point at a time (the steppers never take it)
 std::atomic<int> g_abort{0};
 std::atomic<uint64_t> g_step_trials{kDefaultStepTrials};  // read without the lock (bmpow_get_step_trials)
 
@@ -60,16 +61,44 @@ int set_err(int code, const std::string& msg) {
       return set_err(BMPOW_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));           \
   } while (0)
 
+// How a stepper waits for its launch (BMPOW_WAIT, read once): "block" (default) sleeps in
+// hipEventSynchronize on an event created with hipEventBlockingSync -- the thread uses no CPU while
+// the GPU works; "spin" is HIP's default wait (busy); "poll" queries the event every 50 us.
+enum WaitMode { kWaitBlock, kWaitSpin, kWaitPoll };
+WaitMode g_wait = kWaitBlock;
+// run()'s single-object path (search_one): BMPOW_WAIT1 "spin" (default) polls the result word,
+// "block" sleeps in hipEventSynchronize on a blocking-sync event first; BMPOW_ONE=0 sends run()
+// through the engine instead (A/B).
+bool g_one_block = false;
+bool g_one_enabled = true;
+
+// One of a shard's two engine launch buffers (the running launch and the one staged behind it).
+struct LaunchBuf {
+  bm_item* h_items = nullptr;  // pinned: items, then 2 + n counters (zeroed on the host)
+  bm_item* d_items = nullptr;
+  bm_result* h_res = nullptr;  // pinned: results, then the trials counter
+  bm_result* d_res = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr, evd = nullptr;  // search start / end, launch done
+};
+
+// Pinned staging of slot records for the slot-init kernel (an add while launches are in flight):
+// reused once the kernel that read it has run.
+struct UpBuf {
+  uint8_t* h = nullptr;
+  uint8_t* d = nullptr;  // the device's address of h
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  bool pending = false;
+};
+
 struct Shard {
   int dev = -1;
   hipStream_t stream = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  // per-step staging (capacity grows)
-  // a step's upload, one copy: its items, then its counters (zeroed on the host) -- [0] trials hashed,
-  // [1] the relay's finished workgroups, then per item the next block of its window to hand out (the
-  // block queue, bmpow_kernels.h).  d_trials / d_queue point into it for the current step.
+  // per-step staging of the min-trial probe (capacity grows): its items, then its counters
   bm_item* d_items = nullptr;
-  bm_result* d_res = nullptr;      // nitems results, then the trials counter (bm_resolve_kernel)
+  bm_result* d_res = nullptr;
   unsigned long long* d_trials = nullptr;
   unsigned long long* d_queue = nullptr;
   bm_item* h_items = nullptr;      // pinned, the same layout
@@ -82,8 +111,10 @@ struct Shard {
   bm_minpart* d_parts = nullptr;
   bm_minpart* h_parts = nullptr;  // pinned
   size_t parts_cap = 0;
-  // stats
-  double kernel_ms = 0.0;
+  // the engine's launches (searches)
+  LaunchBuf lb[2];
+  std::vector<UpBuf> up;
+  double t_prev_done = 0;  // steady-clock ms when the stepper last saw a launch complete
   // address search: the fixed-base comb tables (v * 2^(W i) * G) for W = 16 ([0]) and 24 ([1]),
   // built on first use and shared by the shards of one device (owns_table marks the freeing one)
   ec::ge* d_table[2] = {nullptr, nullptr};
@@ -110,11 +141,11 @@ std::vector<Shard> g_shards;
 // The cross-shard bound (bmpow_layout.h): BM_MAX_SHARDS rows of BM_XSLOTS words, host-pinned, coherent
 // and mapped into every device; allocated with the shard set.
 unsigned long long* g_xb = nullptr;
-// Columns a work item may get per shard (slice's `resident`): the device's resident workgroups over
-// the shards sharing it, so every shard's sweep is on the chip at once.
+// Columns a work item may get per shard: the device's resident workgroups over the shards sharing
+// it, so every shard's sweep is on the chip at once.
 uint32_t g_resident = 0;
-// per-shard throughput of the search launches: the weights of the next step's slices (bmpow_sched.h)
-bmsched::ShardRates g_rates;
+// The per-device steppers over the shard set (created with it; bmsched::Engine).
+std::unique_ptr<bmsched::Engine> g_engine;
 bool g_inited = false;
 bmpow_stats g_stats{};
 
@@ -147,15 +178,51 @@ int ensure_items(Shard& s, size_t n) {
   return 0;
 }
 
+// Grow an engine launch buffer to n items (only ever called for a buffer not in flight).
+int ensure_launch_buf(Shard& s, LaunchBuf& lb, size_t n) {
+  if (n <= lb.cap) return 0;
+  const size_t cap = std::max<size_t>({n, 2 * lb.cap, 1024});
+  HIPTRY(hipSetDevice(s.dev));
+  if (lb.h_items) HIPTRY(hipHostFree(lb.h_items));
+  if (lb.d_items) HIPTRY(hipFree(lb.d_items));
+  if (lb.h_res) HIPTRY(hipHostFree(lb.h_res));
+  if (lb.d_res) HIPTRY(hipFree(lb.d_res));
+  lb.h_items = nullptr;
+  lb.d_items = nullptr;
+  lb.h_res = nullptr;
+  lb.d_res = nullptr;
+  lb.cap = 0;
+  HIPTRY(hipHostMalloc(&lb.h_items, stage_bytes(cap), hipHostMallocDefault));
+  HIPTRY(hipMalloc(&lb.d_items, stage_bytes(cap)));
+  HIPTRY(hipHostMalloc(&lb.h_res, (cap + 1) * sizeof(bm_result), hipHostMallocDefault));
+  HIPTRY(hipMalloc(&lb.d_res, (cap + 1) * sizeof(bm_result)));
+  lb.cap = cap;
+  return 0;
+}
+
 void free_shard(Shard& s) {
   if (s.dev < 0) return;
   (void)hipSetDevice(s.dev);
+  if (s.stream) (void)hipStreamSynchronize(s.stream);
   if (s.d_items) (void)hipFree(s.d_items);
   if (s.d_res) (void)hipFree(s.d_res);
   if (s.h_items) (void)hipHostFree(s.h_items);
   if (s.h_res) (void)hipHostFree(s.h_res);
   if (s.d_parts) (void)hipFree(s.d_parts);
   if (s.h_parts) (void)hipHostFree(s.h_parts);
+  for (LaunchBuf& lb : s.lb) {
+    if (lb.h_items) (void)hipHostFree(lb.h_items);
+    if (lb.d_items) (void)hipFree(lb.d_items);
+    if (lb.h_res) (void)hipHostFree(lb.h_res);
+    if (lb.d_res) (void)hipFree(lb.d_res);
+    if (lb.ev0) (void)hipEventDestroy(lb.ev0);
+    if (lb.ev1) (void)hipEventDestroy(lb.ev1);
+    if (lb.evd) (void)hipEventDestroy(lb.evd);
+  }
+  for (UpBuf& u : s.up) {
+    if (u.h) (void)hipHostFree(u.h);
+    if (u.ev) (void)hipEventDestroy(u.ev);
+  }
   for (int c = 0; c < 2; ++c)
     if (s.d_table[c] && s.owns_table[c]) (void)hipFree(s.d_table[c]);
   for (int c = 0; c < 2; ++c) {
@@ -179,6 +246,12 @@ int make_shard(int dev, Shard& s) {
   HIPTRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
   HIPTRY(hipEventCreate(&s.ev0));
   HIPTRY(hipEventCreate(&s.ev1));
+  for (LaunchBuf& lb : s.lb) {
+    HIPTRY(hipEventCreate(&lb.ev0));
+    HIPTRY(hipEventCreate(&lb.ev1));
+    HIPTRY(hipEventCreateWithFlags(&lb.evd, hipEventDisableTiming |
+                                                (g_wait == kWaitBlock ? hipEventBlockingSync : 0)));
+  }
   HIPTRY(hipDeviceGetAttribute(&s.cus, hipDeviceAttributeMultiprocessorCount, dev));
   s.resident = (uint32_t)std::max(1, bm_search_resident_per_cu()) * (uint32_t)s.cus;
   if (const char* e = std::getenv("BMPOW_COLUMNS"))  // A/B knob: columns per shard and window
@@ -198,7 +271,42 @@ std::vector<int> visible_gfx950() {
   return out;
 }
 
+double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// ---- the engine's device side (bmsched::EngineOps) ----
+int engine_launch(bmsched::Launch& L, std::string& err);
+int engine_wait(bmsched::Launch& L, std::string& err);
+
+void engine_xstore(uint32_t x, uint64_t v) {
+  // every shard's row: the relays poll their own row (bm_relay); plain stores to coherent pinned memory
+  for (size_t r = 0; r < g_shards.size(); ++r) __atomic_store_n(&g_xb[r * BM_XSLOTS + x], (unsigned long long)v, __ATOMIC_RELAXED);
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+}
+
+void make_engine() {
+  bmsched::EngineOps ops;
+  ops.launch = engine_launch;
+  ops.wait = engine_wait;
+  ops.xstore = engine_xstore;
+  ops.aborted = [] { return g_abort.load() != 0; };
+  ops.thread_init = [](size_t s) {
+    (void)hipSetDevice(g_shards[s].dev);
+    bmsched::set_thread_background();
+  };
+  g_engine.reset(new bmsched::Engine(ops, g_shards.size(), g_resident, g_step_trials.load()));
+  if (const char* e = std::getenv("BMPOW_THROTTLE")) {  // A/B knob "shard:ms" (the throttled-shard GPU test)
+    const char* c = std::strchr(e, ':');
+    if (c) g_engine->set_throttle((size_t)std::atoi(e), std::atof(c + 1));
+  }
+}
+
+void free_one();
+
 int select_devices(const std::vector<int>& ids) {
+  g_engine.reset();  // joins the steppers once their launches are applied
+  free_one();
   for (auto& s : g_shards) free_shard(s);
   g_shards.clear();
   if (ids.size() > BM_MAX_SHARDS) return set_err(BMPOW_E_ARG, "more than BM_MAX_SHARDS shards");
@@ -218,7 +326,6 @@ int select_devices(const std::vector<int>& ids) {
     for (size_t i = 0; i < (size_t)BM_MAX_SHARDS * BM_XSLOTS; ++i) g_xb[i] = ~0ULL;
   }
   g_resident = ~0u;
-  g_rates.reset(g_shards.size());
   for (auto& sh : g_shards) {
     HIPTRY(hipSetDevice(sh.dev));
     void* dp = nullptr;
@@ -228,11 +335,16 @@ int select_devices(const std::vector<int>& ids) {
                                                   [&](const Shard& o) { return o.dev == sh.dev; });
     g_resident = std::min<uint32_t>(g_resident, std::max<uint32_t>(1, sh.resident / same));
   }
+  make_engine();
   return (int)g_shards.size();
 }
 
 int init_locked() {
   if (g_inited) return (int)g_shards.size();
+  if (const char* w = std::getenv("BMPOW_WAIT"))
+    g_wait = std::strcmp(w, "spin") == 0 ? kWaitSpin : (std::strcmp(w, "poll") == 0 ? kWaitPoll : kWaitBlock);
+  if (const char* w = std::getenv("BMPOW_WAIT1")) g_one_block = std::strcmp(w, "block") == 0;
+  if (const char* w = std::getenv("BMPOW_ONE")) g_one_enabled = std::atoi(w) != 0;
   const auto vis = visible_gfx950();
   if (vis.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
   std::vector<int> ids = vis;
@@ -263,7 +375,9 @@ using bmsched::pack_obj;
 
 // ---------------------------------------------------------------------------------------
 // Batch state: the object table and per-object running minimum stay in HBM for the
-// lifetime of the batch (one copy per shard).
+// lifetime of the batch (one copy per shard).  best[]/found[] persist across launches: a launch
+// queued behind another on the same stream stops at once above the hit the earlier one left there;
+// a slot is reset on the device when it gets a new object (slot init, stream-ordered).
 // ---------------------------------------------------------------------------------------
 struct bmpow_batch : bmsched::BatchState {
   struct Dev {
@@ -273,9 +387,6 @@ struct bmpow_batch : bmsched::BatchState {
     uint64_t* d_vpool = nullptr;           // copy of vpool (var-form objects' words), vcap words
   };
   std::vector<Dev> dev;  // one per shard (indexed like g_shards)
-  // a step was launched and not completed (an error mid-step): the devices' best/found may hold a
-  // hit the resolve kernel did not reset, so a reuse of the slots must reset them
-  bool dirty = false;
   size_t vcap = 0;         // words allocated per shard for the var pool
   size_t vsynced = 0;      // vpool words already on the devices (of epoch vepoch)
   uint64_t vepoch = ~0ULL;
@@ -283,9 +394,16 @@ struct bmpow_batch : bmsched::BatchState {
 
 namespace {
 
+// The batch's launches must be finished before its device buffers change: drains the engine when
+// it is working on b.
+void quiesce(std::unique_lock<std::mutex>& lk, bmpow_batch* b) {
+  if (g_engine && g_engine->attached() == b) g_engine->drain(lk);
+}
+
 void batch_free_dev(bmpow_batch* b) {
   for (size_t s = 0; s < b->dev.size() && s < g_shards.size(); ++s) {
     (void)hipSetDevice(g_shards[s].dev);
+    (void)hipStreamSynchronize(g_shards[s].stream);
     if (b->dev[s].d_obj) (void)hipFree(b->dev[s].d_obj);
     if (b->dev[s].d_best) (void)hipFree(b->dev[s].d_best);
     if (b->dev[s].d_found) (void)hipFree(b->dev[s].d_found);
@@ -298,9 +416,9 @@ void batch_free_dev(bmpow_batch* b) {
 }
 
 // Bring the devices' copy of the var pool up to date: the words appended since the last sync (one
-// copy per shard), or all of them after a reallocation or a new epoch (bmsched::add emptied it).
-// Stream-ordered before the next launch on each shard.
-int sync_vpool(bmpow_batch* b) {
+// copy per shard, into words no launch reads yet), or all of them after a reallocation or a new
+// epoch (bmsched::add emptied it), which first drains the batch's launches.
+int sync_vpool(std::unique_lock<std::mutex>& lk, bmpow_batch* b) {
   const size_t n = b->vpool.size();
   if (b->vepoch != b->vpool_epoch) {
     b->vsynced = 0;
@@ -310,6 +428,7 @@ int sync_vpool(bmpow_batch* b) {
   const bool grow = n > b->vcap;
   const size_t cap = grow ? std::max<size_t>(n, 2 * b->vcap) : b->vcap;
   const size_t from = grow ? 0 : b->vsynced;
+  if (grow || from == 0) quiesce(lk, b);
   for (size_t s = 0; s < g_shards.size(); ++s) {
     Shard& sh = g_shards[s];
     HIPTRY(hipSetDevice(sh.dev));
@@ -321,7 +440,7 @@ int sync_vpool(bmpow_batch* b) {
       }
       HIPTRY(hipMalloc(&b->dev[s].d_vpool, cap * sizeof(uint64_t)));
     }
-    // the host vector may be appended to before the copy runs: stage through a synchronous copy
+    // the host vector may be appended to before an async copy ran: a synchronous copy
     HIPTRY(hipMemcpy(b->dev[s].d_vpool + from, b->vpool.data() + from, (n - from) * sizeof(uint64_t),
                      hipMemcpyHostToDevice));
   }
@@ -330,7 +449,7 @@ int sync_vpool(bmpow_batch* b) {
   return 0;
 }
 
-int batch_upload(bmpow_batch* b) {
+int batch_upload(std::unique_lock<std::mutex>& lk, bmpow_batch* b) {
   b->dev.assign(g_shards.size(), bmpow_batch::Dev());
   const size_t n = std::max<size_t>(b->cap, std::max<size_t>(b->n, 1));
   b->cap = n;
@@ -351,57 +470,88 @@ int batch_upload(bmpow_batch* b) {
     HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(hipStreamSynchronize(sh.stream));
   }
-  return sync_vpool(b);
+  return sync_vpool(lk, b);
 }
 
-int batch_init(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
-               const uint64_t* ih_off = nullptr) {
+int batch_init(std::unique_lock<std::mutex>& lk, bmpow_batch* b, size_t n, const uint8_t* ihs,
+               const uint64_t* targets, const uint64_t* start, const uint64_t* ih_off = nullptr) {
   bmsched::init(*b, n, ihs, targets, start, ih_off);
-  return batch_upload(b);
+  return batch_upload(lk, b);
 }
 
-// Append m objects to a live session between steps (bmsched::add: released slots first, then the
-// table grows -- device buffers reallocated at twice the size and re-uploaded from the host
-// mirror).  Otherwise only the slots written are uploaded, one copy per contiguous run.
-// Resetting best[] and found[] over those runs is safe between steps: a pending object's device
-// state is always (UINT64_MAX, 0) there, since a hit finishes its object in the step that finds it.
-int batch_add_locked(bmpow_batch* b, size_t m, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
-                     uint32_t* slot_out, const uint64_t* ih_off = nullptr) {
+// Write objects into slots of the devices' tables -- the record, best = UINT64_MAX, found = 0 --
+// on each shard's stream, behind whatever is in flight there (bm_slots_init_kernel reading the
+// records from pinned staging).  A launch planned before the slot got its new object and still
+// queued then reads the new record: what it finds are real hits of the new object, and its results
+// are stale (the slot's generation) anyway.
+int init_slots(bmpow_batch* b, const uint32_t* slots, size_t m) {
+  if (m == 0) return 0;
+  const size_t rec = m * sizeof(bm_obj), bytes = rec + m * sizeof(uint32_t);
+  for (size_t s = 0; s < g_shards.size(); ++s) {
+    Shard& sh = g_shards[s];
+    HIPTRY(hipSetDevice(sh.dev));
+    UpBuf* u = nullptr;
+    for (UpBuf& x : sh.up) {
+      if (x.pending && hipEventQuery(x.ev) == hipSuccess) x.pending = false;
+      if (!x.pending && (!u || (x.cap >= bytes && u->cap < bytes))) u = &x;
+    }
+    if (!u) {
+      sh.up.emplace_back();
+      u = &sh.up.back();
+      HIPTRY(hipEventCreateWithFlags(&u->ev, hipEventDisableTiming));
+    }
+    if (u->cap < bytes) {
+      if (u->h) HIPTRY(hipHostFree(u->h));
+      u->h = nullptr;
+      u->cap = 0;
+      const size_t cap = std::max<size_t>(bytes, 64 << 10);
+      HIPTRY(hipHostMalloc(&u->h, cap, hipHostMallocMapped));
+      void* dp = nullptr;
+      HIPTRY(hipHostGetDevicePointer(&dp, u->h, 0));
+      u->d = (uint8_t*)dp;
+      u->cap = cap;
+    }
+    bm_obj* recs = reinterpret_cast<bm_obj*>(u->h);
+    for (size_t i = 0; i < m; ++i) recs[i] = b->objs[slots[i]];
+    std::memcpy(u->h + rec, slots, m * sizeof(uint32_t));
+    HIPTRY(bm_launch_slots_init(sh.stream, b->dev[s].d_obj, b->dev[s].d_best, b->dev[s].d_found,
+                                reinterpret_cast<const bm_obj*>(u->d), reinterpret_cast<const uint32_t*>(u->d + rec),
+                                (uint32_t)m));
+    HIPTRY(hipEventRecord(u->ev, sh.stream));
+    u->pending = true;
+  }
+  return 0;
+}
+
+// Append m objects to a live session (bmsched::add: released slots first, then the table grows --
+// device buffers reallocated at twice the size and re-uploaded from the host mirror, after the
+// batch's launches drained).  Otherwise only the slots written go up (init_slots), behind the
+// launches in flight: the steppers go on.  lk holds the engine's mutex.
+int batch_add_locked(std::unique_lock<std::mutex>& lk, bmpow_batch* b, size_t m, const uint8_t* ihs,
+                     const uint64_t* targets, const uint64_t* start, uint32_t* slot_out,
+                     const uint64_t* ih_off = nullptr) {
   if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
   const size_t fresh = m > b->free_slots.size() ? m - b->free_slots.size() : 0;
   if (b->n + fresh > 0xffffffffULL) return set_err(BMPOW_E_ARG, "too many objects");
+  if (b->n + fresh > b->cap) quiesce(lk, b);  // the tables will be reallocated
   std::vector<uint32_t> slots;
   const bool grew = bmsched::add(*b, m, ihs, targets, start, slots, ih_off);
   if (slot_out) std::copy(slots.begin(), slots.end(), slot_out);
   if (grew) {
     b->cap = std::max<size_t>({b->n, 2 * b->cap, 1024});
     batch_free_dev(b);
-    return batch_upload(b);
+    const int rc = batch_upload(lk, b);
+    if (g_engine) g_engine->notify();
+    return rc;
   }
-  std::sort(slots.begin(), slots.end());
-  for (size_t s = 0; s < g_shards.size(); ++s) {
-    Shard& sh = g_shards[s];
-    HIPTRY(hipSetDevice(sh.dev));
-    for (size_t i = 0; i < slots.size();) {
-      size_t j = i + 1;
-      while (j < slots.size() && slots[j] == slots[j - 1] + 1) ++j;
-      const size_t lo = slots[i], cnt = j - i;
-      HIPTRY(hipMemcpyAsync(b->dev[s].d_obj + lo, b->objs.data() + lo, cnt * sizeof(bm_obj), hipMemcpyHostToDevice,
-                            sh.stream));
-      HIPTRY(hipMemsetAsync(b->dev[s].d_best + lo, 0xFF, cnt * sizeof(unsigned long long), sh.stream));
-      HIPTRY(hipMemsetAsync(b->dev[s].d_found + lo, 0, cnt * sizeof(uint32_t), sh.stream));
-      i = j;
-    }
-  }
-  for (auto& sh : g_shards) {
-    HIPTRY(hipSetDevice(sh.dev));
-    HIPTRY(hipStreamSynchronize(sh.stream));
-  }
-  return sync_vpool(b);
+  int rc = sync_vpool(lk, b);  // before the slots that use the new words are handed to the steppers' kernels
+  if (rc == 0) rc = init_slots(b, slots.data(), slots.size());
+  if (g_engine) g_engine->notify();
+  return rc;
 }
 
 // Stage the plan's per-shard item lists in the shards' pinned buffers (sized once per step, so
-// nothing written is ever reallocated under the copy).
+// nothing written is ever reallocated under the copy): the min-trial probe's staging.
 int stage_items(const bmsched::StepPlan& p) {
   for (size_t s = 0; s < g_shards.size(); ++s) {
     Shard& sh = g_shards[s];
@@ -422,99 +572,83 @@ int stage_items(const bmsched::StepPlan& p) {
   return 0;
 }
 
-// One bounded step.  Returns pending count (>= 0) or < 0.
-int batch_step_locked(bmpow_batch* b, uint64_t budget, uint64_t* trials_out) {
-  if (trials_out) *trials_out = 0;
-  if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
-  if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
-  const size_t S = g_shards.size();
-  // 1-2. windows for the pending objects, sliced over the shards (bmpow_sched.cpp)
-  bmsched::StepPlan plan;
-  std::vector<double> w;
-  const bool weighted = S > 1 && g_rates.weights(w);
-  if (!bmsched::plan_step(*b, budget, g_step_trials, S, plan, g_resident, weighted ? w.data() : nullptr)) return 0;
-  // windows split over the shards share a running minimum through the cross-shard bound: their
-  // slots start empty in every row, before any launch of the step
-  for (size_t s = 0; s < S; ++s)
-    for (uint32_t x = 0; x < plan.nx; ++x)
-      __atomic_store_n(&g_xb[s * BM_XSLOTS + x], ~0ULL, __ATOMIC_RELAXED);
-  if (plan.nx) __atomic_thread_fence(__ATOMIC_SEQ_CST);
-  {
-    int rc = stage_items(plan);
-    if (rc == 0) rc = sync_vpool(b);
-    if (rc < 0) return rc;
-  }
+// ---- the engine's device side ----
 
-  b->dirty = true;
-  // 3. stage every shard's items and counters, then launch on every shard back to back (the shards of a
-  // split window sweep the same rows, so their kernels should start together), then collect
-  for (size_t s = 0; s < S; ++s) {
-    Shard& sh = g_shards[s];
-    if (sh.nitems == 0) continue;
-    HIPTRY(hipSetDevice(sh.dev));
-    HIPTRY(hipMemcpyAsync(sh.d_items, sh.h_items, stage_bytes(sh.nitems), hipMemcpyHostToDevice, sh.stream));
+// Stage and enqueue one launch on its shard's stream: items and zeroed counters up (one copy), the
+// search kernel(s), the resolve kernel (each item's minimum and its trial value), results home.
+int engine_launch(bmsched::Launch& L, std::string& err) {
+  Shard& sh = g_shards[L.shard];
+  LaunchBuf& lb = sh.lb[L.buf];
+  bmpow_batch* b = static_cast<bmpow_batch*>(L.batch);
+  const std::vector<bm_item>& items = L.plan.items[0];
+  const size_t n = items.size();
+  int rc = ensure_launch_buf(sh, lb, std::max<size_t>(n, 1));
+  if (rc < 0) {
+    err = g_err;
+    return rc;
   }
-  for (size_t s = 0; s < S; ++s) {
-    Shard& sh = g_shards[s];
-    if (sh.nitems == 0) continue;
-    HIPTRY(hipSetDevice(sh.dev));
-    HIPTRY(hipEventRecord(sh.ev0, sh.stream));
-    bm_xbound xb;
-    if (plan.nx) {
-      xb.table = sh.d_xb;
-      xb.row = (uint32_t)s;
-      xb.rows = (uint32_t)S;
+  std::memcpy(lb.h_items, items.data(), n * sizeof(bm_item));
+  std::memset(lb.h_items + n, 0, (2 + n) * sizeof(unsigned long long));
+  unsigned long long* d_trials = reinterpret_cast<unsigned long long*>(lb.d_items + n);
+  unsigned long long* d_queue = d_trials + 2;
+  const uint32_t nmain = L.plan.nmain.empty() ? (uint32_t)n : L.plan.nmain[0];
+  const uint32_t nch = L.plan.nchunks[0];
+  const uint32_t chmain = L.plan.chmain.empty() ? nch : L.plan.chmain[0];
+  const bmpow_batch::Dev& d = b->dev[L.shard];
+  bm_xbound xb;
+  if (L.plan.nx) {
+    xb.table = sh.d_xb;
+    xb.row = (uint32_t)L.shard;
+    xb.rows = (uint32_t)g_shards.size();
+  }
+  hipError_t e = hipSetDevice(sh.dev);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(lb.d_items, lb.h_items, stage_bytes(n), hipMemcpyHostToDevice, sh.stream);
+  if (e == hipSuccess) e = hipEventRecord(lb.ev0, sh.stream);
+  if (e == hipSuccess && nmain)
+    e = bm_launch_search(sh.stream, chmain, d.d_obj, lb.d_items, nmain, d.d_best, d.d_found, d_trials, d_queue, xb);
+  if (e == hipSuccess && n > nmain && nmain && xb.table)  // the var launch's relay counts its own columns
+    e = hipMemsetAsync(d_trials + 1, 0, sizeof(unsigned long long), sh.stream);
+  if (e == hipSuccess && n > nmain)
+    e = bm_launch_search_var(sh.stream, nch - chmain, d.d_obj, lb.d_items + nmain, (uint32_t)n - nmain, d.d_best,
+                             d.d_found, d_trials, d_queue + nmain, xb, d.d_vpool);
+  if (e == hipSuccess) e = hipEventRecord(lb.ev1, sh.stream);
+  if (e == hipSuccess)
+    e = bm_launch_resolve(sh.stream, d.d_obj, lb.d_items, (uint32_t)n, d.d_best, d.d_found, lb.d_res, d.d_vpool,
+                          d_trials);
+  if (e == hipSuccess)
+    e = hipMemcpyAsync(lb.h_res, lb.d_res, (n + 1) * sizeof(bm_result), hipMemcpyDeviceToHost, sh.stream);
+  if (e == hipSuccess) e = hipEventRecord(lb.evd, sh.stream);
+  if (e != hipSuccess) {
+    err = std::string("search launch: ") + hipGetErrorString(e);
+    return BMPOW_E_HIP;
+  }
+  return 0;
+}
+
+int engine_wait(bmsched::Launch& L, std::string& err) {
+  Shard& sh = g_shards[L.shard];
+  LaunchBuf& lb = sh.lb[L.buf];
+  hipError_t e = hipSetDevice(sh.dev);
+  if (e == hipSuccess) {
+    if (g_wait == kWaitPoll) {
+      while ((e = hipEventQuery(lb.evd)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(50));
+    } else {
+      e = hipEventSynchronize(lb.evd);
     }
-    if (sh.nmain)
-      HIPTRY(bm_launch_search(sh.stream, sh.chmain, b->dev[s].d_obj, sh.d_items, sh.nmain, b->dev[s].d_best,
-                              b->dev[s].d_found, sh.d_trials, sh.d_queue, xb));
-    if (sh.nitems > sh.nmain && sh.nmain && xb.table)  // the var launch's relay counts its own columns
-      HIPTRY(hipMemsetAsync(sh.d_trials + 1, 0, sizeof(unsigned long long), sh.stream));
-    if (sh.nitems > sh.nmain)
-      HIPTRY(bm_launch_search_var(sh.stream, sh.nchunks - sh.chmain, b->dev[s].d_obj, sh.d_items + sh.nmain,
-                                  sh.nitems - sh.nmain, b->dev[s].d_best, b->dev[s].d_found, sh.d_trials,
-                                  sh.d_queue + sh.nmain, xb, b->dev[s].d_vpool));
-    HIPTRY(hipEventRecord(sh.ev1, sh.stream));
   }
-  for (size_t s = 0; s < S; ++s) {
-    Shard& sh = g_shards[s];
-    if (sh.nitems == 0) continue;
-    HIPTRY(hipSetDevice(sh.dev));
-    HIPTRY(bm_launch_resolve(sh.stream, b->dev[s].d_obj, sh.d_items, sh.nitems, b->dev[s].d_best,
-                             b->dev[s].d_found, sh.d_res, b->dev[s].d_vpool, sh.d_trials));
-    HIPTRY(hipMemcpyAsync(sh.h_res, sh.d_res, (sh.nitems + 1) * sizeof(bm_result), hipMemcpyDeviceToHost,
-                          sh.stream));
+  float ms = 0;
+  if (e == hipSuccess) e = hipEventElapsedTime(&ms, lb.ev0, lb.ev1);
+  if (e != hipSuccess) {
+    err = std::string("search wait: ") + hipGetErrorString(e);
+    return BMPOW_E_HIP;
   }
-  uint64_t step_trials = 0;
-  double step_max_ms = 0;
-  for (size_t s = 0; s < S; ++s) {
-    Shard& sh = g_shards[s];
-    if (sh.nitems == 0) continue;
-    HIPTRY(hipSetDevice(sh.dev));
-    HIPTRY(hipStreamSynchronize(sh.stream));
-    float ms = 0;
-    HIPTRY(hipEventElapsedTime(&ms, sh.ev0, sh.ev1));
-    sh.kernel_ms += ms;
-    g_stats.kernel_ms += ms;
-    g_stats.launches++;
-    step_max_ms = std::max<double>(step_max_ms, ms);
-    const uint64_t tr = sh.h_res[sh.nitems].nonce;  // the trials counter, after the results
-    step_trials += tr;
-    g_rates.sample(s, tr, ms);
-  }
-  b->dirty = false;  // every shard's resolve ran: best/found are (UINT64_MAX, 0) again
-  g_stats.trials += step_trials;
-  g_stats.steps++;
-  double mx = 0;
-  for (auto& sh : g_shards) mx = std::max(mx, sh.kernel_ms);
-  g_stats.max_shard_kernel_ms = mx;
-  if (trials_out) *trials_out = step_trials;
-
-  // 4. host min-reduction over shards per object (bmpow_sched.cpp)
-  std::vector<const bm_result*> res(S);
-  for (size_t s = 0; s < S; ++s) res[s] = g_shards[s].h_res;
-  bmsched::apply_step(*b, plan, res);
-  return (int)std::min<size_t>(b->pending, 0x7fffffff);
+  sh.t_prev_done = now_ms();
+  const size_t n = L.plan.items[0].size();
+  L.res.assign(lb.h_res, lb.h_res + n);
+  L.trials = lb.h_res[n].nonce;  // the trials counter rides home after the results
+  L.ms = ms;
+  return 0;
 }
 
 int ensure_parts(Shard& s, size_t n) {
@@ -630,40 +764,188 @@ int min_trial_locked(size_t n, const uint8_t* ihs, const uint64_t* start, const 
   return rc;
 }
 
-// Library-owned scratch batch reused by the stateless entry points.
+
+// Library-owned scratch batch reused by the stateless entry points (bmpow_search*, bmpow_search_batch).
 bmpow_batch* g_scratch = nullptr;
 
-// Reused while it is large enough and the device set is unchanged: a run() call (one object per
-// bounded bmpow_search) then pays one upload of its 128-B record, not three hipMalloc/hipFree pairs.
-int scratch_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
-                  const uint64_t* ih_off = nullptr) {
+// Re-initialise the scratch batch with n objects and attach it.  Reused while it is large enough and
+// the device set is unchanged: a run() call then writes its 128-B record into slot 0 behind whatever
+// is still in flight there (the previous call's lookahead launch, which stops at once on that call's
+// hit; its results are stale by the slot's generation), with no allocation and no host wait.
+int scratch_batch(std::unique_lock<std::mutex>& lk, size_t n, const uint8_t* ihs, const uint64_t* targets,
+                  const uint64_t* start, const uint64_t* ih_off = nullptr) {
   if (g_scratch && g_scratch->dev.size() == g_shards.size() && g_scratch->cap >= n) {
+    g_engine->attach(lk, g_scratch);
     const size_t cap = g_scratch->cap;
     bmsched::init(*g_scratch, n, ihs, targets, start, ih_off);
     g_scratch->cap = cap;
-    const int rc = sync_vpool(g_scratch);
+    int rc = sync_vpool(lk, g_scratch);
     if (rc < 0) return rc;
-    for (size_t s = 0; s < g_shards.size(); ++s) {
-      Shard& sh = g_shards[s];
-      HIPTRY(hipSetDevice(sh.dev));
-      if (!n) continue;
-      HIPTRY(hipMemcpyAsync(g_scratch->dev[s].d_obj, g_scratch->objs.data(), n * sizeof(bm_obj), hipMemcpyHostToDevice,
-                            sh.stream));
-      if (!g_scratch->dirty) continue;  // the last steps' resolve left every slot at (UINT64_MAX, 0)
-      HIPTRY(hipMemsetAsync(g_scratch->dev[s].d_best, 0xFF, n * sizeof(unsigned long long), sh.stream));
-      HIPTRY(hipMemsetAsync(g_scratch->dev[s].d_found, 0, n * sizeof(uint32_t), sh.stream));
-    }
-    g_scratch->dirty = false;
-    // no host sync needed: the step's launches follow on the same streams
-    return 0;
+    std::vector<uint32_t> slots(n);
+    for (size_t i = 0; i < n; ++i) slots[i] = (uint32_t)i;
+    return init_slots(g_scratch, slots.data(), n);
   }
   if (g_scratch) {
+    if (g_engine->attached() == g_scratch) g_engine->detach(lk);
     batch_free_dev(g_scratch);
     delete g_scratch;
     g_scratch = nullptr;
   }
   g_scratch = new bmpow_batch();
-  return batch_init(g_scratch, n, ihs, targets, start, ih_off);
+  g_engine->detach(lk);  // nothing may run while the new tables are uploaded synchronously
+  const int rc = batch_init(lk, g_scratch, n, ihs, targets, start, ih_off);
+  if (rc == 0) g_engine->attach(lk, g_scratch);
+  return rc;
+}
+
+// ---------------------------------------------------------------------------------------
+// run()'s single-object path on one shard (bm_search1_kernel, bm_one_* in bmpow_layout.h).  A serial
+// run() call -- every call site in the reference (class_singleWorker.py:236,1276, api.py:1304,1350)
+// -- needs the lowest latency per object: the object rides in the kernel arguments (no upload), each
+// window is one launch with the next window queued behind it (it stops at once on the call's hit),
+// and the launch's last wave writes the result into host-mapped memory that this thread polls (no
+// resolve kernel, no copy, no event wait, no stepper thread in between).
+// ---------------------------------------------------------------------------------------
+constexpr int kOneEvents = 8;
+struct OnePath {
+  int dev = -1;
+  bm_one_call* d_calls = nullptr;
+  bm_one_ctr* d_ctr = nullptr;
+  bm_one_out* h_out = nullptr;  // host-mapped ring of results
+  bm_one_out* d_out = nullptr;  // the device's address of h_out
+  hipEvent_t ev[kOneEvents] = {};
+  uint64_t call = 0, seq = 0;
+};
+OnePath g_one;
+
+void free_one() {
+  if (g_one.dev < 0) return;
+  (void)hipSetDevice(g_one.dev);
+  for (hipEvent_t& e : g_one.ev) {
+    if (e) (void)hipEventSynchronize(e);
+  }
+  if (g_one.d_calls) (void)hipFree(g_one.d_calls);
+  if (g_one.d_ctr) (void)hipFree(g_one.d_ctr);
+  if (g_one.h_out) (void)hipHostFree(g_one.h_out);
+  for (hipEvent_t& e : g_one.ev)
+    if (e) (void)hipEventDestroy(e);
+  g_one = OnePath();
+}
+
+int ensure_one(const Shard& sh) {
+  if (g_one.dev == sh.dev && g_one.d_calls) return 0;
+  free_one();
+  HIPTRY(hipSetDevice(sh.dev));
+  g_one.dev = sh.dev;
+  bm_one_call init[BM_ONE_CALLS];
+  std::memset(init, 0, sizeof init);
+  for (bm_one_call& c : init) c.best = ~0ULL;
+  HIPTRY(hipMalloc(&g_one.d_calls, sizeof init));
+  HIPTRY(hipMemcpy(g_one.d_calls, init, sizeof init, hipMemcpyHostToDevice));
+  HIPTRY(hipMalloc(&g_one.d_ctr, BM_ONE_RING * sizeof(bm_one_ctr)));
+  HIPTRY(hipMemset(g_one.d_ctr, 0, BM_ONE_RING * sizeof(bm_one_ctr)));
+  HIPTRY(hipHostMalloc(&g_one.h_out, BM_ONE_RING * sizeof(bm_one_out), hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(g_one.h_out, 0, BM_ONE_RING * sizeof(bm_one_out));
+  void* dp = nullptr;
+  HIPTRY(hipHostGetDevicePointer(&dp, g_one.h_out, 0));
+  g_one.d_out = (bm_one_out*)dp;
+  for (hipEvent_t& e : g_one.ev)
+    HIPTRY(hipEventCreateWithFlags(&e, hipEventDisableTiming | (g_one_block ? hipEventBlockingSync : 0)));
+  return 0;
+}
+
+// Wait for launch `seq`'s result word.  The event recorded behind the launch catches a launch that
+// ended without writing it (a fault) instead of spinning forever.
+int wait_one(uint64_t seq) {
+  bm_one_out* o = &g_one.h_out[seq % BM_ONE_RING];
+  hipEvent_t ev = g_one.ev[seq % kOneEvents];
+  if (g_one_block) HIPTRY(hipEventSynchronize(ev));
+  for (uint32_t spin = 1;; ++spin) {
+    if (__atomic_load_n(&o->seq, __ATOMIC_ACQUIRE) == seq) return 0;
+    if ((spin & 1023) == 0) {
+      const hipError_t e = hipEventQuery(ev);
+      if (e == hipSuccess) {
+        if (__atomic_load_n(&o->seq, __ATOMIC_ACQUIRE) == seq) return 0;
+        return set_err(BMPOW_E_HIP, "single-object launch completed without its result");
+      }
+      if (e != hipErrorNotReady) return set_err(BMPOW_E_HIP, std::string("single-object launch: ") + hipGetErrorString(e));
+    }
+    __builtin_ia32_pause();
+  }
+}
+
+int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials, uint64_t* nonce_out,
+               uint64_t* trial_out) {
+  Shard& sh = g_shards[0];
+  int rc = ensure_one(sh);
+  if (rc < 0) return rc;
+  HIPTRY(hipSetDevice(sh.dev));
+  const uint64_t end = (max_trials - 1 > kU64Max - start) ? kU64Max : start + max_trials - 1;  // last nonce
+  bm_one_args a;
+  std::memset(&a, 0, sizeof a);
+  for (int i = 0; i < 8; ++i) a.w[i] = bmsched::load_be64(ih + 8 * i);
+  a.target = target;
+  const uint64_t call = ++g_one.call;  // every call launches at least once (it resets call + 2's state)
+  a.call = g_one.d_calls + call % BM_ONE_CALLS;
+  a.reset = g_one.d_calls + (call + 2) % BM_ONE_CALLS;
+  const uint64_t step = g_step_trials.load();
+  const uint64_t bpw = bmsched::kBlocksPerWorker;
+  uint64_t next = start;
+  bool top = false;
+  uint64_t fly[4];  // sequence numbers in flight, oldest first
+  int nfly = 0;
+  auto launch = [&]() -> int {
+    const uint64_t room = end - next;  // nonces after next, up to end
+    const uint64_t count = room >= step ? step : room + 1;
+    const uint64_t nblk = count / BM_BLOCK + (count % BM_BLOCK ? 1 : 0);
+    a.start = next;
+    a.count = count;
+    a.nwg = (uint32_t)std::min<uint64_t>(g_resident, std::max<uint64_t>(1, (nblk + bpw - 1) / bpw));
+    a.seq = ++g_one.seq;
+    const uint32_t r = (uint32_t)(a.seq % BM_ONE_RING);
+    a.ctr = g_one.d_ctr + r;
+    a.out = g_one.d_out + r;
+    HIPTRY(bm_launch_search1(sh.stream, a));
+    HIPTRY(hipEventRecord(g_one.ev[a.seq % kOneEvents], sh.stream));
+    fly[nfly++] = a.seq;
+    if (room < step) top = true;
+    else next += count;
+    return 0;
+  };
+  rc = launch();
+  if (rc == 0 && !top) rc = launch();  // the next window, queued behind
+  while (rc == 0) {
+    const uint64_t seq = fly[0];
+    rc = wait_one(seq);
+    if (rc < 0) break;
+    const bm_one_out& o = g_one.h_out[seq % BM_ONE_RING];
+    g_stats.launches++;
+    g_stats.steps++;
+    g_stats.trials += o.trials;
+    const double ms = (double)(o.t1 - o.t0) * 1e-5;  // s_memrealtime: 100 MHz
+    g_stats.kernel_ms += ms;
+    g_stats.max_shard_kernel_ms += ms;
+    if (o.found) {  // the lowest hit: every earlier window of the call ended without one
+      *nonce_out = o.nonce;
+      *trial_out = o.trial;
+      return BMPOW_FOUND;  // a window still queued stops at its first block (the call's best)
+    }
+    for (int i = 1; i < nfly; ++i) fly[i - 1] = fly[i];
+    --nfly;
+    if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
+    if (!top) rc = launch();
+    if (nfly == 0) return BMPOW_NOT_FOUND;
+  }
+  return rc;
+}
+
+// Drop the scratch batch (device set change, shutdown).  lk: the engine's mutex.
+void drop_scratch(std::unique_lock<std::mutex>& lk) {
+  if (!g_scratch) return;
+  if (g_engine && g_engine->attached() == g_scratch) g_engine->detach(lk);
+  batch_free_dev(g_scratch);
+  delete g_scratch;
+  g_scratch = nullptr;
 }
 
 }  // namespace
@@ -1151,26 +1433,35 @@ bmsched::ServiceOps service_ops(bmpow_service* s) {
   ops.add = [s](size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* tg, uint32_t* slots,
                 std::string& err) {
     std::lock_guard<std::mutex> g(g_mu);
-    const int rc = batch_add_locked(s->b, n, ihs, tg, nullptr, slots, ih_off);
+    std::unique_lock<std::mutex> lk(g_engine->mu);
+    const int rc = batch_add_locked(lk, s->b, n, ihs, tg, nullptr, slots, ih_off);
     if (rc < 0) err = g_err;
     return rc;
   };
+  // let the steppers claim one round of launches (and keep one queued behind it) and return as soon
+  // as an object finished, so the service hands it out while the devices go on
   ops.step = [s](std::string& err) {
     std::lock_guard<std::mutex> g(g_mu);
-    const int rc = batch_step_locked(s->b, s->budget, nullptr);
-    if (rc < 0) err = g_err;
-    return rc;
+    std::unique_lock<std::mutex> lk(g_engine->mu);
+    g_engine->attach(lk, s->b);
+    bmpow_batch* b = s->b;
+    const uint64_t budget = (s->budget ? s->budget : g_step_trials.load()) * g_shards.size();
+    return g_engine->run(lk, budget, true, [b] { return b->finished_head < b->finished.size() || b->pending == 0; },
+                         err);
   };
   ops.take = [s](size_t cap, uint32_t* slot, uint64_t* nonce, uint64_t* trial, uint8_t* done) {
     std::lock_guard<std::mutex> g(g_mu);
+    std::lock_guard<std::mutex> lk(g_engine->mu);
     return bmsched::take_done(*s->b, cap, slot, nonce, trial, done);
   };
   ops.reset = [s](std::string& err) {
     std::lock_guard<std::mutex> g(g_mu);
+    std::unique_lock<std::mutex> lk(g_engine->mu);
+    if (g_engine->attached() == s->b) g_engine->detach(lk);
     batch_free_dev(s->b);
     delete s->b;
     s->b = new bmpow_batch();
-    const int rc = batch_init(s->b, 0, nullptr, nullptr, nullptr);
+    const int rc = batch_init(lk, s->b, 0, nullptr, nullptr, nullptr);
     if (rc < 0) err = g_err;
     return rc;
   };
@@ -1205,10 +1496,10 @@ int bmpow_set_devices(const int* ids, int n) {
   } else {
     v.assign(ids, ids + n);
   }
-  if (g_scratch) {
-    batch_free_dev(g_scratch);
-    delete g_scratch;
-    g_scratch = nullptr;
+  if (g_engine) {
+    std::unique_lock<std::mutex> el(g_engine->mu);
+    drop_scratch(el);
+    g_engine->detach(el);
   }
   if (v.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
   int rc = select_devices(v);
@@ -1230,18 +1521,22 @@ int bmpow_get_devices(int* ids, int cap) {
 int bmpow_get_shard_rates(double* rates, int cap) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!rates && cap > 0) return set_err(BMPOW_E_ARG, "null pointer");
-  for (int i = 0; i < (int)g_shards.size() && i < cap; ++i)
-    rates[i] = i < (int)g_rates.ema.size() ? g_rates.ema[i] : 0.0;
+  if (!g_engine) return 0;
+  std::lock_guard<std::mutex> el(g_engine->mu);
+  const std::vector<double>& ema = g_engine->rates.ema;
+  for (int i = 0; i < (int)g_shards.size() && i < cap; ++i) rates[i] = i < (int)ema.size() ? ema[i] : 0.0;
   return (int)g_shards.size();
 }
 
 void bmpow_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_scratch) {
-    batch_free_dev(g_scratch);
-    delete g_scratch;
-    g_scratch = nullptr;
+  if (g_engine) {
+    std::unique_lock<std::mutex> el(g_engine->mu);
+    drop_scratch(el);
+    g_engine->detach(el);
   }
+  g_engine.reset();
+  free_one();
   for (auto& s : g_shards) free_shard(s);
   g_shards.clear();
   if (g_xb) (void)hipHostFree(g_xb);
@@ -1307,41 +1602,30 @@ int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t
 
 int bmpow_search_len(const uint8_t* ih, size_t ih_len, uint64_t target, uint64_t start, uint64_t max_trials,
                      uint64_t* nonce_out, uint64_t* trial_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if ((!ih && ih_len) || !nonce_out || !trial_out) return set_err(BMPOW_E_ARG, "null pointer");
   if (ih_len > BMPOW_MAX_IH_LEN) return set_err(BMPOW_E_ARG, "initialHash longer than BMPOW_MAX_IH_LEN");
   if (max_trials == 0) return BMPOW_NOT_FOUND;
+  if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
+  if (g_shards.size() == 1 && ih_len == 64 && g_one_enabled) return search_one(ih, target, start, max_trials, nonce_out, trial_out);
   const uint8_t zero = 0;
   const uint64_t off[2] = {0, ih_len};
-  rc = scratch_batch(1, ih ? ih : &zero, &target, &start, ih_len == 64 ? nullptr : off);
+  std::unique_lock<std::mutex> lk(g_engine->mu);
+  rc = scratch_batch(lk, 1, ih ? ih : &zero, &target, &start, ih_len == 64 ? nullptr : off);
   if (rc < 0) return rc;
   bmpow_batch* b = g_scratch;
-  uint64_t left = max_trials;
-  // Every step is a full one (2^28 trials per shard by default): the columns sweep the window as one
-  // front and stop one block row after the hit (bmpow_layout.h), so an easy object costs a row, not
-  // a drained grid -- no ramp of small first steps, no step tail.  Windows over several shards are
-  // capped near the expected trials by plan_step (expect_cap).
-  const uint64_t step = g_step_trials.load() * g_shards.size();
-  while (left > 0) {
-    // This step's window for the single object is `want` nonces rounded up to whole chunks;
-    // a hit in the round-up tail lies beyond the caller's budget and is reported as
-    // NOT_FOUND (the caller resumes at start + max_trials and finds it again: exactness
-    // only needs every nonce below a reported hit to have been hashed).
-    const uint64_t want = std::min(left, step);
-    const uint64_t chunks = (want + BM_CHUNK - 1) / BM_CHUNK;
-    const uint64_t st = b->next[0];
-    rc = batch_step_locked(b, chunks * BM_CHUNK, nullptr);
-    if (rc < 0) return rc;
-    if (b->done[0] == BMPOW_DONE_FOUND) {
-      if (b->nonce[0] - st >= want) return BMPOW_NOT_FOUND;
-      *nonce_out = b->nonce[0];
-      *trial_out = b->trial[0];
-      return BMPOW_FOUND;
-    }
-    if (b->done[0] == BMPOW_DONE_EXHAUSTED) return BMPOW_NOT_FOUND;
-    left -= std::min(left, b->next[0] - st);
+  // the search's last nonce: windows are cut there, so a hit past the caller's budget is never
+  // reported (it resumes at start + max_trials and finds it again)
+  b->lim[0] = (max_trials - 1 > kU64Max - start) ? kU64Max : start + max_trials - 1;
+  std::string err;
+  rc = g_engine->run(lk, kU64Max, false, [b] { return b->done[0] != BMPOW_PENDING; }, err);
+  if (rc < 0) return set_err(rc, err);
+  if (b->done[0] == BMPOW_DONE_FOUND) {
+    *nonce_out = b->nonce[0];
+    *trial_out = b->trial[0];
+    return BMPOW_FOUND;
   }
   return BMPOW_NOT_FOUND;
 }
@@ -1390,13 +1674,15 @@ int bmpow_min_trial_var(size_t n, const uint8_t* ihs, const uint64_t* ih_off, co
 
 int bmpow_search_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* next_start,
                        uint64_t budget, uint64_t* nonce_out, uint64_t* trial_out, uint8_t* done) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if (n == 0) return 0;
   if (!ihs || !targets || !next_start || !nonce_out || !trial_out || !done)
     return set_err(BMPOW_E_ARG, "null pointer");
-  rc = scratch_batch(n, ihs, targets, next_start);
+  if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
+  std::unique_lock<std::mutex> lk(g_engine->mu);
+  rc = scratch_batch(lk, n, ihs, targets, next_start);
   if (rc < 0) return rc;
   bmpow_batch* b = g_scratch;
   for (size_t i = 0; i < n; ++i) {
@@ -1405,29 +1691,25 @@ int bmpow_search_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, ui
       b->pending--;
     }
   }
-  uint64_t spent = 0;
   if (budget == 0) budget = g_step_trials * g_shards.size();
-  int pending = (int)b->pending;
-  while (pending > 0 && spent < budget) {
-    uint64_t t = 0;
-    pending = batch_step_locked(b, std::min<uint64_t>(budget - spent, g_step_trials.load() * g_shards.size()), &t);
-    if (pending < 0) return pending;
-    spent += std::max<uint64_t>(t, BM_CHUNK);
-  }
+  // no lookahead: every claim is applied when the call returns, so next_start is where the batch stands
+  std::string err;
+  rc = g_engine->run(lk, budget, false, [b] { return b->pending == 0; }, err);
+  if (rc < 0) return set_err(rc, err);
   for (size_t i = 0; i < n; ++i) {
     if (done[i] != BMPOW_PENDING) continue;
     done[i] = b->done[i];
-    next_start[i] = b->next[i];
+    next_start[i] = bmsched::resume_point(*b, i);
     if (b->done[i] == BMPOW_DONE_FOUND) {
       nonce_out[i] = b->nonce[i];
       trial_out[i] = b->trial[i];
     }
   }
-  return pending;
+  return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
 bmpow_batch* bmpow_batch_create(size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   if (init_locked() < 0) return nullptr;
   if (n && (!ihs || !targets)) {
     set_err(BMPOW_E_ARG, "null pointer");
@@ -1437,8 +1719,9 @@ bmpow_batch* bmpow_batch_create(size_t n, const uint8_t* ihs, const uint64_t* ta
     set_err(BMPOW_E_ARG, "too many objects");
     return nullptr;
   }
+  std::unique_lock<std::mutex> lk(g_engine->mu);
   bmpow_batch* b = new bmpow_batch();
-  if (batch_init(b, n, ihs, targets, start) < 0) {
+  if (batch_init(lk, b, n, ihs, targets, start) < 0) {
     batch_free_dev(b);
     delete b;
     return nullptr;
@@ -1446,29 +1729,44 @@ bmpow_batch* bmpow_batch_create(size_t n, const uint8_t* ihs, const uint64_t* ta
   return b;
 }
 
+// Let the steppers claim ~budget trials of the batch (and one more launch per shard, which stays
+// queued behind the running one when this returns, so consecutive calls keep every device busy).
 int bmpow_batch_step(bmpow_batch* b, uint64_t budget) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
-  return batch_step_locked(b, budget, nullptr);
+  if (!g_engine) return set_err(BMPOW_E_STATE, "library not initialised");
+  if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
+  if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
+  std::unique_lock<std::mutex> lk(g_engine->mu);
+  g_engine->attach(lk, b);
+  if (budget == 0) budget = g_step_trials.load() * g_shards.size();
+  std::string err;
+  const int rc = g_engine->run(lk, budget, true, [b] { return b->pending == 0; }, err);
+  if (rc < 0) return set_err(rc, err);
+  return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
 int bmpow_batch_results(const bmpow_batch* b, uint64_t* nonce_out, uint64_t* trial_out, uint8_t* done,
                         uint64_t* next_start) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
+  std::unique_lock<std::mutex> lk;
+  if (g_engine) lk = std::unique_lock<std::mutex>(g_engine->mu);
   for (size_t i = 0; i < b->n; ++i) {
     if (nonce_out) nonce_out[i] = b->nonce[i];
     if (trial_out) trial_out[i] = b->trial[i];
     if (done) done[i] = b->done[i];
-    if (next_start) next_start[i] = b->next[i];
+    if (next_start) next_start[i] = bmsched::resume_point(*b, i);
   }
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
 int bmpow_batch_reset(bmpow_batch* b, const uint64_t* start) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
-  if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
+  if (b->dev.size() != g_shards.size() || !g_engine) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
+  std::unique_lock<std::mutex> lk(g_engine->mu);
+  quiesce(lk, b);
   bmsched::reset(*b, start);
   for (size_t s = 0; s < g_shards.size(); ++s) {
     Shard& sh = g_shards[s];
@@ -1480,54 +1778,68 @@ int bmpow_batch_reset(bmpow_batch* b, const uint64_t* start) {
     HIPTRY(hipSetDevice(sh.dev));
     HIPTRY(hipStreamSynchronize(sh.stream));
   }
+  g_engine->notify();
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
 int bmpow_batch_set_pending(bmpow_batch* b, size_t first, size_t count, int pending) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (first > b->n || count > b->n - first) return set_err(BMPOW_E_ARG, "range outside the batch");
+  std::unique_lock<std::mutex> lk;
+  if (g_engine) lk = std::unique_lock<std::mutex>(g_engine->mu);
   bmsched::set_pending(*b, first, count, pending != 0);
+  if (g_engine) g_engine->notify();
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
 int bmpow_batch_add(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
                     uint32_t* slot_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (n == 0) return (int)std::min<size_t>(b->pending, 0x7fffffff);
   if (!ihs || !targets) return set_err(BMPOW_E_ARG, "null pointer");
-  const int rc = batch_add_locked(b, n, ihs, targets, start, slot_out);
+  if (!g_engine) return set_err(BMPOW_E_STATE, "library not initialised");
+  std::unique_lock<std::mutex> lk(g_engine->mu);
+  const int rc = batch_add_locked(lk, b, n, ihs, targets, start, slot_out);
   if (rc < 0) return rc;
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
 int bmpow_batch_add_var(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* targets,
                         const uint64_t* start, uint32_t* slot_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (n == 0) return (int)std::min<size_t>(b->pending, 0x7fffffff);
   if (!targets) return set_err(BMPOW_E_ARG, "null pointer");
+  if (!g_engine) return set_err(BMPOW_E_STATE, "library not initialised");
   int rc = check_ih_offsets(n, ihs, ih_off);
   if (rc < 0) return rc;
   const uint8_t zero = 0;
-  rc = batch_add_locked(b, n, ihs ? ihs : &zero, targets, start, slot_out, ih_off);
+  std::unique_lock<std::mutex> lk(g_engine->mu);
+  rc = batch_add_locked(lk, b, n, ihs ? ihs : &zero, targets, start, slot_out, ih_off);
   if (rc < 0) return rc;
   return (int)std::min<size_t>(b->pending, 0x7fffffff);
 }
 
 int bmpow_batch_take_done(bmpow_batch* b, size_t cap, uint32_t* slot_out, uint64_t* nonce_out, uint64_t* trial_out,
                           uint8_t* done_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (cap && !slot_out) return set_err(BMPOW_E_ARG, "null pointer");
+  std::unique_lock<std::mutex> lk;
+  if (g_engine) lk = std::unique_lock<std::mutex>(g_engine->mu);
   const size_t k = bmsched::take_done(*b, std::min<size_t>(cap, 0x7fffffff), slot_out, nonce_out, trial_out, done_out);
   return (int)k;
 }
 
 void bmpow_batch_destroy(bmpow_batch* b) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<std::mutex> g(g_mu);
   if (!b) return;
+  if (g_engine) {
+    std::unique_lock<std::mutex> lk(g_engine->mu);
+    if (g_engine->attached() == b) g_engine->detach(lk);
+  }
   batch_free_dev(b);
   delete b;
 }
@@ -1535,9 +1847,15 @@ void bmpow_batch_destroy(bmpow_batch* b) {
 bmpow_service* bmpow_service_create(uint64_t step_budget, uint32_t flags) {
   bmpow_service* s = new bmpow_service();
   {
-    std::lock_guard<std::mutex> lk(g_mu);
+    std::lock_guard<std::mutex> g(g_mu);
     s->b = new bmpow_batch();
-    if (init_locked() < 0 || batch_init(s->b, 0, nullptr, nullptr, nullptr) < 0) {
+    if (init_locked() < 0) {
+      delete s->b;
+      delete s;
+      return nullptr;
+    }
+    std::unique_lock<std::mutex> lk(g_engine->mu);
+    if (batch_init(lk, s->b, 0, nullptr, nullptr, nullptr) < 0) {
       batch_free_dev(s->b);
       delete s->b;
       delete s;
@@ -1596,8 +1914,12 @@ void bmpow_service_stop(bmpow_service* s) {
 
 void bmpow_service_destroy(bmpow_service* s) {
   if (!s) return;
-  s->svc.reset();  // joins the stepper thread after its current step
-  std::lock_guard<std::mutex> lk(g_mu);
+  s->svc.reset();  // joins the service thread after its current op
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_engine) {
+    std::unique_lock<std::mutex> lk(g_engine->mu);
+    if (g_engine->attached() == s->b) g_engine->detach(lk);
+  }
   batch_free_dev(s->b);
   delete s->b;
   delete s;
@@ -1843,13 +2165,31 @@ int bmpow_get_stats(bmpow_stats* out) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!out) return BMPOW_E_ARG;
   *out = g_stats;
+  if (g_engine) {  // the searches: the engine's launches
+    std::lock_guard<std::mutex> el(g_engine->mu);
+    const bmsched::EngineStats& es = g_engine->stats;
+    out->launches += es.launches;
+    out->trials += es.trials;
+    out->kernel_ms += es.kernel_ms;
+    out->steps += es.launches;
+    double mx = 0;
+    for (double ms : es.shard_ms) mx = std::max(mx, ms);
+    out->max_shard_kernel_ms += mx;
+  }
   return 0;
 }
 
 void bmpow_reset_stats(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_stats = bmpow_stats{};
-  for (auto& s : g_shards) s.kernel_ms = 0;
+  if (g_engine) {
+    std::lock_guard<std::mutex> el(g_engine->mu);
+    bmsched::EngineStats& es = g_engine->stats;
+    const size_t S = es.shard_ms.size();
+    es = bmsched::EngineStats();
+    es.shard_ms.assign(S, 0.0);
+    es.shard_trials.assign(S, 0);
+  }
 }
 
 uint64_t bmpow_get_step_trials(void) { return g_step_trials.load(); }
@@ -1857,6 +2197,10 @@ uint64_t bmpow_get_step_trials(void) { return g_step_trials.load(); }
 void bmpow_set_step_trials(uint64_t t) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_step_trials.store(t ? std::max<uint64_t>(t, BM_CHUNK) : kDefaultStepTrials);
+  if (g_engine) {
+    std::lock_guard<std::mutex> el(g_engine->mu);
+    g_engine->set_step_trials(g_step_trials.load());
+  }
 }
 
 unsigned long long BitmessagePOW(unsigned char* starthash, unsigned long long target) {

@@ -40,7 +40,8 @@ __device__ __forceinline__ void bm_publish(unsigned long long* bestp, unsigned l
 // published into the device's own running minimum (atomicMin on best[obj]), which every column already
 // reads once per block from L2.  A value it folds in is a real hit of the window: the columns above it
 // stop, and the found[] flag stays the device's own, so the step's results are unchanged.  Exit: every
-// column has finished (cols_done, counted by each column workgroup as it ends), or 2^24 polls.
+// column wave has finished (cols_done, counted by each wave of the column workgroups as it ends), or
+// 2^24 polls.
 __device__ __forceinline__ void bm_relay(const bm_item* __restrict__ items, uint32_t nitems,
                                          unsigned long long* __restrict__ best, unsigned long long* xb,
                                          uint32_t xrow, unsigned long long* cols_done, uint32_t ncols) {
@@ -86,21 +87,26 @@ __device__ __forceinline__ uint64_t bm_block_of(const bm_item& it, uint64_t k) {
 hipError_t bm_launch_search(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                             unsigned long long* best, uint32_t* found, unsigned long long* trials_done,
                             unsigned long long* queue, const bm_xbound& xb);
-// trials_done points at two counters: [0] trials hashed, [1] column workgroups finished (the relay's
+// trials_done points at two counters: [0] trials hashed, [1] column waves finished (the relay's
 // exit; both zeroed before each launch).  With xb.table set, the grid is nwg + 1 workgroups (the relay).
 // workgroups of bm_search_kernel resident per CU (its occupancy): the columns a shard's window
 // gets at most, so a sweep is on the chip at once
 int bm_search_resident_per_cu();
+// the single-object kernel of run() (bm_one_args, bmpow_layout.h): grid a.nwg
+hipError_t bm_launch_search1(hipStream_t st, const bm_one_args& a);
 hipError_t bm_launch_search_var(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items,
                                 uint32_t nitems, unsigned long long* best, uint32_t* found,
                                 unsigned long long* trials_done, unsigned long long* queue, const bm_xbound& xb,
                                 const uint64_t* vpool);
 // vpool: the batch's var pool (may be null when no object of the launch is var-form)
-// Writes each item's result and puts its object's best/found back to (UINT64_MAX, 0); res[nitems].nonce
-// = trials[0] (the step's trial count, so one copy brings both home).
+// Writes each item's result (best/found are left as they are: they persist across the launches of a
+// stream); res[nitems].nonce = trials[0] (the step's trial count, so one copy brings both home).
 hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                              unsigned long long* best, uint32_t* found, bm_result* res,
                              const uint64_t* vpool, const unsigned long long* trials);
+// objs[slots[i]] = recs[i], best = UINT64_MAX, found = 0 (recs, slots: pinned host memory)
+hipError_t bm_launch_slots_init(hipStream_t st, bm_obj* objs, unsigned long long* best, uint32_t* found,
+                                const bm_obj* recs, const uint32_t* slots, uint32_t n);
 hipError_t bm_launch_mintrial(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items, uint32_t nitems,
                               bm_minpart* parts);
 hipError_t bm_launch_mintrial_var(hipStream_t st, uint32_t nwg, const bm_obj* objs, const bm_item* items,

@@ -46,46 +46,37 @@ using namespace bm;
 #ifndef BM_SEARCH_WAVES
 #define BM_SEARCH_WAVES 4
 #endif
-// One workgroup of a launch: it takes blocks of its item from the item's queue (bm_block_of), in
-// order, until the window ends or the next block lies above the running minimum.
-// kX: the launch holds windows split over shards, whose hits are published to the cross-shard bound.
+// One workgroup's sweep of a work item: it takes the item's blocks from the item's queue (bm_block_of),
+// in order, until the window ends or the next block lies above the running minimum.
+// kX: the launch holds items with a cross-shard bound slot, whose hits are published there.
+// log (the single-object kernel): each hit's trial value is logged, so the result needs no re-hash.
+// Returns the trials this wave hashed (its own lanes: every wave counts itself, whichever of the
+// workgroup's waves leaves first).
 template <bool kX>
-__device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
-                                              uint32_t nitems, unsigned long long* __restrict__ best,
-                                              uint32_t* __restrict__ found, unsigned long long* __restrict__ trials_done,
-                                              unsigned long long* __restrict__ queue, unsigned long long* __restrict__ xb,
-                                              uint32_t xrows, uint32_t b) {
-  // largest item index with chunk_base <= b (items sorted by chunk_base, uniform search)
-  uint32_t lo = 0, hi = nitems;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (items[mid].chunk_base <= b) lo = mid; else hi = mid;
-  }
-  const bm_item it = items[lo];
+__device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const uint64_t* __restrict__ wsrc,
+                                          uint64_t target, unsigned long long* __restrict__ bestp,
+                                          uint32_t* __restrict__ foundp, unsigned long long* __restrict__ queue,
+                                          unsigned long long* __restrict__ xb, uint32_t xrows,
+                                          bm_one_call* __restrict__ log) {
   const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;  // blocks of the window
   // the queue hands out units of BM_GRAB blocks (1 by default; larger is an A/B knob)
   const uint64_t nunit = (nblk + BM_GRAB - 1) / BM_GRAB;
-  unsigned long long* bestp = best + it.obj;
-  unsigned long long* qp = queue + lo;
+  unsigned long long* qp = queue + qi;
   __shared__ unsigned long long s_k[2];  // the unit taken, alternating slots (one barrier per unit)
   if (threadIdx.x == 0) s_k[0] = atomicAdd(qp, 1ull);
   __syncthreads();
   uint64_t unit = bm_block_of(it, s_k[0]);
-  if (unit >= nunit) return;
+  if (unit >= nunit) return 0;
   if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it.start + unit * (BM_GRAB * BM_BLOCK))
-    return;
+    return 0;
 
 #ifdef BM_PRIO_MOD
-  if (b % BM_PRIO_MOD == 0) __builtin_amdgcn_s_setprio(2);  // A/B knob: a share of the waves issue first
+  if (blockIdx.x % BM_PRIO_MOD == 0) __builtin_amdgcn_s_setprio(2);  // A/B knob: a share of the waves issue first
 #endif
-#ifdef BM_STAGGER
-  for (uint32_t z = 0; z < (b & 3); ++z) __builtin_amdgcn_s_sleep(BM_STAGGER);  // A/B knob: de-phase the waves sharing a SIMD
-#endif
-  const bm_obj* o = objs + it.obj;
   uint64_t ihw[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    ihw[i] = o->w[i];
+    ihw[i] = wsrc[i];
     // The per-object words, and the terms hoisted from them, live in VGPRs: left in SGPRs they
     // overflow the SGPR budget and every trial pays v_readlane reloads of the spilled ones (32 per
     // trial -> 18).  Same-box A/B, C3: 6.345 vs 6.302 GH/s (profiles/r02/search_kernel_ab*.txt).
@@ -93,7 +84,6 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
     asm volatile("" : "+v"(ihw[i]));
 #endif
   }
-  const uint64_t target = o->target;
 
   uint32_t done = 0;
   for (uint32_t slot = 1;; slot ^= 1) {
@@ -114,31 +104,36 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
       const uint64_t first = it.start + off;
       const uint64_t nonce = first + threadIdx.x;
       const uint64_t tv = trial_of(ihw, nonce);
-#ifndef BM_LANE_ATOMICS
+      const bool live = off + threadIdx.x < it.count;
       // Wavefront min-reduction of the hits: a wave's 64 nonces are consecutive, so its smallest hit
       // is its lowest hitting lane -- one atomicMin per wave instead of one per hitting lane.  Same
       // box (profiles/r03/waves_queue_ab/wave_min_ab.txt): C3 6.713-6.718 against 6.709-6.718 GH/s
-      // with lane atomics (BM_LANE_ATOMICS), C2 6.674-6.681 against 6.678, and the hit-heavy C5
-      // flood at test-mode difficulty 5.816-5.837 against 5.761-5.835.
-      const uint64_t hits = __builtin_amdgcn_ballot_w64(off + threadIdx.x < it.count && tv <= target);
+      // with lane atomics, C2 6.674-6.681 against 6.678, and the hit-heavy C5 flood at test-mode
+      // difficulty 5.816-5.837 against 5.761-5.835.
+      const uint64_t hits = __builtin_amdgcn_ballot_w64(live && tv <= target);
       if (hits) {
-        const uint64_t wmin = first + (threadIdx.x & ~63u) + (uint64_t)__builtin_ctzll(hits);
+        const uint32_t lane = (uint32_t)__builtin_ctzll(hits);
+        const uint64_t wmin = first + (threadIdx.x & ~63u) + lane;
+        uint64_t wtv = 0;
+        if (log)  // the hit lane's trial value, for the single-object result
+          wtv = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(tv >> 32), (int)lane) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)tv, (int)lane);
         if ((threadIdx.x & 63) == 0) {
           const unsigned long long prev = atomicMin(bestp, (unsigned long long)wmin);
-          __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(foundp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (log) {
+            const uint32_t k = atomicAdd(&log->nhits, 1u);
+            if (k < BM_ONE_LOG) {
+              log->hit_trial[k] = wtv;
+              __hip_atomic_store(&log->hit_nonce[k], (unsigned long long)wmin, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            }
+          }
           if (kX && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < wmin ? prev : wmin);
         }
       }
-#else
-      if (off + threadIdx.x < it.count && tv <= target) {
-        const unsigned long long prev = atomicMin(bestp, (unsigned long long)nonce);
-        __hip_atomic_store(found + it.obj, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (kX && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < nonce ? prev : nonce);
-      }
-#endif
-      done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
+      done += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(live));
     }
-    // Early exit: the running minimum (for a split window also the other shards' hits, folded in by
+    // Early exit: the running minimum (for a shared object also the other shards' hits, folded in by
     // the launch's relay) is tested against the next unit.  It is read after the hash, so a hit
     // published while this unit was hashed stops the workgroup now rather than one unit later; the
     // load's latency overlaps the wait at the barrier below.  Same box (profiles/r03/fresh_bound_ab.txt):
@@ -150,9 +145,11 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
     // block, so the lanes it leaves unhashed lie above an answer; the one that goes on finds its
     // slots no longer refreshed by thread 0 and re-hashes blocks it already hashed (their hits are
     // real ones) until its own read shows the hit -- within two blocks, since the last slot written
-    // holds the block the other wave stopped at.  Sharing thread 0's read through LDS instead keeps
-    // the waves in step but exposes the load's latency before the barrier: 4.7 % slower (C3 6.39
-    // against 6.70 GH/s, same box, profiles/r03/steal_ab/lds_bound_ab.txt).
+    // holds the block the other wave stopped at.  The barrier below then waits only for the waves
+    // still running: a wave that has ended no longer counts at s_barrier (the hardware drops ended
+    // waves from the workgroup's barrier).  Sharing thread 0's read through LDS instead keeps the
+    // waves in step but exposes the load's latency before the barrier: 4.7 % slower (C3 6.39 against
+    // 6.70 GH/s, same box, profiles/r03/steal_ab/lds_bound_ab.txt).
     const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0) s_k[slot] = kn;
     __syncthreads();
@@ -162,12 +159,32 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
     if (nu >= nunit || seen < it.start + nu * (BM_GRAB * BM_BLOCK)) break;
     unit = nu;
   }
-  if (threadIdx.x == 0) atomicAdd(trials_done, (unsigned long long)done);
+  return done;
 }
 
-// kX = false: every launch without split windows (one shard; as many objects as shards) -- the hot
-// loop carries nothing of the cross-shard bound.  kX = true: workgroup 0 is the relay (bm_relay),
-// columns are workgroups 1.., and each column counts itself in trials_done[1] as it ends.
+// One workgroup of a batch launch: the item holding workgroup b (the largest item index with
+// chunk_base <= b; items sorted by chunk_base, a uniform binary search), then its sweep.
+template <bool kX>
+__device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
+                                              uint32_t nitems, unsigned long long* __restrict__ best,
+                                              uint32_t* __restrict__ found, unsigned long long* __restrict__ trials_done,
+                                              unsigned long long* __restrict__ queue, unsigned long long* __restrict__ xb,
+                                              uint32_t xrows, uint32_t b) {
+  uint32_t lo = 0, hi = nitems;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (items[mid].chunk_base <= b) lo = mid; else hi = mid;
+  }
+  const bm_item it = items[lo];
+  const bm_obj* o = objs + it.obj;
+  const uint32_t done = sweep<kX>(it, lo, o->w, o->target, best + it.obj, found + it.obj, queue, xb, xrows, nullptr);
+  if ((threadIdx.x & 63) == 0 && done) atomicAdd(trials_done, (unsigned long long)done);
+}
+
+// kX = false: every launch without shared objects -- the hot loop carries nothing of the
+// cross-shard bound.  kX = true: workgroup 0 is the relay (bm_relay), columns are workgroups 1..,
+// and each of their waves counts itself in trials_done[1] as it ends (waves of one workgroup may
+// leave at different blocks, so no barrier after the sweep).
 template <bool kX>
 __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(const bm_obj* __restrict__ objs,
                                                              const bm_item* __restrict__ items,
@@ -180,14 +197,87 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
                                                              uint32_t xrow, uint32_t xrows) {
   if constexpr (kX) {
     if (blockIdx.x == 0) {
-      bm_relay(items, nitems, best, xb, xrow, trials_done + 1, gridDim.x - 1);
+      bm_relay(items, nitems, best, xb, xrow, trials_done + 1, (gridDim.x - 1) * (BM_BLOCK / 64));
       return;
     }
     search_column<true>(objs, items, nitems, best, found, trials_done, queue, xb, xrows, blockIdx.x - 1);
-    if (threadIdx.x == 0) atomicAdd(trials_done + 1, 1ull);
+    if ((threadIdx.x & 63) == 0) atomicAdd(trials_done + 1, 1ull);
   } else {
     search_column<false>(objs, items, nitems, best, found, trials_done, queue, nullptr, 0, blockIdx.x);
   }
+}
+
+// The trial value of the single-object result when the hit log overflowed (a very easy object): out
+// of line, so its registers are not the sweep's.
+__device__ __noinline__ uint64_t trial_one(uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3, uint64_t w4,
+                                           uint64_t w5, uint64_t w6, uint64_t w7, uint64_t nonce) {
+  const uint64_t ihw[8] = {w0, w1, w2, w3, w4, w5, w6, w7};
+  return trial_of(ihw, nonce);
+}
+
+// The single-object kernel of run() (bm_one_args, bmpow_layout.h): one window, the object in the
+// arguments; the launch's last wave to leave its sweep writes the result into host-mapped memory --
+// the minimum, its trial value from the hit log (re-hashed only when the log overflowed), the trials
+// hashed and the launch's start and end on the 100 MHz realtime clock -- and then its sequence
+// number, which the host polls.  (The argument's fields are read into locals: taking the address of
+// a by-value kernel argument copies it to scratch.)
+__global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search1_kernel(const bm_one_args a) {
+  bm_one_ctr* const ctr = a.ctr;
+  bm_one_call* const call = a.call;
+  uint64_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = a.w[i];
+  if (threadIdx.x == 0) {
+    if (blockIdx.x == 0) {  // the call two ahead starts from "no hit" (no launch in flight uses it)
+      bm_one_call* const r = a.reset;
+      r->best = ~0ULL;
+      r->found = 0;
+      r->nhits = 0;
+    }
+    atomicCAS(&ctr->t0, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+  bm_item it;
+  it.start = a.start;
+  it.count = a.count;
+  it.obj = 0;
+  it.chunk_base = 0;
+  it.g0 = 0;
+  it.gn = a.nwg;
+  it.nwg = a.nwg;
+  it.xslot = BM_NO_XSLOT;
+  it.pad = 0;
+  const uint32_t done = sweep<false>(it, 0, w, a.target, &call->best, &call->found, &ctr->queue, nullptr, 0, call);
+  if ((threadIdx.x & 63) != 0) return;
+  if (done) atomicAdd(&ctr->trials, (unsigned long long)done);
+  const uint32_t waves = a.nwg * (BM_BLOCK / 64);
+  if (__hip_atomic_fetch_add(&ctr->waves_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) != waves - 1) return;
+  // the last wave (lane 0): every other wave's hits and counts are visible (acq_rel above)
+  const uint64_t best = __hip_atomic_load(&call->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t found = __hip_atomic_load(&call->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nh = __hip_atomic_load(&call->nhits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t trial = 0;
+  bool have = false;
+  for (uint32_t k = 0; found && k < nh && k < BM_ONE_LOG && !have; ++k)
+    if (__hip_atomic_load(&call->hit_nonce[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == best) {
+      trial = call->hit_trial[k];
+      have = true;
+    }
+  if (found && !have) trial = trial_one(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], best);  // log overflowed
+  bm_one_out* const o = a.out;
+  const uint64_t t0 = __hip_atomic_load(&ctr->t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t tr = __hip_atomic_load(&ctr->trials, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&o->nonce, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&o->trial, trial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&o->trials, tr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&o->t0, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&o->t1, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&o->found, found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  // the launch's counters, for the launch that next uses this ring entry
+  ctr->queue = 0;
+  ctr->trials = 0;
+  ctr->t0 = 0;
+  ctr->waves_done = 0;
+  __hip_atomic_store(&o->seq, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -202,6 +292,11 @@ hipError_t bm_launch_search(hipStream_t st, uint32_t nwg, const bm_obj* objs, co
   else
     hipLaunchKernelGGL(bm_search_kernel<false>, dim3(nwg), dim3(BM_BLOCK), 0, st, objs, items, nitems, best, found,
                        trials_done, queue, nullptr, 0u, 0u);
+  return hipGetLastError();
+}
+
+hipError_t bm_launch_search1(hipStream_t st, const bm_one_args& a) {
+  hipLaunchKernelGGL(bm_search1_kernel, dim3(a.nwg), dim3(BM_BLOCK), 0, st, a);
   return hipGetLastError();
 }
 

@@ -76,6 +76,46 @@ static_assert(sizeof(bm_item) == 48, "bm_item is 48 B");
 #define BM_XSLOTS 64
 #define BM_MAX_SHARDS 64
 
+// ---- the single-object path of run() (bmpow_search_len on one shard; bm_search1_kernel) ----
+// One launch per window of the object, the object's words in the kernel arguments, the next window
+// queued behind; the launch's last wave writes its result into host-mapped memory, so a call costs
+// one kernel launch per window and no copy, event or resolve kernel.
+// Per call (a ring of BM_ONE_CALLS, slot c % BM_ONE_CALLS; every launch of call c puts slot
+// (c + 2) % BM_ONE_CALLS back to "no hit", which no launch in flight uses): the running minimum and
+// a log of the hits with their trial values (so the result needs no re-hash).
+#define BM_ONE_CALLS 4
+#define BM_ONE_LOG 32
+struct bm_one_call {
+  unsigned long long best;  // running minimum hit nonce (valid where found)
+  uint32_t found, nhits;
+  unsigned long long hit_nonce[BM_ONE_LOG], hit_trial[BM_ONE_LOG];
+};
+// Per launch (a ring of BM_ONE_RING; reset by the launch's last wave once it has used them).
+#define BM_ONE_RING 256
+struct bm_one_ctr {
+  unsigned long long queue;   // the block queue
+  unsigned long long trials;  // trials hashed (each wave adds its own)
+  unsigned long long t0;      // s_memrealtime of the first workgroup (0 = unset)
+  uint32_t waves_done, pad;   // waves that have left the sweep
+};
+// The launch's result, host-mapped; seq is written last (release), the host polls it.
+struct bm_one_out {
+  uint64_t nonce, trial, trials, t0, t1;  // t0, t1: s_memrealtime (100 MHz) at the first start, last exit
+  uint32_t found, pad;
+  uint64_t seq;
+};
+// The kernel's arguments (by value).
+struct bm_one_args {
+  uint64_t w[8];  // the initialHash as big-endian words (W1..W8 of block 1)
+  uint64_t target, start, count;
+  bm_one_call* call;   // this call's state
+  bm_one_call* reset;  // the state of the call two ahead: put back to "no hit"
+  bm_one_ctr* ctr;
+  bm_one_out* out;     // the device's address of the host-mapped result
+  uint64_t seq;
+  uint32_t nwg, pad;
+};
+
 struct bm_result {
   uint64_t nonce;  // the object's minimum hit so far (meaningful only when found)
   uint64_t trial;

@@ -7,9 +7,16 @@
 #include <emmintrin.h>
 #include <unistd.h>
 
+#include <pthread.h>
+#include <sched.h>
+#include <sys/resource.h>
+#include <sys/syscall.h>
+
 #include <algorithm>
+#include <cmath>
 #include <condition_variable>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <queue>
 #include <thread>
@@ -112,21 +119,57 @@ void pack_var(const uint8_t* ih, size_t len, uint64_t target, bm_obj* o, std::ve
 // ---------------------------------------------------------------------------------------
 // sessions
 // ---------------------------------------------------------------------------------------
+namespace {
+
+// The frontier of slot k starts over at nonce st: a new generation (launches planned for the slot
+// before are stale), no hit, no window.
+void restart_slot(BatchState& b, size_t k, uint64_t st) {
+  b.gen[k]++;
+  b.next[k] = st;
+  b.lim[k] = kU64Max;
+  b.nonce[k] = b.trial[k] = 0;
+  b.hit[k] = 0;
+  b.top[k] = 0;
+  b.holder[k] = kNoHolder;
+  b.nfly[k] = 0;
+  b.xs[k] = 0;
+  b.open[k].clear();
+}
+
+void grow_slots(BatchState& b, size_t n) {
+  b.objs.resize(n);
+  b.next.resize(n);
+  b.nonce.resize(n);
+  b.trial.resize(n);
+  b.done.resize(n, BMPOW_FREE);
+  if (b.gen.size() < n) b.gen.resize(n, 0);  // never shrinks: a slot's generations only count up
+  b.lim.resize(n, kU64Max);
+  b.hit.resize(n, 0);
+  b.top.resize(n, 0);
+  b.holder.resize(n, kNoHolder);
+  b.nfly.resize(n, 0);
+  b.xs.resize(n, 0);
+  b.open.resize(n);
+}
+
+}  // namespace
+
 void init(BatchState& b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
           const uint64_t* ih_off) {
   const uint64_t epoch = b.vpool_epoch + 1;
+  // generations carry over: launches still in flight for the previous contents stay stale
+  std::vector<uint32_t> gen;
+  gen.swap(b.gen);
   b = BatchState();
   b.vpool_epoch = epoch;
   b.n = n;
-  b.objs.resize(n);
-  b.next.resize(n);
-  b.nonce.assign(n, 0);
-  b.trial.assign(n, 0);
-  b.done.assign(n, BMPOW_PENDING);
+  b.gen.swap(gen);
+  grow_slots(b, n);
   for (size_t i = 0; i < n; ++i) {
     pack_var(ih_ptr(ihs, ih_off, i), ih_len(ih_off, i), targets[i], &b.objs[i], b.vpool);
     if (b.objs[i].ihlen != BM_IH_MAIN) b.nvar_slots++;
-    b.next[i] = start ? start[i] : 1;
+    b.done[i] = BMPOW_PENDING;
+    restart_slot(b, i, start ? start[i] : 1);
   }
   b.pending = n;
   b.cap = n;
@@ -160,19 +203,12 @@ bool add(BatchState& b, size_t m, const uint8_t* ihs, const uint64_t* targets, c
       slots[i] = (uint32_t)b.n++;
     }
   }
-  if (b.n > n0) {
-    b.objs.resize(b.n);
-    b.next.resize(b.n);
-    b.nonce.resize(b.n);
-    b.trial.resize(b.n);
-    b.done.resize(b.n, BMPOW_FREE);
-  }
+  if (b.n > n0) grow_slots(b, b.n);
   for (size_t i = 0; i < m; ++i) {
     const uint32_t k = slots[i];
     pack_var(ih_ptr(ihs, ih_off, i), ih_len(ih_off, i), targets[i], &b.objs[k], b.vpool);
     if (b.objs[k].ihlen != BM_IH_MAIN) b.nvar_slots++;
-    b.next[k] = start ? start[i] : 1;
-    b.nonce[k] = b.trial[k] = 0;
+    restart_slot(b, k, start ? start[i] : 1);
     b.done[k] = BMPOW_PENDING;
     b.pending++;
     if (k < b.first_pending) b.first_pending = k;
@@ -204,8 +240,7 @@ size_t take_done(BatchState& b, size_t cap, uint32_t* slot_out, uint64_t* nonce_
 void reset(BatchState& b, const uint64_t* start) {
   b.pending = 0;
   for (size_t i = 0; i < b.n; ++i) {
-    b.next[i] = start ? start[i] : 1;
-    b.nonce[i] = b.trial[i] = 0;
+    restart_slot(b, i, start ? start[i] : 1);
     if (b.done[i] == BMPOW_FREE) continue;  // released slots stay free
     b.done[i] = BMPOW_PENDING;
     b.pending++;
@@ -213,6 +248,11 @@ void reset(BatchState& b, const uint64_t* start) {
   b.first_pending = 0;
   b.finished.clear();
   b.finished_head = 0;
+  b.broken = false;
+}
+
+namespace {
+bool settle(BatchState& b, size_t o);
 }
 
 void set_pending(BatchState& b, size_t first, size_t count, bool pending) {
@@ -220,6 +260,7 @@ void set_pending(BatchState& b, size_t first, size_t count, bool pending) {
     if (pending && b.done[i] == BMPOW_PARKED) {
       b.done[i] = BMPOW_PENDING;
       b.pending++;
+      settle(b, i);  // its windows may have completed while it was parked
     } else if (!pending && b.done[i] == BMPOW_PENDING) {
       b.done[i] = BMPOW_PARKED;
       b.pending--;
@@ -229,56 +270,26 @@ void set_pending(BatchState& b, size_t first, size_t count, bool pending) {
 }
 
 // ---------------------------------------------------------------------------------------
-// search steps
+// work items
 // ---------------------------------------------------------------------------------------
 uint32_t g_blocks_per_worker = 0;
 
-void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident,
-           bool split, const double* weights) {
+namespace {
+
+uint64_t blocks_per_worker(uint64_t chunk) {
+  return g_blocks_per_worker ? g_blocks_per_worker
+                             : std::max<uint64_t>(1, std::min<uint64_t>(kBlocksPerWorker, chunk / BM_BLOCK));
+}
+
+}  // namespace
+
+void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident) {
   p.items.assign(S, std::vector<bm_item>());
   p.nchunks.assign(S, 0);
   p.nx = 0;
   p.C = C;
-  if (split && S > 1) {
-    // every shard sweeps every window: G columns per shard and window, at least 4 blocks per column;
-    // one resident workgroup per shard is the launch's relay of the cross-shard bound (bm_relay)
-    const uint64_t share =
-        resident ? std::max<uint64_t>(1, (resident > 1 ? resident - 1 : 1) / std::max<size_t>(wins.size(), 1)) : ~0ULL;
-    for (const Win& w : wins) {
-      const uint64_t nblk = (w.count + BM_BLOCK - 1) / BM_BLOCK;
-      const uint64_t G = std::max<uint64_t>(1, std::min<uint64_t>(share, (nblk + 4 * S - 1) / (4 * S)));
-      for (size_t s = 0; s < S; ++s) {
-        bm_item it;
-        std::memset(&it, 0, sizeof it);
-        it.start = w.start;
-        it.count = w.count;
-        it.obj = w.obj;
-        it.chunk_base = p.nchunks[s];
-        it.g0 = (uint32_t)(G * s);
-        it.gn = (uint32_t)(G * S);
-        it.nwg = (uint32_t)G;
-        it.xslot = p.nx < BM_XSLOTS ? p.nx : BM_NO_XSLOT;
-        p.items[s].push_back(it);
-        p.nchunks[s] += (uint32_t)G;
-      }
-      if (p.nx < BM_XSLOTS) ++p.nx;
-    }
-    return;
-  }
   std::vector<uint64_t> cut(S + 1);
-  if (weights) {
-    double tot = 0;
-    for (size_t s = 0; s < S; ++s) tot += weights[s];
-    double acc = 0;
-    cut[0] = 0;
-    for (size_t s = 1; s < S; ++s) {
-      acc += weights[s - 1];
-      cut[s] = std::max(cut[s - 1], std::min<uint64_t>(C, (uint64_t)((double)C * acc / tot + 0.5)));
-    }
-    cut[S] = C;
-  } else {
-    for (size_t s = 0; s <= S; ++s) cut[s] = C * s / S;
-  }
+  for (size_t s = 0; s <= S; ++s) cut[s] = C * s / S;
   size_t s = 0;
   for (const Win& w : wins) {
     uint64_t c = w.chunk0;
@@ -294,8 +305,7 @@ void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, S
       it.obj = w.obj;
       it.chunk_base = p.nchunks[s];
       const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
-      const uint64_t bpw =
-          g_blocks_per_worker ? g_blocks_per_worker : std::max<uint64_t>(1, std::min<uint64_t>(kBlocksPerWorker, chunk / BM_BLOCK));
+      const uint64_t bpw = blocks_per_worker(chunk);
       uint64_t G = std::max<uint64_t>(1, (nblk + bpw - 1) / bpw);
       if (resident) G = std::min<uint64_t>(G, resident);
       it.g0 = 0;
@@ -314,12 +324,12 @@ uint64_t expect_cap(uint64_t target, size_t S, uint64_t chunk) {
   // probability (target + 1) / 2^64)
   const double e = 18446744073709551616.0 / ((double)target + 1.0);
   const double cap = kExpectWindows * e;
-  const uint64_t floor_ = (uint64_t)S * chunk;  // every shard gets at least one chunk of the object
+  const uint64_t floor_ = (uint64_t)S * chunk;  // every piece gets at least one chunk of the object
   return cap < (double)floor_ ? floor_ : (cap >= 1.8e19 ? kU64Max : (uint64_t)cap);
 }
 
 void ShardRates::sample(size_t s, uint64_t trials, double ms) {
-  if (s >= ema.size() || trials < kRateMinTrials || !(ms > 0)) return;
+  if (s >= ema.size() || trials < min_trials || !(ms > 0)) return;
   const double r = (double)trials / ms;
   ema[s] = ema[s] > 0 ? (1 - kRateAlpha) * ema[s] + kRateAlpha * r : r;
 }
@@ -334,41 +344,6 @@ bool ShardRates::weights(std::vector<double>& w) const {
   if (ema.empty()) return false;
   mean /= (double)ema.size();
   for (size_t s = 0; s < ema.size(); ++s) w[s] = std::min(2.0, std::max(0.5, ema[s] / mean));
-  return true;
-}
-
-bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p, uint32_t resident,
-               const double* weights) {
-  while (b.first_pending < b.n && b.done[b.first_pending] != BMPOW_PENDING) ++b.first_pending;
-  if (b.pending == 0) return false;
-  if (budget == 0) budget = step_trials * S;
-  budget = std::min<uint64_t>(budget, (uint64_t)S << 36);  // grid.x stays far below 2^31
-  // workgroup size in nonces: short rounds for small steps (below ~6 full rounds of the chip
-  // per shard), full chunks otherwise
-  p.iters = budget < ((uint64_t)1 << 26) * S ? BM_ITERS_SMALL : BM_ITERS;
-  p.chunk = (uint64_t)BM_BLOCK * p.iters;
-  const uint64_t total_chunks = std::max<uint64_t>(budget / p.chunk, S);
-  // windows: pending objects in slot order, k chunks each
-  p.wins.clear();
-  const uint64_t k = std::max<uint64_t>(1, total_chunks / b.pending);
-  // fewer pending objects than shards: each window is nonce-sharded over several shards
-  const bool split = S > 1 && b.pending < S;
-  uint64_t acc = 0;
-  for (size_t i = b.first_pending; i < b.n && acc < total_chunks; ++i) {
-    if (b.done[i] != BMPOW_PENDING) continue;
-    const uint64_t st = b.next[i];
-    uint64_t want = k * p.chunk;
-#ifndef BM_NO_EXPECT_CAP  // (A/B knob: the uncapped windows of round 1)
-    if (split) want = std::min(want, expect_cap(b.objs[i].target, S, p.chunk));
-#endif
-    const uint64_t room = kU64Max - st;  // nonces remaining after st
-    if (room < want - 1) want = room + 1;   // st + want - 1 <= 2^64-1
-    const uint64_t ch = (want + p.chunk - 1) / p.chunk;
-    p.wins.push_back({(uint32_t)i, st, want, ch, acc});
-    acc += ch;
-  }
-  slice(p.wins, acc, p.chunk, S, p, resident, split, weights);
-  split_kinds(b.objs, b.nvar_slots > 0, p);
   return true;
 }
 
@@ -407,50 +382,255 @@ void split_kinds(const std::vector<bm_obj>& objs, bool any_var, StepPlan& p) {
   }
 }
 
-void apply_step(BatchState& b, const StepPlan& p, const std::vector<const bm_result*>& res) {
-  const std::vector<Win>& wins = p.wins;
-  std::vector<uint64_t> bestn(wins.size(), kU64Max), bestt(wins.size(), 0);
-  std::vector<uint8_t> hit(wins.size(), 0);  // kU64Max is a legal nonce: hits are flagged, not encoded
-  // wins are in ascending object order: obj -> win index by binary search
-  auto win_of = [&](uint32_t obj) {
-    size_t lo = 0, hi = wins.size();
-    while (hi - lo > 1) {
-      const size_t mid = (lo + hi) / 2;
-      if (wins[mid].obj <= obj) lo = mid; else hi = mid;
+// ---------------------------------------------------------------------------------------
+// per-device stepping: claims from the frontier
+// ---------------------------------------------------------------------------------------
+int XPool::alloc(uint32_t obj) {
+  for (uint32_t x = 0; x < BM_XSLOTS; ++x)
+    if (owner[x] == 0 && ref[x] == 0) {
+      owner[x] = obj + 1;
+      return (int)x;
     }
-    return lo;
-  };
-  for (size_t s = 0; s < p.items.size(); ++s) {
-    const std::vector<bm_item>& items = p.items[s];
-    for (size_t k = 0; k < items.size(); ++k) {
-      const bm_result& r = res[s][k];
-      if (!r.found) continue;
-      const size_t wi = win_of(items[k].obj);
-      if (!hit[wi] || r.nonce < bestn[wi]) {
-        hit[wi] = 1;
-        bestn[wi] = r.nonce;
-        bestt[wi] = r.trial;
+  return -1;
+}
+
+bool claimable(const BatchState& b, size_t o) {
+  if (b.done[o] != BMPOW_PENDING) return false;
+  const std::vector<OpenWin>& w = b.open[o];
+  // pieces of the latest window left to hand out, needed unless a hit lies below that window
+  if (!w.empty() && w.back().claimed < w.back().P && (!b.hit[o] || w.back().start <= b.nonce[o])) return true;
+  return !b.hit[o] && !b.top[o];
+}
+
+namespace {
+
+bool has_pieces(const BatchState& b, size_t o) {
+  const std::vector<OpenWin>& w = b.open[o];
+  return !w.empty() && w.back().claimed < w.back().P && (!b.hit[o] || w.back().start <= b.nonce[o]);
+}
+
+// An object whose search is over: FOUND once it has a hit and every open window starts above it;
+// EXHAUSTED once the frontier passed 2^64 - 1 with no hit and nothing open.
+bool settle(BatchState& b, size_t o) {
+  if (b.done[o] != BMPOW_PENDING) return false;
+  const std::vector<OpenWin>& w = b.open[o];
+  if (b.hit[o] && (w.empty() || w.front().start > b.nonce[o])) {
+    b.done[o] = BMPOW_DONE_FOUND;
+    b.next[o] = b.nonce[o] == kU64Max ? kU64Max : b.nonce[o] + 1;
+  } else if (!b.hit[o] && b.top[o] && w.empty() && b.lim[o] == kU64Max) {
+    b.done[o] = BMPOW_DONE_EXHAUSTED;
+    b.next[o] = kU64Max;
+  } else {
+    return false;
+  }
+  b.pending--;
+  mark_finished(b, (uint32_t)o);
+  return true;
+}
+
+}  // namespace
+
+uint64_t resume_point(const BatchState& b, size_t o) {
+  if (b.done[o] == BMPOW_DONE_FOUND || b.done[o] == BMPOW_DONE_EXHAUSTED) return b.next[o];
+  if (!b.open[o].empty()) return b.open[o].front().start;
+  if (b.top[o]) return b.lim[o] == kU64Max ? kU64Max : b.lim[o] + 1;
+  return b.next[o];
+}
+
+bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L) {
+  while (b.first_pending < b.n && b.done[b.first_pending] != BMPOW_PENDING) ++b.first_pending;
+  if (b.pending == 0 || b.broken) return false;
+  thread_local std::vector<uint32_t> cand, take;
+  cand.clear();
+  take.clear();
+  for (size_t i = b.first_pending; i < b.n; ++i)
+    if (claimable(b, i)) cand.push_back((uint32_t)i);
+  if (cand.empty()) return false;
+  const size_t S = std::max<size_t>(c.S, 1), C = cand.size();
+  const bool split = S > 1 && C < S;
+  if (split || S == 1) {
+    take = cand;
+  } else {
+    // fair share of the claimable objects, by the shard's rate
+    const size_t q = std::max<size_t>(1, (size_t)std::ceil((double)C * c.weight / (double)S - 1e-9));
+    auto pass = [&](auto pred) {
+      for (uint32_t o : cand)
+        if (take.size() < q && pred(o) && std::find(take.begin(), take.end(), o) == take.end()) take.push_back(o);
+    };
+    // windows with pieces left first (they hold up their objects), then the shard's own objects,
+    // then objects no shard holds, then -- only when it found nothing -- other shards' objects
+    pass([&](uint32_t o) { return has_pieces(b, o); });
+    pass([&](uint32_t o) { return b.holder[o] == (int16_t)c.s; });
+    pass([&](uint32_t o) { return b.holder[o] == kNoHolder; });
+    if (take.empty()) pass([&](uint32_t) { return true; });
+    std::sort(take.begin(), take.end());
+  }
+  const uint32_t iters = c.budget < ((uint64_t)1 << 26) ? BM_ITERS_SMALL : BM_ITERS;
+  const uint64_t chunk = (uint64_t)BM_BLOCK * iters;
+  const uint64_t budget_chunks = std::max<uint64_t>(1, c.budget / chunk);
+  const uint64_t k = std::max<uint64_t>(1, budget_chunks / take.size());
+  const uint64_t bpw = blocks_per_worker(chunk);
+  // columns of a split window's piece: the shard's resident workgroups (less the relay's) over the
+  // split objects, at least 4 blocks per column
+  const uint64_t share =
+      c.resident ? std::max<uint64_t>(1, (c.resident > 1 ? c.resident - 1 : 1) / take.size()) : ~0ULL;
+  L.claims.clear();
+  L.xslots.clear();
+  L.planned = 0;
+  L.batch = &b;
+  L.plan.items.assign(1, std::vector<bm_item>());
+  L.plan.nchunks.assign(1, 0);
+  L.plan.nx = 0;
+  L.plan.iters = iters;
+  L.plan.chunk = chunk;
+  std::vector<bm_item>& items = L.plan.items[0];
+  uint64_t acc = 0;
+  for (uint32_t o : take) {
+    std::vector<OpenWin>& ow = b.open[o];
+    Claim cl;
+    cl.obj = o;
+    cl.gen = b.gen[o];
+    if (has_pieces(b, o)) {
+      OpenWin& w = ow.back();
+      cl.start = w.start;
+      cl.count = w.count;
+      cl.G = w.G;
+      cl.P = w.P;
+      cl.piece = w.claimed++;
+    } else {
+      const uint64_t st = b.next[o], lim = b.lim[o];
+      const uint16_t P = split ? (uint16_t)S : 1;
+      uint64_t want = k * chunk;
+      if (split) {
+        const uint64_t cap = expect_cap(b.objs[o].target, S, chunk);
+        want = std::min<uint64_t>(cap, (k * chunk > kU64Max / S) ? kU64Max : k * chunk * S);
+      }
+      const uint64_t room = lim - st;  // nonces after st up to lim
+      if (want - 1 >= room) {
+        want = room + 1;  // the window ends at lim (room + 1 wraps to 0 only for [0, 2^64): clamp)
+        if (want == 0) want = kU64Max;
+        b.top[o] = 1;
+        b.next[o] = lim;
+      } else {
+        b.next[o] = st + want;
+      }
+      const uint64_t nblk = want / BM_BLOCK + (want % BM_BLOCK ? 1 : 0);
+      uint64_t G;
+      if (P == 1) {
+        G = std::max<uint64_t>(1, (nblk + bpw - 1) / bpw);
+        if (c.resident) G = std::min<uint64_t>(G, c.resident);
+      } else {
+        G = std::max<uint64_t>(1, std::min<uint64_t>(share, (nblk + 4 * P - 1) / (4 * P)));
+      }
+      ow.push_back(OpenWin{st, want, (uint32_t)G, P, 1, 0});
+      cl.start = st;
+      cl.count = want;
+      cl.G = (uint32_t)G;
+      cl.P = P;
+      cl.piece = 0;
+    }
+    // holder and the cross-shard bound
+    if (b.nfly[o] == 0) b.holder[o] = (int16_t)c.s;
+    else if (b.holder[o] != (int16_t)c.s) b.holder[o] = kShared;
+    b.nfly[o]++;
+    if (c.xp && !b.xs[o] && (cl.P > 1 || b.holder[o] == kShared)) {
+      const int x = c.xp->alloc(o);
+      if (x >= 0) {
+        b.xs[o] = (uint8_t)(x + 1);
+        if (c.xreset) c.xreset((uint32_t)x);
       }
     }
+    bm_item it;
+    std::memset(&it, 0, sizeof it);
+    it.start = cl.start;
+    it.count = cl.count;
+    it.obj = o;
+    it.chunk_base = (uint32_t)acc;
+    it.g0 = cl.G * cl.piece;
+    it.gn = cl.G * cl.P;
+    it.nwg = cl.G;
+    it.xslot = BM_NO_XSLOT;
+    if (b.xs[o] && c.xp) {
+      it.xslot = b.xs[o] - 1u;
+      c.xp->ref[it.xslot]++;
+      L.xslots.push_back(it.xslot);
+      L.plan.nx++;
+    }
+    it.pad = L.claims.size();
+    acc += cl.G;
+    items.push_back(it);
+    // nonces of the piece: its columns' share of the window
+    L.planned += cl.P == 1 ? cl.count : std::max<uint64_t>(1, cl.count / cl.P);
+    L.claims.push_back(cl);
   }
-  for (size_t wi = 0; wi < wins.size(); ++wi) {
-    const Win& w = wins[wi];
-    if (hit[wi]) {
-      b.done[w.obj] = BMPOW_DONE_FOUND;
-      b.nonce[w.obj] = bestn[wi];
-      b.trial[w.obj] = bestt[wi];
-      b.next[w.obj] = bestn[wi] == kU64Max ? kU64Max : bestn[wi] + 1;
-      b.pending--;
-      mark_finished(b, w.obj);
-    } else if (w.count - 1 == kU64Max - w.start) {
-      b.done[w.obj] = BMPOW_DONE_EXHAUSTED;
-      b.next[w.obj] = kU64Max;
-      b.pending--;
-      mark_finished(b, w.obj);
-    } else {
-      b.next[w.obj] = w.start + w.count;
+  L.plan.nchunks[0] = (uint32_t)acc;
+  L.plan.C = acc;
+  split_kinds(b.objs, b.nvar_slots > 0, L.plan);
+  return true;
+}
+
+namespace {
+
+// Release the launch's holds on its cross-shard bound slots: a slot whose last in-flight item is
+// gone goes back to the pool when its object no longer needs it (finished, restarted, or nothing in
+// flight).
+void release_xslots(BatchState& b, const Launch& L, XPool* xp) {
+  if (!xp) return;
+  for (uint32_t x : L.xslots) {
+    if (xp->ref[x]) xp->ref[x]--;
+    if (xp->ref[x] || !xp->owner[x]) continue;
+    const uint32_t o = xp->owner[x] - 1;
+    const bool mine = o < b.n && b.xs[o] == x + 1;
+    if (!mine || b.done[o] != BMPOW_PENDING || b.nfly[o] == 0) {
+      if (mine) b.xs[o] = 0;
+      xp->owner[x] = 0;
     }
   }
+}
+
+// The item's piece is no longer in flight.
+const Claim* unfly(BatchState& b, const Launch& L, const bm_item& it) {
+  const Claim& cl = L.claims[it.pad];
+  const uint32_t o = cl.obj;
+  if (o >= b.n || b.gen[o] != cl.gen) return nullptr;  // stale: the slot restarted since the plan
+  if (b.nfly[o]) b.nfly[o]--;
+  if (b.nfly[o] == 0) b.holder[o] = kNoHolder;
+  return &cl;
+}
+
+}  // namespace
+
+size_t apply_launch(BatchState& b, const Launch& L, XPool* xp, const std::function<void(uint32_t, uint64_t)>& publish) {
+  const std::vector<bm_item>& items = L.plan.items[0];
+  thread_local std::vector<uint32_t> touched;
+  touched.clear();
+  for (size_t k = 0; k < items.size(); ++k) {
+    const Claim* cl = unfly(b, L, items[k]);
+    if (!cl) continue;
+    const uint32_t o = cl->obj;
+    std::vector<OpenWin>& ow = b.open[o];
+    auto w = std::lower_bound(ow.begin(), ow.end(), cl->start,
+                              [](const OpenWin& x, uint64_t st) { return x.start < st; });
+    if (w != ow.end() && w->start == cl->start && ++w->done == w->P) ow.erase(w);
+    const bm_result& r = L.res[k];
+    if (r.found && (!b.hit[o] || r.nonce < b.nonce[o])) {
+      b.hit[o] = 1;
+      b.nonce[o] = r.nonce;
+      b.trial[o] = r.trial;
+      if (b.xs[o] && publish) publish(b.xs[o] - 1u, r.nonce);
+    }
+    touched.push_back(o);
+  }
+  size_t fin = 0;
+  for (uint32_t o : touched) fin += settle(b, o) ? 1 : 0;
+  release_xslots(b, L, xp);
+  return fin;
+}
+
+void drop_launch(BatchState& b, const Launch& L, XPool* xp) {
+  for (const bm_item& it : L.plan.items[0]) unfly(b, L, it);
+  release_xslots(b, L, xp);
+  b.broken = true;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -989,6 +1169,199 @@ void Service::loop() {
     tg.clear();
     tk.clear();
   }
+}
+
+// ---------------------------------------------------------------------------------------
+// Engine: one stepper thread per shard
+// ---------------------------------------------------------------------------------------
+Engine::Engine(EngineOps ops, size_t S, uint32_t resident, uint64_t step_trials)
+    : ops_(std::move(ops)), S_(S), resident_(resident), step_(step_trials), sh_(S) {
+  rates.reset(S);
+  stats.shard_ms.assign(S, 0.0);
+  stats.shard_trials.assign(S, 0);
+  for (size_t s = 0; s < S; ++s) {
+    sh_[s].buf[0].buf = 0;
+    sh_[s].buf[1].buf = 1;
+    sh_[s].buf[0].shard = sh_[s].buf[1].shard = s;
+  }
+  for (size_t s = 0; s < S; ++s) th_.emplace_back(&Engine::stepper, this, s);
+}
+
+Engine::~Engine() {
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    stop_ = true;
+    limit_ = claimed_;
+  }
+  cv_.notify_all();
+  for (auto& t : th_) t.join();
+}
+
+void Engine::set_throttle(size_t s, double ms) {
+  std::lock_guard<std::mutex> lk(mu);
+  if (s < S_) sh_[s].throttle_ms = ms;
+}
+
+bool Engine::can_plan() const {
+  return b_ && !b_->broken && !error_ && !stop_ && claimed_ < limit_ && !(ops_.aborted && ops_.aborted());
+}
+
+void Engine::stepper(size_t s) {
+  if (ops_.thread_init) ops_.thread_init(s);
+  std::unique_lock<std::mutex> lk(mu);
+  EShard& e = sh_[s];
+  for (;;) {
+    // 1. while fewer than two launches are in flight, plan the next one (it queues behind the
+    //    running one on the shard's stream)
+    if (e.q.size() < 2 && can_plan()) {
+      Launch& L = e.buf[e.next];
+      PlanCtx c;
+      c.s = s;
+      c.S = S_;
+      c.budget = std::min<uint64_t>(step_, limit_ - claimed_);
+      c.resident = resident_;
+      std::vector<double> w;
+      if (S_ > 1 && rates.weights(w)) c.weight = w[s];
+      c.xp = &xp_;
+      c.xreset = [this](uint32_t x) {
+        if (ops_.xstore) ops_.xstore(x, kU64Max);
+      };
+      if (plan_launch(*b_, c, L)) {
+        e.next ^= 1;
+        claimed_ += L.planned;
+        stats.planned += L.planned;
+        ++inflight_;
+        e.q.push_back(&L);
+        const double thr = e.throttle_ms;
+        lk.unlock();
+        if (thr > 0) std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(thr * 1000)));
+        std::string err;
+        L.t_launch = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+        const int rc = ops_.launch(L, err);
+        lk.lock();
+        if (rc < 0) {
+          e.q.pop_back();
+          e.next ^= 1;  // its buffer is free again
+          --inflight_;
+          applied_ += L.planned;
+          drop_launch(*L.batch, L, &xp_);
+          if (!error_) {
+            error_ = rc;
+            err_ = err;
+          }
+        }
+        cv_.notify_all();
+        continue;
+      }
+    }
+    // 2. wait for the oldest launch and fold it in
+    if (!e.q.empty()) {
+      Launch& L = *e.q.front();
+      lk.unlock();
+      std::string err;
+      const int rc = ops_.wait(L, err);
+      lk.lock();
+      e.q.pop_front();
+      --inflight_;
+      applied_ += L.planned;
+      if (rc < 0) {
+        drop_launch(*L.batch, L, &xp_);
+        if (!error_) {
+          error_ = rc;
+          err_ = err;
+        }
+      } else {
+        stats.launches++;
+        stats.trials += L.trials;
+        stats.kernel_ms += L.ms;
+        stats.shard_ms[s] += L.ms;
+        stats.shard_trials[s] += L.trials;
+        rates.sample(s, L.trials, L.ms);
+        apply_launch(*L.batch, L, &xp_, [this](uint32_t x, uint64_t v) {
+          if (ops_.xstore) ops_.xstore(x, v);
+        });
+      }
+      cv_.notify_all();
+      continue;
+    }
+    if (stop_) return;
+    cv_.wait(lk);
+  }
+}
+
+void Engine::drain(std::unique_lock<std::mutex>& lk) {
+  limit_ = claimed_;
+  cv_.wait(lk, [&] { return inflight_ == 0; });
+}
+
+void Engine::attach(std::unique_lock<std::mutex>& lk, BatchState* b) {
+  if (b_ != b) {
+    drain(lk);
+    b_ = b;
+  }
+  clear_error();
+}
+
+void Engine::detach(std::unique_lock<std::mutex>& lk) {
+  drain(lk);
+  b_ = nullptr;
+}
+
+int Engine::run(std::unique_lock<std::mutex>& lk, uint64_t budget, bool lookahead, const std::function<bool()>& done,
+                std::string& err) {
+  if (!b_) {
+    err = "no batch attached";
+    return BMPOW_E_STATE;
+  }
+  if (b_->broken) {
+    err = "a launch of this batch was lost to a device error: reset it";
+    return BMPOW_E_STATE;
+  }
+  const uint64_t a0 = applied_;
+  const uint64_t extra = lookahead ? S_ * step_ : 0;
+  const bool unbounded = budget == kU64Max || a0 + budget < a0 || a0 + budget + extra < a0 + budget;
+  limit_ = unbounded ? kU64Max : a0 + budget + extra;
+  cv_.notify_all();
+  int rc = 0;
+  for (;;) {
+    if (error_) {
+      err = err_;
+      rc = error_;
+      break;
+    }
+    if (ops_.aborted && ops_.aborted()) {
+      err = "aborted";
+      rc = BMPOW_E_ABORTED;
+      break;
+    }
+    if (done && done()) break;
+    if (!unbounded && applied_ - a0 >= budget) break;
+    if (inflight_ == 0) {
+      bool any = false;
+      if (claimed_ < limit_ && b_->pending)
+        for (size_t i = b_->first_pending; i < b_->n && !any; ++i) any = claimable(*b_, i);
+      if (!any) break;
+    }
+    cv_.wait(lk);
+  }
+  // an unbounded call (a search bounded by its objects' lim), an error or an abort leaves nothing
+  // more to claim; a bounded call keeps its lookahead launch per shard queued behind the running one
+  if (unbounded || rc < 0) limit_ = claimed_;
+  return rc;
+}
+
+int set_thread_background(const char* policy) {
+  const char* env = std::getenv("BMPOW_THREAD_POLICY");
+  const std::string p = (env && *env) ? env : (policy ? policy : "idle");
+  sched_param sp;
+  std::memset(&sp, 0, sizeof sp);
+  if (p == "idle") {
+    (void)pthread_setschedparam(pthread_self(), SCHED_IDLE, &sp);
+  } else if (p == "batch") {
+    (void)pthread_setschedparam(pthread_self(), SCHED_BATCH, &sp);
+    (void)setpriority(PRIO_PROCESS, (id_t)syscall(SYS_gettid), 19);
+  }
+  return sched_getscheduler(0);
 }
 
 }  // namespace bmsched

@@ -3,7 +3,9 @@
 // source builds with g++ for the sanitizer tests (tests/native/: ThreadSanitizer, ASan/UBSan),
 // which run it against a CPU stand-in for the kernels.
 //
-//   search steps   plan_step -> (launch per shard) -> apply_step        (bmpow_batch_step)
+//   search         Engine: one stepper thread per shard claiming windows from the objects'
+//                  frontiers (plan_launch -> launch -> wait -> apply_launch), no lockstep
+//                  (bmpow_search*, bmpow_batch_step, the service)
 //   sessions       init / add / take_done / reset / set_pending          (bmpow_batch_*)
 //   min-trial      MinTrial::plan -> (launch) -> reduce_parts -> advance (bmpow_min_trial*)
 //   verification   plan_verify, pad_range, pow_sufficient                (bmpow_verify*, bmpow_pow_values)
@@ -15,6 +17,7 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -44,12 +47,30 @@ void pack_var(const uint8_t* ih, size_t len, uint64_t target, bm_obj* o, std::ve
 inline const uint8_t* ih_ptr(const uint8_t* ihs, const uint64_t* off, size_t i) { return ihs + (off ? off[i] : 64 * i); }
 inline size_t ih_len(const uint64_t* off, size_t i) { return off ? (size_t)(off[i + 1] - off[i]) : 64; }
 
+// A window of an object's nonce space [start, start + count), handed out in P interleaved pieces:
+// piece p is columns [p G, (p + 1) G) of the window's P G columns (bmpow_layout.h: column c takes
+// blocks c, c + P G, ...).  P = 1: one shard sweeps the whole window (an object owned by one
+// device); P > 1: a window split over the shards, each piece claimed by whichever shard plans next,
+// so every device sweeps the same rows of it.  Pieces are claimed in order; the window stays open
+// until every piece has been applied.
+struct OpenWin {
+  uint64_t start, count;
+  uint32_t G;                 // columns per piece
+  uint16_t P, claimed, done;  // pieces: in all, handed out, applied
+};
+
+// Holder of an object's in-flight windows (BatchState::holder): none, one shard (its index), or
+// several shards at once.
+constexpr int16_t kNoHolder = -1, kShared = -2;
+
 // Host mirror of a device-resident batch (one slot per object; slots of finished objects are
 // released by take_done and reused by add).
 struct BatchState {
   size_t n = 0;    // slots in the table (objects, finished ones and free slots included)
   size_t cap = 0;  // device allocation, in objects (set by the device side; add() reports growth)
   std::vector<bm_obj> objs;
+  // next: the claim frontier (the first nonce no window covers yet); nonce/trial: the least hit
+  // applied so far (the answer once done = FOUND)
   std::vector<uint64_t> next, nonce, trial;
   std::vector<uint8_t> done;
   size_t first_pending = 0;
@@ -62,6 +83,16 @@ struct BatchState {
   std::vector<uint64_t> vpool;
   size_t nvar_slots = 0;  // non-free slots holding a var-form object
   uint64_t vpool_epoch = 0;
+  // ---- the claim frontier of per-device stepping (Engine, plan_launch / apply_launch) ----
+  std::vector<uint32_t> gen;     // bumped whenever the slot's search restarts: older launches are stale
+  std::vector<uint64_t> lim;     // last nonce a window may reach (inclusive): a bounded search's end
+  std::vector<uint8_t> hit;      // an applied window reported a hit (nonce/trial hold the least)
+  std::vector<uint8_t> top;      // the frontier passed lim: no window left to create
+  std::vector<int16_t> holder;   // shard holding the object's in-flight items, kNoHolder or kShared
+  std::vector<uint32_t> nfly;    // the object's items in flight
+  std::vector<uint8_t> xs;       // cross-shard bound slot + 1 while the object is shared, 0 none
+  std::vector<std::vector<OpenWin>> open;  // windows not yet fully applied, ascending start
+  bool broken = false;           // a launch was lost to a device error: only reset() continues it
 };
 
 // ih_off: null (n x 64-byte initialHashes) or n + 1 byte offsets into ihs (any lengths)
@@ -105,66 +136,204 @@ struct StepPlan {
 // item is 64-byte and nothing moves.
 void split_kinds(const std::vector<bm_obj>& objs, bool any_var, StepPlan& p);
 
-// Deal the step's windows (C chunks, ascending chunk0) to S shards as work items (bmpow_layout.h).
-//   * default: the flattened chunk list is cut into S contiguous slices -- big windows are
-//     nonce-sharded, small ones object-sharded -- and each (window, shard) piece is one item whose
-//     workgroups take its blocks in order; a piece gets one workgroup per g_blocks_per_worker blocks,
-//     at most `resident` (0 = no cap), the workgroups its shard keeps on the chip at once;
-//   * split (fewer pending objects than shards, S > 1): every shard gets an item over each whole
-//     window, interleaved column by column (shard s runs columns [g0_s, g0_s + G) of S x G), so all
-//     devices sweep the same front, and the window's cross-shard bound slot (p.nx of them) lets a hit
-//     on one device stop the columns above it on every other.
-// chunk_base of each item is relative to its shard's launch.
-//   * weights (null = equal): the default mode's slices are cut in proportion to w[s] (ShardRates), so a
-//     slower shard gets fewer chunks; split mode keeps equal columns (every shard sweeps the same rows).
-void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident = 0,
-           bool split = false, const double* weights = nullptr);
-// Blocks of a piece per workgroup in the default mode: a piece of n blocks gets ceil(n / this)
-// workgroups, at most `resident`.  Each workgroup takes about that many blocks from the item's queue
-// before the item runs dry, so this sets how long the workgroups live, and the launch's tail with it.
-// Same box, twice each (profiles/r03/waves_queue_ab/blocks_per_worker_ab.txt): 16 blocks 6.644 /
-// 6.654 GH/s on the C5 sample and 6.656 / 6.661 on C2, against 6.633 / 6.634 and 6.648 / 6.649 at 32
-// (one workgroup per chunk) and 6.633 / 6.642, 6.648 / 6.646 at 8; 128 and 512 were 2 % and 9 %
-// slower.  g_blocks_per_worker (0 = kBlocksPerWorker, at most a chunk) is set once by the library
+// Deal windows (C chunks, ascending chunk0) to S shards as work items (bmpow_layout.h): the flattened
+// chunk list is cut into S contiguous slices and each (window, shard) piece is one item whose
+// workgroups take its blocks in order; a piece gets one workgroup per g_blocks_per_worker blocks, at
+// most `resident` (0 = no cap), the workgroups its shard keeps on the chip at once.  chunk_base of each
+// item is relative to its shard's launch.  (The min-trial probe's layout; searches use plan_launch.)
+void slice(const std::vector<Win>& wins, uint64_t C, uint64_t chunk, size_t S, StepPlan& p, uint32_t resident = 0);
+// Blocks of a piece per workgroup: a window of n blocks gets ceil(n / this) workgroups, at most
+// `resident`.  Each workgroup takes about that many blocks from the item's queue before the item
+// runs dry, so this sets how long the workgroups live, and the launch's tail with it.  Same box,
+// twice each (profiles/r03/waves_queue_ab/blocks_per_worker_ab.txt): 16 blocks 6.644 / 6.654 GH/s on
+// the C5 sample and 6.656 / 6.661 on C2, against 6.633 / 6.634 and 6.648 / 6.649 at 32 (one workgroup
+// per chunk) and 6.633 / 6.642, 6.648 / 6.646 at 8; 128 and 512 were 2 % and 9 % slower.
+// g_blocks_per_worker (0 = kBlocksPerWorker, at most a chunk) is set once by the library
 // (bmpow_host.hip, BMPOW_BLOCKS_PER_WORKER for A/B runs).
 constexpr uint64_t kBlocksPerWorker = 16;
 extern uint32_t g_blocks_per_worker;
 
-// Per-shard throughput, to weight a step's slices.  The in-process multi-device step is lockstep
-// (launch on every shard, wait for all, plan the next), so the slowest shard sets its length; a
-// shard's share of the next step is made proportional to its measured rate instead of 1/S: an
-// exponential average of trials per ms over its launches of at least kRateMinTrials trials (short
-// launches measure launch latency, not rate).  Weights are 1 until every shard has a sample and are
-// clamped to [1/2, 2] x the mean.
+// Per-shard throughput: an exponential average of trials per ms over its launches of at least
+// kRateMinTrials trials (short launches measure launch latency, not rate).  An object-sharded
+// shard's fair share of the claimable objects is proportional to its rate (plan_launch), and a
+// stepper estimates from it when its launch will end (the wait's sleep, bmpow_host.hip).  Weights are
+// 1 until every shard has a sample and are clamped to [1/2, 2] x the mean.
 constexpr uint64_t kRateMinTrials = (uint64_t)1 << 24;
 constexpr double kRateAlpha = 0.25;
 struct ShardRates {
   std::vector<double> ema;  // trials per ms; 0 = no sample yet
+  uint64_t min_trials = kRateMinTrials;  // (the CPU stand-in's launches are small)
   void reset(size_t S) { ema.assign(S, 0.0); }
   void sample(size_t s, uint64_t trials, double ms);
   // w[s] with mean 1; false (w all 1) until every shard has a sample
   bool weights(std::vector<double>& w) const;
 };
 
-// A window split over the shards is capped at kExpectWindows x E nonces (E = 2^64 / (target + 1), the
-// expected trials to a hit; at least one chunk per shard): a step then lasts about as long as the
-// object, and with the cross-shard bound the shards above a hit stop within a block row of it.  With
-// as many objects as shards or more, objects are object-sharded and a shard's own early exit stops at
-// its object's hit: no cap (it would only add steps).
+// A window split over the shards (P = S pieces) covers kExpectWindows x E nonces (E = 2^64 /
+// (target + 1), the expected trials to a hit; at least one chunk per piece): a split object then
+// takes about one round of pieces, and with the cross-shard bound the pieces above a hit stop within
+// a block row of it.  An object owned by one shard is not capped: its own early exit stops at its hit.
 constexpr double kExpectWindows = 2.0;
 uint64_t expect_cap(uint64_t target, size_t S, uint64_t chunk);
 
-// Windows for the next step over S shards with about `budget` trials (0 = step_trials x S): pending
-// objects in slot order, k chunks each (capped by expect_cap when fewer than S are pending), dealt by
-// slice (split mode when fewer than S objects are pending).  resident, weights: as slice.  Returns false (p
-// untouched) when nothing is pending.
-bool plan_step(BatchState& b, uint64_t budget, uint64_t step_trials, size_t S, StepPlan& p, uint32_t resident = 0,
-               const double* weights = nullptr);
+// ---------------------------------------------------------------------------------------
+// Per-device stepping (round 4): one stepper thread and stream per shard,
+// each claiming windows from the objects' frontiers under the engine's mutex whenever it is ready
+// to launch, with its next launch staged behind the running one.  No shard waits for another.
+//
+// Exactness (the _doSafePoW answer, src/proofofwork.py:100-111, at any number of shards):
+//   * an object's windows are created in ascending order at its frontier (next), and a launch's
+//     result for an item is its device's running minimum hit of the object: every nonce of the
+//     item's columns below that minimum was hashed (an early exit only skips nonces above a real
+//     hit: the device's own, one folded in from the cross-shard bound, or one a previous launch on
+//     the same stream left in best[]);
+//   * an object is final once it has a hit h and every open window starts above h: every window
+//     below h, and every piece of the window holding h, has been applied, whichever shard ran it;
+//   * results of launches planned for an earlier occupant of a slot (its generation) are ignored.
+// ---------------------------------------------------------------------------------------
 
-// Fold the step's per-shard results (res[s][k] for p.items[s][k]) into the state: the min over
-// shards of each object's hits is final (every lower nonce of its window was hashed); no hit moves
-// next past the window; a window ending at 2^64-1 without a hit exhausts the object.
-void apply_step(BatchState& b, const StepPlan& p, const std::vector<const bm_result*>& res);
+// One item of a launch: piece `piece` of window [start, start + count) of object obj.
+struct Claim {
+  uint32_t obj, gen;
+  uint64_t start, count;
+  uint32_t G;
+  uint16_t P, piece;
+};
+
+// One launch of one shard: planned under the engine's mutex, enqueued and waited for without it.
+struct Launch {
+  size_t shard = 0;
+  int buf = 0;                  // the shard's launch buffer (two per shard: running + staged)
+  BatchState* batch = nullptr;  // the batch it was planned from (the device side's bmpow_batch)
+  std::vector<Claim> claims;
+  StepPlan plan;                // items[0]: one per claim (bm_item.pad = its claim index), split_kinds order
+  uint64_t planned = 0;         // nonces the launch covers (the engine's budget accounting)
+  std::vector<uint32_t> xslots; // cross-shard bound slots its items carry (one count each)
+  std::vector<bm_result> res;   // filled by EngineOps::wait, per item
+  uint64_t trials = 0;          // hashed (the device counter)
+  double ms = 0;                // search kernels' time (HIP events)
+  double t_launch = 0;          // steady-clock ms at enqueue (the wait's sleep estimate)
+};
+
+// The cross-shard bound slots (BM_XSLOTS; bmpow_layout.h) of the objects that have items on more
+// than one shard: an object keeps its slot while it has items in flight or open windows, and a
+// slot is reused only once no in-flight item carries it (a stale launch still publishes there).
+struct XPool {
+  uint32_t ref[BM_XSLOTS] = {};    // in-flight items carrying the slot
+  uint32_t owner[BM_XSLOTS] = {};  // object + 1, 0 = unowned
+  int alloc(uint32_t obj);         // -1 when every slot is taken (the items then go without one)
+};
+
+// What plan_launch needs to know about the shard it plans for.
+struct PlanCtx {
+  size_t s = 0, S = 1;
+  uint64_t budget = 0;       // nonces this launch may claim (at least one chunk is claimed)
+  uint32_t resident = 0;     // columns a piece may get on this shard (0 = no cap)
+  double weight = 1.0;       // the shard's rate over the mean (ShardRates)
+  XPool* xp = nullptr;       // null: no cross-shard bound
+  std::function<void(uint32_t)> xreset;  // a slot was allocated: set it to UINT64_MAX in every row
+};
+
+// Objects a launch may take a window or a piece from.
+bool claimable(const BatchState& b, size_t o);
+
+// Plan the next launch of shard c.s from the claimable objects (slot order):
+//   * object mode (at least S claimable objects, or S == 1): the shard takes its fair share q =
+//     ceil(C x weight / S) of them -- those it already holds first, then ones no shard holds, then
+//     (only if it found none) ones other shards hold -- each a window of budget / taken nonces;
+//   * split mode (fewer claimable objects than shards): every object, one piece each of windows of
+//     P = S pieces, expect_cap nonces per window;
+//   * an object whose latest window still has pieces to hand out gets the next piece first.
+// Objects with items on several shards get a cross-shard bound slot (c.xp).  Returns false (L
+// untouched) when nothing is claimable.
+bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L);
+
+// Fold a completed launch into the state (results L.res[k] for L.plan.items[0][k]); an object that
+// becomes final is queued for take_done.  publish(xslot, nonce): a new least hit of a shared object,
+// for the other shards' relays.  Returns the objects finished by it.
+size_t apply_launch(BatchState& b, const Launch& L, XPool* xp,
+                    const std::function<void(uint32_t, uint64_t)>& publish);
+// A launch that was never enqueued (an error before its kernels): its items are no longer in flight,
+// and its windows never complete (the batch is broken).
+void drop_launch(BatchState& b, const Launch& L, XPool* xp);
+// The first nonce not known to be hashed: the lowest open window's start, else the frontier.
+uint64_t resume_point(const BatchState& b, size_t o);
+
+// The device side of the engine (bmpow_host.hip; tests/native/sched_sim.cpp runs a CPU stand-in).
+struct EngineOps {
+  std::function<int(Launch& L, std::string& err)> launch;  // stage + enqueue on shard L.shard, buffer L.buf
+  std::function<int(Launch& L, std::string& err)> wait;    // block until it completed; fill res, trials, ms
+  std::function<void(uint32_t xslot, uint64_t v)> xstore;  // store v in the slot of every shard's row
+  std::function<bool()> aborted;
+  std::function<void(size_t shard)> thread_init;           // first thing each stepper thread runs
+};
+
+struct EngineStats {
+  uint64_t launches = 0, trials = 0, planned = 0, stale_items = 0;
+  double kernel_ms = 0;
+  std::vector<double> shard_ms;      // per shard: summed kernel time
+  std::vector<uint64_t> shard_trials;
+};
+
+class Engine {
+ public:
+  Engine(EngineOps ops, size_t S, uint32_t resident, uint64_t step_trials);
+  ~Engine();  // drains and joins the steppers
+  std::mutex mu;  // the attached batch's state and everything below; never held across a device call
+  // Make b the batch the steppers work on; a different attached batch is drained first.  lk holds mu.
+  void attach(std::unique_lock<std::mutex>& lk, BatchState* b);
+  // No new claims; wait until no launch is in flight (results applied); the batch stays attached.
+  void drain(std::unique_lock<std::mutex>& lk);
+  void detach(std::unique_lock<std::mutex>& lk);  // drain, then no batch
+  BatchState* attached() const { return b_; }
+  // Let the steppers claim `budget` more nonces beyond what has been applied (kU64Max: no bound) --
+  // plus, with lookahead, one more launch per shard, which stays queued behind the running one when
+  // run returns -- and wait until `budget` nonces have been applied since the call, done() holds
+  // (checked after every applied launch), nothing is left to claim or in flight, or an error / abort.
+  // Returns 0 or < 0 (err).
+  int run(std::unique_lock<std::mutex>& lk, uint64_t budget, bool lookahead, const std::function<bool()>& done,
+          std::string& err);
+  void notify() { cv_.notify_all(); }  // after changing the attached batch's state (add, set_pending)
+  void set_step_trials(uint64_t t) { step_ = t; }
+  void set_throttle(size_t s, double ms);  // A/B knob: a shard sleeps this long before each launch
+  size_t shards() const { return S_; }
+  size_t in_flight() const { return inflight_; }
+  ShardRates rates;  // under mu
+  EngineStats stats; // under mu
+  int error() const { return error_; }
+  void clear_error() { error_ = 0; err_.clear(); }
+
+ private:
+  struct EShard {
+    std::deque<Launch*> q;  // in flight, oldest first
+    Launch buf[2];
+    int next = 0;
+    double throttle_ms = 0;
+  };
+  void stepper(size_t s);
+  bool can_plan() const;
+  EngineOps ops_;
+  const size_t S_;
+  const uint32_t resident_;
+  uint64_t step_;
+  std::vector<EShard> sh_;
+  BatchState* b_ = nullptr;
+  XPool xp_;
+  uint64_t claimed_ = 0, applied_ = 0, limit_ = 0;  // nonces (planned), monotonic
+  size_t inflight_ = 0;
+  int error_ = 0;
+  std::string err_;
+  bool stop_ = false;
+  std::condition_variable cv_;
+  std::vector<std::thread> th_;
+};
+
+// Scheduling class of the library's PoW threads (the steppers): the reference runs its PoW threads at
+// SCHED_IDLE (src/bitmsghash/bitmsghash.cpp:149) and its pool workers at nice 20
+// (src/proofofwork.py:72-87), so the PoW never takes a CPU from the application.  `policy` "idle"
+// (SCHED_IDLE, the default), "batch" (SCHED_BATCH, nice 19) or "normal"; BMPOW_THREAD_POLICY overrides
+// it.  Returns the sched_getscheduler() value in effect, or -1.
+int set_thread_background(const char* policy = nullptr);
 
 // Min-trial probe over n (object, range) pairs, in steps.
 struct MinTrial {

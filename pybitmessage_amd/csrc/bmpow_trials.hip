@@ -60,11 +60,22 @@ __global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item
   r.pad = 0;
   if (r.found) r.trial = trial_obj(objs + obj, r.nonce, vpool);
   res[k] = r;
-  // Back to the "no hit" state: an object with a hit on any shard (its own, or one the relay folded
-  // in from another shard) is finished by this step, and a pending one is unchanged -- so between
-  // steps every slot reads (UINT64_MAX, 0) and a reused slot needs no reset (bmpow_host.hip).
-  best[obj] = ~0ULL;
-  found[obj] = 0;
+  // best[] / found[] are left as they are: a launch queued behind this one on the stream (the
+  // engine's lookahead, bmsched::Engine) stops at once above the hit; a slot is put back to (UINT64_MAX,
+  // 0) when it gets a new object (bm_slots_init_kernel) or the batch is reset.
+}
+
+// Objects written into slots of a shard's table, stream-ordered behind the launches in flight
+// (bmpow_host.hip init_slots): the record, and the "no hit" state.  recs / slots: pinned host memory.
+__global__ void bm_slots_init_kernel(bm_obj* __restrict__ objs, unsigned long long* __restrict__ best,
+                                     uint32_t* __restrict__ found, const bm_obj* __restrict__ recs,
+                                     const uint32_t* __restrict__ slots, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t k = slots[i];
+  objs[k] = recs[i];
+  best[k] = ~0ULL;
+  found[k] = 0;
 }
 
 // Trial values for an arbitrary list of nonces of one object, either form (parity probe).
@@ -86,6 +97,14 @@ hipError_t bm_launch_resolve(hipStream_t st, const bm_obj* objs, const bm_item* 
   const uint32_t bs = 64;
   hipLaunchKernelGGL(bm_resolve_kernel, dim3((nitems + bs) / bs), dim3(bs), 0, st, objs, items, nitems,
                      best, found, res, vpool, trials);
+  return hipGetLastError();
+}
+
+hipError_t bm_launch_slots_init(hipStream_t st, bm_obj* objs, unsigned long long* best, uint32_t* found,
+                                const bm_obj* recs, const uint32_t* slots, uint32_t n) {
+  if (n == 0) return hipSuccess;
+  const uint32_t bs = 256;
+  hipLaunchKernelGGL(bm_slots_init_kernel, dim3((n + bs - 1) / bs), dim3(bs), 0, st, objs, best, found, recs, slots, n);
   return hipGetLastError();
 }
 

@@ -84,14 +84,15 @@ __device__ __forceinline__ void search_var_column(const bm_obj* __restrict__ obj
       }
     }
     const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    done += (it.count - off < BM_BLOCK) ? (uint32_t)(it.count - off) : BM_BLOCK;
+    done += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(off + threadIdx.x < it.count));  // this wave's
     if (threadIdx.x == 0) s_k[slot] = kn;
     __syncthreads();
     const uint64_t nxt = bm_block_of(it, s_k[slot]);
     if (nxt >= nblk || seen < it.start + nxt * BM_BLOCK) break;
     blk = nxt;
   }
-  if (threadIdx.x == 0) atomicAdd(trials_done, (unsigned long long)done);
+  // every wave counts its own lanes (waves of one workgroup may leave at different blocks)
+  if ((threadIdx.x & 63) == 0 && done) atomicAdd(trials_done, (unsigned long long)done);
 }
 
 // xb set (split windows): workgroup 0 is the relay and columns are workgroups 1.., as in
@@ -108,11 +109,11 @@ __global__ __launch_bounds__(BM_BLOCK) void bm_search_var_kernel(const bm_obj* _
                                                                  const uint64_t* __restrict__ vpool) {
   if (xb) {
     if (blockIdx.x == 0) {
-      bm_relay(items, nitems, best, xb, xrow, trials_done + 1, gridDim.x - 1);
+      bm_relay(items, nitems, best, xb, xrow, trials_done + 1, (gridDim.x - 1) * (BM_BLOCK / 64));
       return;
     }
     search_var_column(objs, items, nitems, best, found, trials_done, queue, xb, xrows, vpool, blockIdx.x - 1);
-    if (threadIdx.x == 0) atomicAdd(trials_done + 1, 1ull);
+    if ((threadIdx.x & 63) == 0) atomicAdd(trials_done + 1, 1ull);
   } else {
     search_var_column(objs, items, nitems, best, found, trials_done, queue, nullptr, 0, vpool, blockIdx.x);
   }

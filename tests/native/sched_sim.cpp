@@ -4,13 +4,15 @@
 // the code bmpow_host.hip runs between HIP calls) against a CPU stand-in for the gfx950 kernels,
 // whose trial function is the C oracle's (oracle/bmpow_oracle.c).  Built and run by
 // tests/test_native.py under ThreadSanitizer and under AddressSanitizer + UBSan, with the
-// concurrency the library has: one host thread per shard (device) per step, producer threads
-// feeding a shared session under one mutex (the library's g_mu) while a stepper thread steps it
-// and a consumer pops finished objects, and the multi-threaded payload padding of the verifier.
+// concurrency the library has: the engine's stepper thread per shard (each with a launch queued
+// behind its running one, shards of unequal speed), producer threads adding objects to a session
+// while those launches are in flight, a consumer popping finished objects, the service thread,
+// and the multi-threaded payload padding of the verifier.
 //
 // Every answer is checked against the oracle's sequential _doSafePoW search
 // (src/proofofwork.py:100-111); exit status 0 = all scenarios passed.
 #include <cmath>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 
@@ -20,6 +22,8 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstring>
+#include <deque>
+#include <memory>
 #include <mutex>
 #include <random>
 #include <thread>
@@ -102,25 +106,9 @@ static void init_k() {
   for (int i = 0; i < 80; ++i) g_k[i] = k[i];
 }
 
-// ---- CPU stand-in for one shard's device state and kernels ----
-struct SimShard {
-  std::vector<uint64_t> best;
-  std::vector<uint32_t> found;
-  std::vector<bm_result> res;
-};
-
-// bm_search_kernel + bm_resolve_kernel for one shard: per item, nonces in order up to the first hit
-// (the device's early exit gives the same per-object minimum); res[k] = the object's shard minimum.
-static uint64_t sim_trial(const bm_obj& o, const std::vector<uint64_t>& vpool, uint64_t nonce) {
-  if (o.ihlen != BM_IH_MAIN) return trial_from_pool(o, vpool, nonce);
-  uint8_t ih[64];
-  ih_of(o, ih);
-  return bmo_trial(ih, nonce);
-}
-
 // The nonces an item's workgroups hash (bmpow_layout.h): columns [g0, g0 + nwg) of gn, column c taking
-// blocks c, c + gn, ... of BM_BLOCK nonces -- visited here in ascending nonce order (row by row), so
-// the first hit is the item's minimum, whatever the device's early exit skips above it.
+// blocks c, c + gn, ... of BM_BLOCK nonces -- visited here in ascending nonce order (row by row).
+// (The min-trial probe's static columns.)
 template <typename F>
 static void for_each_block(const bm_item& it, F&& fn) {
   const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
@@ -137,99 +125,210 @@ static void for_each_block(const bm_item& it, F&& fn) {
   }
 }
 
-static void sim_step_shard(const std::vector<bm_obj>& objs, const std::vector<uint64_t>& vpool,
-                           const std::vector<bm_item>& items, SimShard& sh) {
-  if (sh.best.size() < objs.size()) {
-    sh.best.resize(objs.size(), kU64Max);
-    sh.found.resize(objs.size(), 0);
-  }
-  for (const bm_item& it : items) {
-    for_each_block(it, [&](uint64_t, uint64_t first, uint64_t cnt) {
-      for (uint64_t j = 0; j < cnt; ++j) {
-        const uint64_t n = first + j;
-        if (sim_trial(objs[it.obj], vpool, n) <= objs[it.obj].target) {
-          if (!sh.found[it.obj] || n < sh.best[it.obj]) sh.best[it.obj] = n;
-          sh.found[it.obj] = 1;
-          return false;
-        }
-      }
-      return true;
-    });
-  }
-  sh.res.resize(items.size());
-  for (size_t k = 0; k < items.size(); ++k) {
-    const uint32_t o = items[k].obj;
-    bm_result r;
-    r.nonce = sh.best[o];
-    r.found = sh.found[o];
-    r.pad = 0;
-    if (r.found) {
-      r.trial = sim_trial(objs[o], vpool, r.nonce);
-    } else {
-      r.trial = 0;
-    }
-    sh.res[k] = r;
-  }
-  // bm_resolve_kernel puts each item's object back to "no hit" after reading it
-  for (const bm_item& it : items) {
-    sh.best[it.obj] = kU64Max;
-    sh.found[it.obj] = 0;
-  }
+// bm_block_of (bmpow_kernels.h): the k-th block an item's queue hands out
+static uint64_t block_of(const bm_item& it, uint64_t k) {
+  if (it.gn == it.nwg) return k;
+  const uint64_t row = k / it.nwg;
+  return row * it.gn + it.g0 + (k - row * it.nwg);
 }
 
-// One bounded step over S shards, one host thread per shard (as one stream per device).
-static bool sim_step(BatchState& b, std::vector<SimShard>& shards, uint64_t budget, uint64_t step_trials,
-                     uint32_t resident = 24, const double* weights = nullptr) {
-  StepPlan p;
-  if (!plan_step(b, budget, step_trials, shards.size(), p, resident, weights)) return false;
-  // every window's columns [0, gn) are covered exactly once over the shards' items; a window split
-  // over the shards has one item per shard and a cross-shard bound slot of its own
-  for (size_t wi = 0; wi < p.wins.size(); ++wi) {
-    std::vector<std::pair<uint64_t, uint64_t>> cols;  // (start of the item's sub-range, column)
-    for (size_t s = 0; s < shards.size(); ++s)
-      for (const bm_item& it : p.items[s])
-        if (it.obj == p.wins[wi].obj) {
-          CHECK(it.nwg >= 1 && it.g0 + it.nwg <= it.gn && it.gn >= 1, "item columns");
-          CHECK(resident == 0 || it.nwg <= resident || it.xslot != BM_NO_XSLOT, "item above the resident cap");
-          for (uint32_t c = it.g0; c < it.g0 + it.nwg; ++c) cols.push_back({it.start, c});
-          if (it.xslot != BM_NO_XSLOT) CHECK(it.xslot < p.nx, "xslot %u of %u", it.xslot, p.nx);
-        }
-    std::sort(cols.begin(), cols.end());
-    CHECK(std::adjacent_find(cols.begin(), cols.end()) == cols.end(), "a column dealt twice (window %zu)", wi);
-  }
-  uint64_t wgs = 0, items_wg = 0;
-  for (size_t s = 0; s < shards.size(); ++s) {
-    wgs += p.nchunks[s];
-    for (const bm_item& it : p.items[s]) items_wg += it.nwg;
-  }
-  CHECK(wgs == items_wg, "launch workgroups %llu != items' %llu", (unsigned long long)wgs, (unsigned long long)items_wg);
-  for (size_t s = 0; s < shards.size(); ++s) {
-    // two launches per shard (split_kinds): 64-byte objects, then var-form ones, chunk_base from 0 in each
-    uint64_t cm = 0, cv = 0;
-    for (size_t k = 0; k < p.items[s].size(); ++k) {
-      const bm_item& it = p.items[s][k];
-      const bool main_kind = k < p.nmain[s];
-      CHECK(main_kind == (b.objs[it.obj].ihlen == BM_IH_MAIN), "item %zu of shard %zu in the wrong launch", k, s);
-      uint64_t& c = main_kind ? cm : cv;
-      CHECK(it.chunk_base == c, "chunk_base %u, want %llu", it.chunk_base, (unsigned long long)c);
-      c += it.nwg;
-    }
-    CHECK(cm == p.chmain[s] && cm + cv == p.nchunks[s], "shard %zu chunk totals", s);
-  }
-  std::vector<std::thread> th;
-  for (size_t s = 0; s < shards.size(); ++s)
-    th.emplace_back(sim_step_shard, std::cref(b.objs), std::cref(b.vpool), std::cref(p.items[s]), std::ref(shards[s]));
-  for (auto& t : th) t.join();
-  std::vector<const bm_result*> res(shards.size());
-  for (size_t s = 0; s < shards.size(); ++s) res[s] = shards[s].res.data();
-  apply_step(b, p, res);
-  // every slot's device state is (UINT64_MAX, 0) between steps (bmpow_host.hip relies on it: a reused
-  // scratch slot is not reset)
-  for (size_t s = 0; s < shards.size(); ++s)
-    for (size_t i = 0; i < b.n && i < shards[s].found.size(); ++i)
-      CHECK(!shards[s].found[i] && shards[s].best[i] == kU64Max, "object %zu keeps a hit on shard %zu", i, s);
-  return true;
+static uint64_t sim_trial(const bm_obj& o, const std::vector<uint64_t>& vpool, uint64_t nonce) {
+  if (o.ihlen != BM_IH_MAIN) return trial_from_pool(o, vpool, nonce);
+  uint8_t ih[64];
+  ih_of(o, ih);
+  return bmo_trial(ih, nonce);
 }
+
+// ---- CPU stand-in for the devices: the engine's device side (bmsched::EngineOps) ----
+// Each shard has a command queue (its stream): table uploads, slot inits and launches run in the
+// order they were enqueued, by the shard's stepper when it waits for a launch.  The device state
+// (the table copy, best[], found[]) persists across launches as on the GPU, and a launch emulates
+// bm_search_kernel's observable behaviour: an item's blocks taken in queue order, the relay folding
+// the cross-shard table into best[] before each block, the early exit at a block above best[], the
+// wave's lowest hit atomicMin'd into best[] and published to every row of an xslot.
+struct SimDev {
+  std::vector<bm_obj> objs;
+  std::vector<uint64_t> vpool;
+  std::vector<uint64_t> best;
+  std::vector<uint32_t> found;
+};
+
+struct SimCmd {
+  enum Kind { kUpload, kSlots, kVpool, kLaunch } kind;
+  std::vector<bm_obj> recs;
+  std::vector<uint32_t> slots;
+  std::vector<uint64_t> words;
+  Launch* L = nullptr;
+  std::vector<bm_item> items;
+  size_t n = 0;
+};
+
+class SimLib {
+ public:
+  SimLib(size_t S, uint32_t resident, uint64_t step, std::vector<double> slowdown = {})
+      : S_(S), dev_(S), q_(S), qmu_(S), slow_(std::move(slowdown)), xb_(new std::atomic<uint64_t>[S * BM_XSLOTS]) {
+    slow_.resize(S, 1.0);
+    for (size_t i = 0; i < S * BM_XSLOTS; ++i) xb_[i].store(kU64Max);
+    policy_.assign(S, -2);
+    EngineOps ops;
+    ops.launch = [this](Launch& L, std::string&) {
+      std::lock_guard<std::mutex> lk(qmu_[L.shard]);
+      SimCmd c;
+      c.kind = SimCmd::kLaunch;
+      c.L = &L;
+      c.items = L.plan.items[0];
+      q_[L.shard].push_back(std::move(c));
+      return 0;
+    };
+    ops.wait = [this](Launch& L, std::string& err) { return exec_until(L, err); };
+    ops.xstore = [this](uint32_t x, uint64_t v) {
+      for (size_t r = 0; r < S_; ++r) xb_[r * BM_XSLOTS + x].store(v, std::memory_order_relaxed);
+    };
+    ops.aborted = [this] { return abort_.load(); };
+    ops.thread_init = [this](size_t s) {
+      const int pol = set_thread_background("idle");
+      std::lock_guard<std::mutex> lk(pmu_);
+      policy_[s] = pol;
+    };
+    eng_.reset(new Engine(ops, S, resident, step));
+  }
+  ~SimLib() { eng_.reset(); }
+  Engine& eng() { return *eng_; }
+  std::atomic<bool> abort_{false};
+  std::vector<int> policies() {
+    std::lock_guard<std::mutex> lk(pmu_);
+    return policy_;
+  }
+  // batch_upload: the whole table, best = UINT64_MAX, found = 0 (stream-ordered)
+  void upload(const BatchState& b) {
+    for (size_t s = 0; s < S_; ++s) {
+      SimCmd c;
+      c.kind = SimCmd::kUpload;
+      c.recs = b.objs;
+      c.words = b.vpool;
+      c.n = b.n;
+      std::lock_guard<std::mutex> lk(qmu_[s]);
+      q_[s].push_back(std::move(c));
+    }
+  }
+  // init_slots (bm_slots_init_kernel) and the var pool's copy, behind what is queued
+  void init_slots(const BatchState& b, const std::vector<uint32_t>& slots) {
+    for (size_t s = 0; s < S_; ++s) {
+      SimCmd v;
+      v.kind = SimCmd::kVpool;
+      v.words = b.vpool;
+      SimCmd c;
+      c.kind = SimCmd::kSlots;
+      c.slots = slots;
+      for (uint32_t k : slots) c.recs.push_back(b.objs[k]);
+      std::lock_guard<std::mutex> lk(qmu_[s]);
+      q_[s].push_back(std::move(v));
+      q_[s].push_back(std::move(c));
+    }
+  }
+  uint64_t xb(size_t row, uint32_t x) const { return xb_[row * BM_XSLOTS + x].load(std::memory_order_relaxed); }
+
+ private:
+  int exec_until(Launch& L, std::string& err) {
+    const size_t s = L.shard;
+    for (;;) {
+      SimCmd c;
+      {
+        std::lock_guard<std::mutex> lk(qmu_[s]);
+        if (q_[s].empty()) {
+          err = "launch not in its queue";
+          return BMPOW_E_HIP;
+        }
+        c = std::move(q_[s].front());
+        q_[s].pop_front();
+      }
+      SimDev& d = dev_[s];
+      switch (c.kind) {
+        case SimCmd::kUpload:
+          d.objs = c.recs;
+          d.vpool = c.words;
+          d.best.assign(std::max(c.n, d.best.size()), kU64Max);
+          d.found.assign(d.best.size(), 0);
+          break;
+        case SimCmd::kVpool:
+          d.vpool = c.words;
+          break;
+        case SimCmd::kSlots:
+          for (size_t i = 0; i < c.slots.size(); ++i) {
+            const uint32_t k = c.slots[i];
+            if (d.objs.size() <= k) {
+              d.objs.resize(k + 1);
+              d.best.resize(k + 1, kU64Max);
+              d.found.resize(k + 1, 0);
+            }
+            d.objs[k] = c.recs[i];
+            d.best[k] = kU64Max;
+            d.found[k] = 0;
+          }
+          break;
+        case SimCmd::kLaunch: {
+          uint64_t trials = 0;
+          std::vector<bm_result> res(c.items.size());
+          const auto t0 = std::chrono::steady_clock::now();
+          for (size_t k = 0; k < c.items.size(); ++k) res[k] = run_item(s, d, c.items[k], trials);
+          const double slow = slow_[s];  // a shard `slow` times slower: it idles (slow - 1) x its hashing time
+          if (slow > 1) std::this_thread::sleep_for((std::chrono::steady_clock::now() - t0) * (slow - 1));
+          if (c.L == &L) {
+            L.res = std::move(res);
+            L.trials = trials;
+            L.ms = std::max(1e-3, (double)trials * 1e-6);
+            return 0;
+          }
+          err = "launches completed out of order";
+          return BMPOW_E_HIP;
+        }
+      }
+    }
+  }
+  bm_result run_item(size_t s, SimDev& d, const bm_item& it, uint64_t& trials) {
+    const bm_obj& o = d.objs[it.obj];
+    uint64_t& best = d.best[it.obj];
+    uint32_t& found = d.found[it.obj];
+    const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
+    for (uint64_t k = 0;; ++k) {
+      const uint64_t blk = block_of(it, k);
+      if (blk >= nblk) break;
+      if (it.xslot != BM_NO_XSLOT) {  // the relay folds the other shards' hits in
+        const uint64_t v = xb_[s * BM_XSLOTS + it.xslot].load(std::memory_order_relaxed);
+        if (v < best) best = v;
+      }
+      const uint64_t first = it.start + blk * BM_BLOCK;
+      if (best < first) break;  // early exit above the running minimum
+      const uint64_t cnt = std::min<uint64_t>(BM_BLOCK, it.count - blk * BM_BLOCK);
+      trials += cnt;
+      for (uint64_t j = 0; j < cnt; ++j) {
+        if (sim_trial(o, d.vpool, first + j) <= o.target) {
+          const uint64_t n = first + j;
+          if (n < best) best = n;
+          found = 1;
+          if (it.xslot != BM_NO_XSLOT)
+            for (size_t r = 0; r < S_; ++r) xb_[r * BM_XSLOTS + it.xslot].store(best, std::memory_order_relaxed);
+          break;  // the block's lowest hit (a wave's ctz); the next block starts above it
+        }
+      }
+    }
+    bm_result r;
+    std::memset(&r, 0, sizeof r);
+    r.nonce = best;
+    r.found = found;
+    r.trial = found ? sim_trial(o, d.vpool, best) : 0;
+    return r;
+  }
+  const size_t S_;
+  std::vector<SimDev> dev_;
+  std::vector<std::deque<SimCmd>> q_;
+  std::vector<std::mutex> qmu_;
+  std::vector<double> slow_;
+  std::unique_ptr<std::atomic<uint64_t>[]> xb_;
+  std::mutex pmu_;
+  std::vector<int> policy_;
+  std::unique_ptr<Engine> eng_;
+};
 
 struct Obj {
   uint8_t ih[64];
@@ -258,39 +357,73 @@ static void expect_exact(const Obj& o, int done, uint64_t nonce, uint64_t trial,
   }
 }
 
-// ---- scenario 1: whole batches, many shard layouts and step sizes ----
-static void scenario_batches() {
-  std::mt19937_64 rng(1);
-  struct Case { size_t n, S; uint64_t budget, max_div; };
-  const Case cases[] = {{40, 1, 0, 3000}, {300, 3, 3001, 2000}, {2500, 2, 1 << 20, 500}, {600, 8, 1 << 14, 5000},
-                        {5000, 1, 1 << 22, 200}, {17, 5, 1, 50000}};
-  for (const Case& c : cases) {
-    std::vector<Obj> objs = random_objs(rng, c.n, c.max_div);
-    std::vector<uint8_t> ihs(64 * c.n);
-    std::vector<uint64_t> tg(c.n), st(c.n);
-    for (size_t i = 0; i < c.n; ++i) {
-      memcpy(&ihs[64 * i], objs[i].ih, 64);
-      tg[i] = objs[i].target;
-      st[i] = objs[i].start;
-    }
-    BatchState b;
-    init(b, c.n, ihs.data(), tg.data(), st.data());
-    std::vector<SimShard> shards(c.S);
-    int steps = 0;
-    while (sim_step(b, shards, c.budget, 1 << 16)) ++steps;
-    CHECK(b.pending == 0, "batch n=%zu left %zu pending", c.n, b.pending);
-    for (size_t i = 0; i < c.n; ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "batch", i);
-    fprintf(stderr, "batches: n=%zu S=%zu budget=%llu: %d steps\n", c.n, c.S, (unsigned long long)c.budget, steps);
+static void pack_list(const std::vector<Obj>& objs, std::vector<uint8_t>& ihs, std::vector<uint64_t>& tg,
+                      std::vector<uint64_t>& st) {
+  ihs.resize(64 * objs.size());
+  tg.resize(objs.size());
+  st.resize(objs.size());
+  for (size_t i = 0; i < objs.size(); ++i) {
+    memcpy(&ihs[64 * i], objs[i].ih, 64);
+    tg[i] = objs[i].target;
+    st[i] = objs[i].start;
   }
 }
 
-// ---- scenario 1c: initialHashes of any length (the var form, pack_var + split_kinds) ----
+// bmpow_batch_step until nothing is pending: the steppers claim `budget` per call plus one lookahead
+// launch per shard, which stays in flight across calls.  Returns the calls made.
+static int solve(SimLib& lib, BatchState& b, uint64_t budget) {
+  int calls = 0;
+  for (;;) {
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().attach(lk, &b);
+    std::string err;
+    const int rc = lib.eng().run(lk, budget, true, [&b] { return b.pending == 0; }, err);
+    CHECK(rc == 0, "run: %d %s", rc, err.c_str());
+    ++calls;
+    if (rc < 0 || b.pending == 0) return calls;
+    CHECK(calls < 1000000, "no progress");
+    if (calls >= 1000000) return calls;
+  }
+}
+
+// ---- scenario 1: whole batches over 1..8 shards, budgets from one chunk up ----
+static void scenario_batches() {
+  std::mt19937_64 rng(1);
+  struct Case { size_t n, S; uint64_t budget, step, max_div; };
+  const Case cases[] = {{40, 1, 0, 1 << 16, 3000},      {300, 3, 3001, 1 << 14, 2000}, {2500, 2, 1 << 20, 1 << 18, 500},
+                        {600, 8, 1 << 14, 1 << 13, 5000}, {5000, 1, 1 << 22, 1 << 20, 200}, {17, 5, 1, 1 << 12, 50000},
+                        {7, 8, 1 << 16, 1 << 15, 20000}};
+  for (const Case& c : cases) {
+    std::vector<Obj> objs = random_objs(rng, c.n, c.max_div);
+    std::vector<uint8_t> ihs;
+    std::vector<uint64_t> tg, st;
+    pack_list(objs, ihs, tg, st);
+    SimLib lib(c.S, 24, c.step);
+    BatchState b;
+    init(b, c.n, ihs.data(), tg.data(), st.data());
+    lib.upload(b);
+    const int calls = solve(lib, b, c.budget ? c.budget : c.step * c.S);
+    CHECK(b.pending == 0, "batch n=%zu left %zu pending", c.n, b.pending);
+    for (size_t i = 0; i < c.n; ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "batch", i);
+    {
+      std::unique_lock<std::mutex> lk(lib.eng().mu);
+      lib.eng().detach(lk);
+      CHECK(lib.eng().in_flight() == 0, "launches in flight after detach");
+      for (size_t i = 0; i < c.n; ++i) CHECK(b.nfly[i] == 0 && b.holder[i] == kNoHolder, "object %zu still held", i);
+      CHECK(lib.eng().stats.launches > 0, "no launch counted");
+    }
+    fprintf(stderr, "batches: n=%zu S=%zu budget=%llu: %d calls, %llu launches\n", c.n, c.S,
+            (unsigned long long)c.budget, calls, (unsigned long long)lib.eng().stats.launches);
+  }
+}
+
+// ---- scenario 2: initialHashes of any length (the var form, pack_var + split_kinds) ----
 static void scenario_var() {
   std::mt19937_64 rng(21);
   // the var pool's words, consumed as bm_search_var_kernel does, give the oracle's trial at every
   // SHA-512 block edge of the first hash's message (8 + L + 17 bytes)
-  for (size_t L : std::initializer_list<size_t>{0, 1, 7, 8, 63, 65, 100, 103, 104, 111, 112, 127, 128, 200, 231, 232, 239, 240, 255, 256, 359,
-                   360, 1000, 4096}) {
+  for (size_t L : std::initializer_list<size_t>{0, 1, 7, 8, 63, 65, 100, 103, 104, 111, 112, 127, 128, 200, 231, 232,
+                                                239, 240, 255, 256, 359, 360, 1000, 4096}) {
     std::vector<uint8_t> ih(L);
     for (auto& c : ih) c = (uint8_t)rng();
     std::vector<uint64_t> pool(3, 7);  // an object not at word 0
@@ -318,11 +451,11 @@ static void scenario_var() {
       off.push_back(cat.size());
       tg[i] = kU64Max / (1 + rng() % 3000);
     }
+    SimLib lib(S, 24, 1 << 12);
     BatchState b;
     init(b, n, cat.data(), tg.data(), nullptr, off.data());
-    std::vector<SimShard> shards(S);
-    while (sim_step(b, shards, 1 << 14, 1 << 12)) {
-    }
+    lib.upload(b);
+    solve(lib, b, 1 << 14);
     for (size_t i = 0; i < n; ++i) {
       uint64_t nn = 0, t = 0;
       const int hit = bmo_search_len(ihs[i].data(), ihs[i].size(), tg[i], 1, kU64Max, &nn, &t);
@@ -330,6 +463,8 @@ static void scenario_var() {
             "var batch S=%zu object %zu (L=%zu): got %llu want %llu", S, i, ihs[i].size(),
             (unsigned long long)b.nonce[i], (unsigned long long)nn);
     }
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().detach(lk);
   }
   // a session: var objects added, taken, the pool emptied once no slot holds one (new epoch)
   BatchState b;
@@ -338,10 +473,15 @@ static void scenario_var() {
   std::vector<uint8_t> ih(100, 0x5a);
   const uint64_t off[2] = {0, 100}, t1 = kU64Max / 50;
   std::vector<uint32_t> sl;
+  SimLib lib(2, 24, 1 << 12);
   add(b, 1, ih.data(), &t1, nullptr, sl, off);
+  b.cap = b.n;
+  lib.upload(b);
   CHECK(b.nvar_slots == 1 && b.vpool.size() == bm_var_words(100), "session var add");
-  std::vector<SimShard> shards(2);
-  while (sim_step(b, shards, 1 << 13, 1 << 12)) {
+  solve(lib, b, 1 << 13);
+  {
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().detach(lk);
   }
   uint32_t slot;
   uint64_t nn, tt;
@@ -357,52 +497,276 @@ static void scenario_var() {
   fprintf(stderr, "var: pack_var at every block edge, mixed batches over 1/2/4 shards, session pool reuse\n");
 }
 
-// ---- scenario 1b: over several shards a window is capped near the expected trials to a hit ----
-static void scenario_expect_cap() {
+// ---- scenario 3: fewer objects than shards -- windows split in interleaved pieces ----
+static void scenario_split() {
   std::mt19937_64 rng(11);
-  for (uint64_t E : {1000ull, 1000000ull, 12700000ull, 1ull << 40}) {
+  // planning: one object over 8 shards, every shard plans in turn -- the first window is cut into 8
+  // pieces, each a shard's columns [p G, (p + 1) G) of the window's 8 G, expect_cap nonces long
+  {
     std::vector<Obj> objs = random_objs(rng, 1, 1);
+    const uint64_t E = 12700000;
     objs[0].target = kU64Max / E;
     BatchState b;
     init(b, 1, objs[0].ih, &objs[0].target, &objs[0].start);
-    for (size_t S : {1, 2, 8}) {
-      StepPlan p;
-      CHECK(plan_step(b, 0, 1 << 28, S, p), "plan_step");
-      const uint64_t window = p.wins[0].chunks * p.chunk;
-      const uint64_t full = ((uint64_t)1 << 28) * S;
-      if (S == 1) {
-        CHECK(window == full, "S=1: window %llu != budget", (unsigned long long)window);
-      } else {
-        const uint64_t cap = std::max<uint64_t>(S * p.chunk, (uint64_t)(kExpectWindows * (double)E));
-        CHECK(window <= std::min(full, cap) + p.chunk && window >= S * p.chunk, "E=%llu S=%zu: window %llu",
-              (unsigned long long)E, S, (unsigned long long)window);
-      }
+    XPool xp;
+    std::vector<std::pair<uint32_t, uint32_t>> cols;
+    for (size_t s = 0; s < 8; ++s) {
+      Launch L;
+      PlanCtx c;
+      c.s = s;
+      c.S = 8;
+      c.budget = 1 << 28;
+      c.resident = 129;
+      c.xp = &xp;
+      CHECK(plan_launch(b, c, L), "plan shard %zu", s);
+      CHECK(L.claims.size() == 1 && L.claims[0].piece == s && L.claims[0].P == 8, "shard %zu claim", s);
+      const bm_item& it = L.plan.items[0][0];
+      CHECK(it.start == 1 && it.count == expect_cap(objs[0].target, 8, L.plan.chunk), "split window %llu",
+            (unsigned long long)it.count);
+      CHECK(it.gn == 8 * it.nwg && it.g0 == s * it.nwg && it.nwg <= 128, "piece columns g0=%u nwg=%u gn=%u", it.g0,
+            it.nwg, it.gn);
+      CHECK(it.xslot != BM_NO_XSLOT && it.xslot == (uint32_t)b.xs[0] - 1, "split piece without a cross-shard slot");
+      for (uint32_t g = it.g0; g < it.g0 + it.nwg; ++g) cols.push_back({it.gn, g});
     }
-    std::vector<SimShard> shards(8);
-    if (E <= 1000000) {  // and the capped steps still give the exact answer
-      while (sim_step(b, shards, 0, 1 << 16)) {
-      }
-      expect_exact(objs[0], b.done[0], b.nonce[0], b.trial[0], "expect_cap", 0);
+    std::sort(cols.begin(), cols.end());
+    CHECK(std::adjacent_find(cols.begin(), cols.end()) == cols.end() && cols.size() == cols.back().first,
+          "pieces do not cover the window's columns exactly once");
+    CHECK(b.open[0].size() == 1 && b.open[0][0].claimed == 8 && b.holder[0] == kShared, "window state");
+    // a ninth plan starts the next window at the frontier
+    Launch L;
+    PlanCtx c;
+    c.S = 8;
+    c.budget = 1 << 28;
+    c.resident = 129;
+    c.xp = &xp;
+    CHECK(plan_launch(b, c, L) && L.claims[0].start == 1 + b.open[0][0].count && L.claims[0].piece == 0,
+          "next window");
+  }
+  // exact answers for single objects over 2, 3 and 8 shards, easy to hard
+  for (uint64_t E : {1000ull, 30000ull, 400000ull}) {
+    for (size_t S : {2, 3, 8}) {
+      std::vector<Obj> objs = random_objs(rng, 2, 1);
+      objs[0].target = kU64Max / E;
+      objs[1].target = kU64Max / (E / 2 + 1);
+      std::vector<uint8_t> ihs;
+      std::vector<uint64_t> tg, st;
+      pack_list(objs, ihs, tg, st);
+      SimLib lib(S, 64, 1 << 16);
+      BatchState b;
+      init(b, 2, ihs.data(), tg.data(), st.data());
+      lib.upload(b);
+      solve(lib, b, (uint64_t)S << 16);
+      for (size_t i = 0; i < 2; ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "split", i);
+      std::unique_lock<std::mutex> lk(lib.eng().mu);
+      lib.eng().detach(lk);
     }
   }
-  // as many objects as shards: object-sharded, no cap (each window a shard's whole share)
-  std::vector<Obj> objs = random_objs(rng, 8, 1);
-  std::vector<uint8_t> ihs(64 * 8);
-  std::vector<uint64_t> tg(8), st(8, 1);
-  for (size_t i = 0; i < 8; ++i) {
-    memcpy(&ihs[64 * i], objs[i].ih, 64);
-    tg[i] = kU64Max / 1000;
-  }
-  BatchState b;
-  init(b, 8, ihs.data(), tg.data(), st.data());
-  StepPlan p;
-  plan_step(b, 0, 1 << 28, 8, p);
-  for (const Win& w : p.wins)
-    CHECK(w.chunks * p.chunk == ((uint64_t)1 << 28), "object-sharded window capped: %llu", (unsigned long long)w.count);
+  fprintf(stderr, "split: interleaved pieces over 8 shards, exact over 2/3/8 shards\n");
 }
 
-// ---- scenario 1d: slices weighted by the shards' measured rates (ShardRates) ----
-static void scenario_weights() {
+// ---- scenario 4: shards of unequal speed (one 3x slower): exact, and the others not gated ----
+static void scenario_unequal() {
+  std::mt19937_64 rng(41);
+  for (size_t S = 1; S <= 8; ++S) {
+    const size_t n = 24 * S;
+    std::vector<Obj> objs = random_objs(rng, n, 1);
+    for (Obj& o : objs) o.target = kU64Max / (2000 + rng() % 30000);
+    std::vector<uint8_t> ihs;
+    std::vector<uint64_t> tg, st;
+    pack_list(objs, ihs, tg, st);
+    std::vector<double> slow(S, 1.0);
+    slow[0] = 3.0;  // shard 0 runs 3x slower
+    SimLib lib(S, 24, 1 << 14, slow);
+    {
+      std::lock_guard<std::mutex> lk(lib.eng().mu);
+      lib.eng().rates.min_trials = 1024;  // the stand-in's launches are small: let them set the weights
+    }
+    BatchState b;
+    init(b, n, ihs.data(), tg.data(), st.data());
+    lib.upload(b);
+    solve(lib, b, (uint64_t)S << 16);
+    for (size_t i = 0; i < n; ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "unequal", i);
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().detach(lk);
+    const EngineStats& es = lib.eng().stats;
+    if (S >= 2) {
+      double others = 0;
+      for (size_t s = 1; s < S; ++s) others += (double)es.shard_trials[s];
+      others /= (double)(S - 1);
+      // not lockstep: a fast shard hashes well over the slow one's share (its fair share of the
+      // objects follows its measured rate, and the others take over its objects at the end)
+      CHECK(others > 1.8 * (double)es.shard_trials[0], "S=%zu: fast shards %.0f trials each, slow shard %llu", S,
+            others, (unsigned long long)es.shard_trials[0]);
+      fprintf(stderr, "unequal: S=%zu slow shard %llu trials, the others %.0f each\n", S,
+              (unsigned long long)es.shard_trials[0], others);
+    }
+  }
+}
+
+// ---- scenario 5: windows clipped at the top of the nonce space ----
+static void scenario_top_of_space() {
+  std::mt19937_64 rng(2);
+  std::vector<Obj> objs = random_objs(rng, 24, 1);
+  for (size_t i = 0; i < objs.size(); ++i) {
+    objs[i].start = kU64Max - (i % 6) * 700;
+    objs[i].target = i % 3 == 0 ? 0 : (i % 3 == 1 ? kU64Max : kU64Max / 900);
+  }
+  std::vector<uint8_t> ihs;
+  std::vector<uint64_t> tg, st;
+  pack_list(objs, ihs, tg, st);
+  for (size_t S : {1, 3, 30}) {
+    SimLib lib(S, 24, 1 << 16);
+    BatchState b;
+    init(b, objs.size(), ihs.data(), tg.data(), st.data());
+    lib.upload(b);
+    solve(lib, b, 1000);
+    for (size_t i = 0; i < objs.size(); ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "top", i);
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().detach(lk);
+  }
+}
+
+// ---- scenario 6: bounded single-object searches (bmpow_search: the scratch batch re-initialised per
+// call, windows cut at the call's last nonce, the previous call's lookahead still in flight) ----
+static void scenario_bounded() {
+  std::mt19937_64 rng(6);
+  for (size_t S : {1, 2, 4}) {
+    SimLib lib(S, 16, 1 << 13);
+    BatchState b;
+    b.cap = 1;
+    for (int obj = 0; obj < 12; ++obj) {
+      std::vector<Obj> o = random_objs(rng, 1, 1);
+      o[0].target = kU64Max / (20000 + rng() % 200000);
+      uint64_t start = 1 + (obj % 3) * 777;
+      o[0].start = start;
+      const uint64_t chunk = 3000 + rng() % 40000;  // the caller's max_trials per call
+      int calls = 0;
+      for (;;) {
+        std::unique_lock<std::mutex> lk(lib.eng().mu);
+        lib.eng().attach(lk, &b);
+        const size_t cap = b.cap;
+        init(b, 1, o[0].ih, &o[0].target, &start);
+        b.cap = cap;
+        lib.init_slots(b, {0});
+        b.lim[0] = start + chunk - 1;
+        std::string err;
+        const int rc = lib.eng().run(lk, kU64Max, false, [&b] { return b.done[0] != BMPOW_PENDING; }, err);
+        CHECK(rc == 0, "bounded run %d %s", rc, err.c_str());
+        ++calls;
+        if (b.done[0] == BMPOW_DONE_FOUND) {
+          CHECK(b.nonce[0] >= start && b.nonce[0] < start + chunk, "hit outside the call's range");
+          expect_exact(o[0], b.done[0], b.nonce[0], b.trial[0], "bounded", (size_t)obj);
+          break;
+        }
+        CHECK(b.done[0] == BMPOW_PENDING && resume_point(b, 0) == start + chunk, "NOT_FOUND resumes at %llu, want %llu",
+              (unsigned long long)resume_point(b, 0), (unsigned long long)(start + chunk));
+        start += chunk;
+        if (calls > 2000) {
+          CHECK(false, "bounded search did not finish");
+          break;
+        }
+      }
+    }
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().detach(lk);
+  }
+  fprintf(stderr, "bounded: resumed single-object searches exact over 1/2/4 shards\n");
+}
+
+// ---- scenario 7: producers feed a running session (PowService's use of the library): adds while
+// launches are in flight, slots reused, a consumer popping finished objects ----
+static void scenario_session() {
+  std::mutex gmu;  // the library's g_mu: every entry point holds it
+  const size_t S = 3;
+  SimLib lib(S, 24, 1 << 13);
+  BatchState b;
+  init(b, 0, nullptr, nullptr, nullptr);
+  b.cap = 1 << 20;  // (no reallocation in the stand-in)
+  std::vector<Obj> all;
+  std::vector<int> slot_owner;                     // slot -> index into `all` (live objects)
+  std::vector<std::array<uint64_t, 3>> results;  // per `all` index: done, nonce, trial
+  std::atomic<int> producers_left{4};
+  std::atomic<bool> stop{false};
+
+  auto producer = [&](int id) {
+    std::mt19937_64 rng(100 + id);
+    for (int burst = 0; burst < 25; ++burst) {
+      const size_t m = 1 + rng() % 40;
+      std::vector<Obj> objs = random_objs(rng, m, 4000);
+      std::vector<uint8_t> ihs;
+      std::vector<uint64_t> tg, st;
+      pack_list(objs, ihs, tg, st);
+      {
+        std::lock_guard<std::mutex> g(gmu);
+        std::unique_lock<std::mutex> lk(lib.eng().mu);
+        std::vector<uint32_t> slots;
+        add(b, m, ihs.data(), tg.data(), nullptr, slots);
+        lib.init_slots(b, slots);
+        lib.eng().notify();
+        for (size_t i = 0; i < m; ++i) {
+          if (slot_owner.size() <= slots[i]) slot_owner.resize(slots[i] + 1, -1);
+          CHECK(slot_owner[slots[i]] == -1, "slot %u handed out while live", slots[i]);
+          slot_owner[slots[i]] = (int)all.size();
+          all.push_back(objs[i]);
+          results.push_back({0, 0, 0});
+        }
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(200 + rng() % 800));
+    }
+    producers_left--;
+  };
+  auto runner = [&]() {  // the service thread: step, pop the finished objects
+    uint32_t slot[64];
+    uint64_t nonce[64], trial[64];
+    uint8_t done[64];
+    for (;;) {
+      std::unique_lock<std::mutex> g(gmu);
+      std::unique_lock<std::mutex> lk(lib.eng().mu);
+      lib.eng().attach(lk, &b);
+      std::string err;
+      const int rc = lib.eng().run(lk, S << 13, true,
+                                   [&] { return b.finished_head < b.finished.size() || b.pending == 0; }, err);
+      CHECK(rc == 0, "session run %d %s", rc, err.c_str());
+      for (;;) {
+        const size_t k = take_done(b, 64, slot, nonce, trial, done);
+        for (size_t j = 0; j < k; ++j) {
+          const int a = slot_owner[slot[j]];
+          CHECK(a >= 0, "finished slot %u has no owner", slot[j]);
+          if (a < 0) continue;
+          results[a] = {done[j], nonce[j], trial[j]};
+          slot_owner[slot[j]] = -1;
+        }
+        if (k < 64) break;
+      }
+      const bool idle = b.pending == 0;
+      if (producers_left.load() == 0 && idle && b.finished_head == b.finished.size()) break;
+      if (idle) {  // let the producers in
+        lk.unlock();
+        g.unlock();
+        std::this_thread::sleep_for(std::chrono::microseconds(300));
+      }
+    }
+    stop.store(true);
+  };
+  std::vector<std::thread> th;
+  for (int i = 0; i < 4; ++i) th.emplace_back(producer, i);
+  th.emplace_back(runner);
+  for (auto& t : th) t.join();
+  {
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().detach(lk);
+  }
+  for (size_t i = 0; i < all.size(); ++i)
+    expect_exact(all[i], (int)results[i][0], results[i][1], results[i][2], "session", i);
+  size_t live = 0;
+  for (int o : slot_owner) live += o >= 0;
+  CHECK(live == 0, "%zu slots still owned after the session drained", live);
+  CHECK(b.n < all.size(), "slots were not reused (%zu slots for %zu objects)", b.n, all.size());
+  fprintf(stderr, "session: %zu objects through %zu slots while the steppers ran\n", all.size(), b.n);
+}
+
+// ---- scenario 8: rate averages, fair shares, the steppers' scheduling class ----
+static void scenario_rates_policy() {
   ShardRates r;
   r.reset(3);
   std::vector<double> w;
@@ -420,160 +784,40 @@ static void scenario_weights() {
   r.sample(1, 1ull << 28, 40.0);  // the average moves a quarter of the way
   CHECK(std::fabs(r.ema[1] - (0.75 * (1 << 28) / 80.0 + 0.25 * (1 << 28) / 40.0)) < 1e-6, "ema step");
 
-  // a weighted step: each shard's chunks in proportion to its weight, and the answers still exact
+  // object mode: a shard takes its weighted fair share, its own objects first
   std::mt19937_64 rng(31);
-  const double wt[4] = {1.0, 0.5, 2.0, 1.25};
-  const size_t n = 400;
-  std::vector<Obj> objs = random_objs(rng, n, 4000);
-  std::vector<uint8_t> ihs(64 * n);
-  std::vector<uint64_t> tg(n), st(n);
-  for (size_t i = 0; i < n; ++i) {
-    memcpy(&ihs[64 * i], objs[i].ih, 64);
-    tg[i] = objs[i].target;
-    st[i] = objs[i].start;
-  }
+  std::vector<Obj> objs = random_objs(rng, 400, 4000);
+  std::vector<uint8_t> ihs;
+  std::vector<uint64_t> tg, st;
+  pack_list(objs, ihs, tg, st);
   BatchState b;
-  init(b, n, ihs.data(), tg.data(), st.data());
-  StepPlan p;
-  CHECK(plan_step(b, (uint64_t)1 << 22, 1 << 20, 4, p, 0, wt), "weighted plan");
-  uint64_t tot = 0;
-  for (size_t s = 0; s < 4; ++s) tot += p.nchunks[s];
-  for (size_t s = 0; s < 4; ++s) {
-    const double share = (double)p.nchunks[s] / (double)tot, want = wt[s] / 4.75;
-    CHECK(std::fabs(share - want) < 0.02, "shard %zu share %.4f want %.4f", s, share, want);
+  init(b, 400, ihs.data(), tg.data(), st.data());
+  Launch L0, L1, L2;
+  PlanCtx c;
+  c.S = 4;
+  c.budget = 1 << 22;
+  c.weight = 0.5;
+  CHECK(plan_launch(b, c, L0) && L0.claims.size() == 50, "weight 0.5 of 400 over 4 shards: %zu", L0.claims.size());
+  c.s = 1;
+  c.weight = 2.0;
+  CHECK(plan_launch(b, c, L1) && L1.claims.size() == 200 && L1.claims[0].obj == 50, "weight 2: %zu from %u",
+        L1.claims.size(), L1.claims.empty() ? 0u : L1.claims[0].obj);
+  c.s = 0;
+  c.weight = 0.5;
+  CHECK(plan_launch(b, c, L2) && L2.claims.size() == 50 && L2.claims[0].obj == 0 && L2.claims[0].start > 1,
+        "shard 0 continues its own objects");
+  // the steppers run at SCHED_IDLE, as the reference's PoW threads (bitmsghash.cpp:149)
+  SimLib lib(3, 8, 1 << 12);
+  {
+    BatchState bb;
+    init(bb, 5, ihs.data(), tg.data(), st.data());
+    lib.upload(bb);
+    solve(lib, bb, 1 << 14);
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().detach(lk);
   }
-  std::vector<SimShard> shards(4);
-  while (sim_step(b, shards, (uint64_t)1 << 16, 1 << 14, 24, wt)) {
-  }
-  for (size_t i = 0; i < n; ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "weighted", i);
-  fprintf(stderr, "weights: rate averages, clamping, weighted slices exact over 4 shards\n");
-}
-
-// ---- scenario 2: windows clipped at the top of the nonce space ----
-static void scenario_top_of_space() {
-  std::mt19937_64 rng(2);
-  std::vector<Obj> objs = random_objs(rng, 24, 1);
-  for (size_t i = 0; i < objs.size(); ++i) {
-    objs[i].start = kU64Max - (i % 6) * 700;
-    objs[i].target = i % 3 == 0 ? 0 : (i % 3 == 1 ? kU64Max : kU64Max / 900);
-  }
-  std::vector<uint8_t> ihs(64 * objs.size());
-  std::vector<uint64_t> tg(objs.size()), st(objs.size());
-  for (size_t i = 0; i < objs.size(); ++i) {
-    memcpy(&ihs[64 * i], objs[i].ih, 64);
-    tg[i] = objs[i].target;
-    st[i] = objs[i].start;
-  }
-  for (size_t S : {1, 3}) {
-    BatchState b;
-    init(b, objs.size(), ihs.data(), tg.data(), st.data());
-    std::vector<SimShard> shards(S);
-    while (sim_step(b, shards, 1000, 1 << 16)) {
-    }
-    for (size_t i = 0; i < objs.size(); ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "top", i);
-  }
-}
-
-// ---- scenario 3: a shared session fed by producer threads (PowService's use of the library) ----
-static void scenario_session() {
-  std::mutex mu;  // the library's g_mu: every entry point holds it
-  BatchState b;
-  init(b, 0, nullptr, nullptr, nullptr);
-  std::vector<SimShard> shards(2);
-  std::vector<Obj> all;
-  std::vector<int> slot_owner;                     // slot -> index into `all` (live objects)
-  std::vector<std::array<uint64_t, 3>> results;  // per `all` index: done, nonce, trial
-  std::atomic<int> producers_left{4};
-  std::atomic<bool> stop{false};
-  std::condition_variable cv;
-
-  auto producer = [&](int id) {
-    std::mt19937_64 rng(100 + id);
-    for (int burst = 0; burst < 25; ++burst) {
-      const size_t m = 1 + rng() % 40;
-      std::vector<Obj> objs = random_objs(rng, m, 4000);
-      std::vector<uint8_t> ihs(64 * m);
-      std::vector<uint64_t> tg(m);
-      for (size_t i = 0; i < m; ++i) {
-        memcpy(&ihs[64 * i], objs[i].ih, 64);
-        tg[i] = objs[i].target;
-      }
-      {
-        std::lock_guard<std::mutex> lk(mu);
-        std::vector<uint32_t> slots;
-        add(b, m, ihs.data(), tg.data(), nullptr, slots);
-        b.cap = std::max(b.cap, b.n);  // the device side's reallocation
-        for (SimShard& sh : shards)      // ... and its reset of the added slots' best[] / found[]
-          for (uint32_t sl : slots)
-            if (sl < sh.best.size()) {
-              sh.best[sl] = kU64Max;
-              sh.found[sl] = 0;
-            }
-        for (size_t i = 0; i < m; ++i) {
-          if (slot_owner.size() <= slots[i]) slot_owner.resize(slots[i] + 1, -1);
-          CHECK(slot_owner[slots[i]] == -1, "slot %u handed out while live", slots[i]);
-          slot_owner[slots[i]] = (int)all.size();
-          all.push_back(objs[i]);
-          results.push_back({0, 0, 0});
-        }
-      }
-      cv.notify_all();
-      std::this_thread::sleep_for(std::chrono::microseconds(200 + rng() % 800));
-    }
-    producers_left--;
-    cv.notify_all();
-  };
-  auto consumer = [&]() {
-    uint32_t slot[64];
-    uint64_t nonce[64], trial[64];
-    uint8_t done[64];
-    for (;;) {
-      std::unique_lock<std::mutex> lk(mu);
-      // wait() (pthread_cond_wait), not wait_for: GCC 11's wait_for uses pthread_cond_clockwait,
-      // which its ThreadSanitizer does not intercept (false "double lock" reports)
-      cv.wait(lk, [&]() { return b.finished_head < b.finished.size() || stop.load(); });
-      const size_t k = take_done(b, 64, slot, nonce, trial, done);
-      for (size_t j = 0; j < k; ++j) {
-        const int a = slot_owner[slot[j]];
-        CHECK(a >= 0, "finished slot %u has no owner", slot[j]);
-        if (a < 0) continue;
-        results[a] = {done[j], nonce[j], trial[j]};
-        slot_owner[slot[j]] = -1;
-      }
-      if (stop.load() && k == 0 && b.finished_head == b.finished.size()) return;
-    }
-  };
-  auto stepper = [&]() {
-    for (;;) {
-      bool stepped;
-      {
-        std::lock_guard<std::mutex> lk(mu);
-        stepped = sim_step(b, shards, 1 << 13, 1 << 16);
-      }
-      cv.notify_all();
-      if (!stepped) {
-        if (producers_left.load() == 0) {
-          std::lock_guard<std::mutex> lk(mu);
-          if (b.pending == 0) break;
-        }
-        std::this_thread::sleep_for(std::chrono::microseconds(300));
-      }
-    }
-    stop.store(true);
-    cv.notify_all();
-  };
-  std::vector<std::thread> th;
-  for (int i = 0; i < 4; ++i) th.emplace_back(producer, i);
-  th.emplace_back(stepper);
-  th.emplace_back(consumer);
-  for (auto& t : th) t.join();
-  for (size_t i = 0; i < all.size(); ++i)
-    expect_exact(all[i], (int)results[i][0], results[i][1], results[i][2], "session", i);
-  size_t live = 0;
-  for (int o : slot_owner) live += o >= 0;
-  CHECK(live == 0, "%zu slots still owned after the session drained", live);
-  CHECK(b.n < all.size(), "slots were not reused (%zu slots for %zu objects)", b.n, all.size());
-  fprintf(stderr, "session: %zu objects through %zu slots\n", all.size(), b.n);
+  for (int p : lib.policies()) CHECK(p == SCHED_IDLE, "stepper thread policy %d, want SCHED_IDLE", p);
+  fprintf(stderr, "rates: averages, clamping, weighted fair shares; steppers at SCHED_IDLE\n");
 }
 
 // ---- scenario 4: min-trial planning and reduction ----
@@ -741,61 +985,60 @@ static void scenario_verify_concurrent() {
   CHECK(bad.load() == 0, "concurrent padding: %d mismatches", bad.load());
 }
 
-// ---- scenario 6: the library's continuous-batching service (bmpow_service_*) over the stand-in ----
+// ---- scenario 9: the library's continuous-batching service (bmpow_service_*) over the engine ----
 static void scenario_service() {
   std::mutex gmu;  // the library's g_mu: every op takes it
+  SimLib lib(2, 24, 1 << 13);
   BatchState b;
   init(b, 0, nullptr, nullptr, nullptr);
-  std::vector<SimShard> shards(2);
+  b.cap = 1 << 20;
   std::atomic<int> fail_step{0}, corrupt{0};
   ServiceOps ops;
   ops.add = [&](size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* tg, uint32_t* slots,
                 std::string&) {
-    std::lock_guard<std::mutex> lk(gmu);
+    std::lock_guard<std::mutex> g(gmu);
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
     std::vector<uint32_t> sl;
     add(b, n, ihs, tg, nullptr, sl, ih_off);
-    b.cap = std::max(b.cap, b.n);
-    for (SimShard& sh : shards)
-      for (uint32_t x : sl)
-        if (x < sh.best.size()) {
-          sh.best[x] = kU64Max;
-          sh.found[x] = 0;
-        }
+    lib.init_slots(b, sl);
+    lib.eng().notify();
     std::copy(sl.begin(), sl.end(), slots);
     return 0;
   };
   ops.step = [&](std::string& err) {
-    std::lock_guard<std::mutex> lk(gmu);
+    std::lock_guard<std::mutex> g(gmu);
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
     if (fail_step.load()) {
       err = "injected step failure";
       return (int)BMPOW_E_HIP;
     }
-    sim_step(b, shards, 1 << 13, 1 << 16);
-    return 0;
+    lib.eng().attach(lk, &b);
+    return lib.eng().run(lk, 2 << 13, true, [&] { return b.finished_head < b.finished.size() || b.pending == 0; },
+                         err);
   };
   ops.take = [&](size_t cap, uint32_t* slot, uint64_t* nonce, uint64_t* trial, uint8_t* done) {
-    std::lock_guard<std::mutex> lk(gmu);
+    std::lock_guard<std::mutex> g(gmu);
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
     const size_t k = take_done(b, cap, slot, nonce, trial, done);
     if (k && corrupt.exchange(0)) trial[0] ^= 1;  // a wrong device answer for the host re-check to catch
     return k;
   };
   ops.reset = [&](std::string&) {
-    std::lock_guard<std::mutex> lk(gmu);
-    b = BatchState();
+    std::lock_guard<std::mutex> g(gmu);
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().detach(lk);
     init(b, 0, nullptr, nullptr, nullptr);
-    shards.assign(2, SimShard());
+    b.cap = 1 << 20;
+    lib.upload(b);
     return 0;
   };
-  Service svc(ops, true);
+  auto svc = std::make_unique<Service>(ops, true);
   auto submit_objs = [&](const std::vector<Obj>& objs, std::vector<uint64_t>& tk) {
-    std::vector<uint8_t> ihs(64 * objs.size());
-    std::vector<uint64_t> tg(objs.size());
-    for (size_t i = 0; i < objs.size(); ++i) {
-      memcpy(&ihs[64 * i], objs[i].ih, 64);
-      tg[i] = objs[i].target;
-    }
+    std::vector<uint8_t> ihs;
+    std::vector<uint64_t> tg, st;
+    pack_list(objs, ihs, tg, st);
     tk.resize(objs.size());
-    return svc.submit(objs.size(), ihs.data(), tg.data(), tk.data());
+    return svc->submit(objs.size(), ihs.data(), tg.data(), tk.data());
   };
   uint64_t tk[64], nn[64], tv[64];
   uint8_t dn[64];
@@ -810,7 +1053,7 @@ static void scenario_service() {
   std::vector<std::array<uint64_t, 4>> got;  // ticket, done, nonce, trial
   std::thread consumer([&] {
     while (got.size() < total) {
-      const int k = svc.poll(64, -1, tk, nn, tv, dn, err);
+      const int k = svc->poll(64, -1, tk, nn, tv, dn, err);
       CHECK(k > 0, "poll returned %d (%s)", k, err.c_str());
       if (k <= 0) return;
       for (int j = 0; j < k; ++j) got.push_back({tk[j], dn[j], nn[j], tv[j]});
@@ -838,7 +1081,7 @@ static void scenario_service() {
           (unsigned long long)sent[i].first, (unsigned long long)got[i][0]);
     expect_exact(sent[i].second, (int)got[i][1], got[i][2], got[i][3], "service", i);
   }
-  CHECK(svc.outstanding() == 0, "outstanding %zu after draining", svc.outstanding());
+  CHECK(svc->outstanding() == 0, "outstanding %zu after draining", svc->outstanding());
 
   // cancel drops in-flight objects that never finish; the service goes on
   std::mt19937_64 rng(77);
@@ -847,22 +1090,22 @@ static void scenario_service() {
   std::vector<uint64_t> t;
   submit_objs(never, t);
   std::this_thread::sleep_for(std::chrono::milliseconds(5));
-  svc.cancel();
-  CHECK(svc.outstanding() == 0, "outstanding after cancel");
+  svc->cancel();
+  CHECK(svc->outstanding() == 0, "outstanding after cancel");
   submit_objs(easy, t);
-  int k = svc.poll(64, -1, tk, nn, tv, dn, err);
+  int k = svc->poll(64, -1, tk, nn, tv, dn, err);
   CHECK(k == 1 && tk[0] == t[0], "after cancel: k=%d", k);
   if (k == 1) expect_exact(easy[0], dn[0], nn[0], tv[0], "after cancel", 0);
 
   // a failing step surfaces as the poll's error; nothing steps until cancel; then it recovers
   submit_objs(never, t);
   fail_step = 1;
-  k = svc.poll(64, -1, tk, nn, tv, dn, err);
+  k = svc->poll(64, -1, tk, nn, tv, dn, err);
   CHECK(k == BMPOW_E_HIP && err == "injected step failure", "error poll: k=%d err=%s", k, err.c_str());
   fail_step = 0;
-  svc.cancel();
+  svc->cancel();
   submit_objs(easy, t);
-  k = svc.poll(64, -1, tk, nn, tv, dn, err);
+  k = svc->poll(64, -1, tk, nn, tv, dn, err);
   CHECK(k == 1 && tk[0] == t[0], "after error: k=%d", k);
   if (k == 1) expect_exact(easy[0], dn[0], nn[0], tv[0], "after error", 0);
 
@@ -880,10 +1123,10 @@ static void scenario_service() {
       off.push_back(cat.size());
     }
     submit_objs(easy, t);  // a 64-byte object queued first: the queue switches to offsets
-    CHECK(svc.submit(5, cat.data(), tgv.data(), tkv.data(), off.data()) == 0, "var submit");
+    CHECK(svc->submit(5, cat.data(), tgv.data(), tkv.data(), off.data()) == 0, "var submit");
     size_t seen = 0;
     while (seen < 6) {
-      k = svc.poll(64, -1, tk, nn, tv, dn, err);
+      k = svc->poll(64, -1, tk, nn, tv, dn, err);
       CHECK(k > 0, "var poll %d", k);
       if (k <= 0) break;
       for (int j = 0; j < k; ++j, ++seen) {
@@ -902,15 +1145,15 @@ static void scenario_service() {
   // the host re-check reports a wrong trial as BMPOW_DONE_BADHASH
   corrupt = 1;
   submit_objs(easy, t);
-  k = svc.poll(64, -1, tk, nn, tv, dn, err);
+  k = svc->poll(64, -1, tk, nn, tv, dn, err);
   CHECK(k == 1 && dn[0] == BMPOW_DONE_BADHASH, "corrupted answer: k=%d done=%d", k, k > 0 ? dn[0] : -1);
   {  // ... also for an initialHash of another length
     std::vector<uint8_t> ih7(7, 3);
     const uint64_t off7[2] = {0, 7}, t7 = kU64Max / 30;
     uint64_t tk7 = 0;
     corrupt = 1;
-    svc.submit(1, ih7.data(), &t7, &tk7, off7);
-    k = svc.poll(64, -1, tk, nn, tv, dn, err);
+    svc->submit(1, ih7.data(), &t7, &tk7, off7);
+    k = svc->poll(64, -1, tk, nn, tv, dn, err);
     CHECK(k == 1 && tk[0] == tk7 && dn[0] == BMPOW_DONE_BADHASH, "corrupted var answer: k=%d", k);
   }
   // stop() wakes a poll blocked on an idle service
@@ -918,28 +1161,42 @@ static void scenario_service() {
     uint64_t a[4], b2[4], c[4];
     uint8_t d[4];
     std::string e2;
-    const int r = svc.poll(4, -1, a, b2, c, d, e2);
+    const int r = svc->poll(4, -1, a, b2, c, d, e2);
     CHECK(r == 0, "poll woken by stop returned %d", r);
   });
   std::this_thread::sleep_for(std::chrono::milliseconds(5));
-  svc.stop();
+  svc->stop();
   waiter.join();
   CHECK(submit_objs(easy, t) == BMPOW_E_STATE, "submit after stop");
+  svc.reset();
+  {
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().detach(lk);
+  }
   fprintf(stderr, "service: %zu objects from 4 producers, cancel and error recovery\n", total);
+}
+
+template <typename F>
+static void timed(const char* name, F f) {
+  const auto t0 = std::chrono::steady_clock::now();
+  f();
+  fprintf(stderr, "  [%s: %.1f s]\n", name, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
 }
 
 int main() {
   init_k();
-  scenario_batches();
-  scenario_var();
-  scenario_expect_cap();
-  scenario_weights();
-  scenario_top_of_space();
-  scenario_session();
-  scenario_min_trial();
-  scenario_verify();
-  scenario_verify_concurrent();
-  scenario_service();
+  timed("batches", scenario_batches);
+  timed("var", scenario_var);
+  timed("split", scenario_split);
+  timed("unequal", scenario_unequal);
+  timed("top_of_space", scenario_top_of_space);
+  timed("bounded", scenario_bounded);
+  timed("session", scenario_session);
+  timed("rates_policy", scenario_rates_policy);
+  timed("min_trial", scenario_min_trial);
+  timed("verify", scenario_verify);
+  timed("verify_concurrent", scenario_verify_concurrent);
+  timed("service", scenario_service);
   if (g_fail) {
     fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

@@ -139,8 +139,9 @@ def test_c1_sweep_stops_within_rows_of_the_hit(gpulib, shards, golden, nshards):
     hashed 29 M on one shard for the 10.9 M useful, profiles/r03/c1_columns_static.jsonl: the SIMD arbiter
     favours older waves, so the columns drifted apart).
 
-    Several shards on ONE device: a split window's shards sweep interleaved columns of the same rows
-    and stop at the first hit of any through the cross-shard bound, but their kernels share this
+    Several shards on ONE device: a split window's pieces (one per shard, claimed by each shard's
+    stepper on its own, bmsched::plan_launch) sweep interleaved columns of the same rows and stop at
+    the first hit of any through the cross-shard bound, but their kernels share this
     device's SIMDs, where the earlier-launched kernel's (older) waves get the issue first, and 8
     streams share the 4 hardware queues (GPU_MAX_HW_QUEUES); so one shard runs ahead of another and
     the waste is bounded by the split window's cap (2E, bmsched::expect_cap), not by rows.  On
@@ -156,9 +157,12 @@ def test_c1_sweep_stops_within_rows_of_the_hit(gpulib, shards, golden, nshards):
         gpulib.bmpow_get_stats(ctypes.byref(st))
         assert st.trials >= k['nonce'] - 1
         if nshards == 1:
-            assert st.trials - k['nonce'] <= 4 * ROW, (st.trials, st.steps)
+            assert st.trials - k['nonce'] <= 4 * ROW, (st.trials, st.launches)
         else:
-            assert st.steps == 1 and st.trials <= 2 * e + nshards * ROW, (st.trials, st.steps)
+            # one split window of 2E (bmsched::expect_cap) in nshards pieces; the pieces of the next
+            # window each shard already queued behind its first stop at their first block (the
+            # relay folds the hit into every shard's best[])
+            assert st.trials <= 2 * e + 2 * nshards * ROW, (st.trials, st.launches)
 
 
 @pytest.mark.slow
