@@ -44,8 +44,6 @@ OPS_PER_TRIAL = 8288
 #: vector-ALU peak, T int32 lane-ops/s: 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz -- the rate
 #: behind MI355X_MICROARCH.md's 157.3 TFLOPS FP32 vector peak (one wave64 VALU op per 2 cycles).
 PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12
-#: BASELINE.md section 3 priced the roofline at 64 lanes/clk/CU (39.32 T); kept for comparison
-BASELINE_MD_PEAK_TOPS = 256 * 64 * 2.4e9 / 1e12
 #: The VALU issue model behind the roofline (profiles/r02): a wave64 VALU
 #: instruction occupies its SIMD for one quad-cycle (4 clocks) unless two waves' full-rate 32-bit ops
 #: pair in it (SQ_ACTIVE_INST_VALU2); bm_search_kernel's mix is 73 % half-rate VOP3 (v_alignbit_b32,
@@ -176,6 +174,54 @@ class Claimer(object):
         return None if lo >= self.n else (lo, min(lo + self.chunk, self.n))
 
 
+def cpu_snapshot(lib):
+    """(process CPU seconds, per-stepper CPU seconds, per-stepper scheduling policy): getrusage of the
+    whole process (every thread: this interpreter, the library's steppers and service thread) and the
+    library's own account of its stepper threads (bmpow_get_thread_info)."""
+    import resource
+    ru = resource.getrusage(resource.RUSAGE_SELF)
+    cpu = (ctypes.c_double * 64)()
+    pol = (ctypes.c_int * 64)()
+    n = lib.bmpow_get_thread_info(cpu, pol, 64)
+    return ru.ru_utime + ru.ru_stime, [cpu[i] for i in range(min(n, 64))], [pol[i] for i in range(min(n, 64))]
+
+
+def cpu_delta(c0, c1, elapsed):
+    """Host CPU the PoW took while the GPU worked: CPU-seconds per wall-second of the timed region."""
+    names = {0: 'SCHED_OTHER', 3: 'SCHED_BATCH', 5: 'SCHED_IDLE'}
+    steppers = [round((b - a) / elapsed, 5) for a, b in zip(c0[1], c1[1])] if len(c0[1]) == len(c1[1]) else []
+    return {'process_cpu_per_s': round((c1[0] - c0[0]) / elapsed, 5), 'stepper_cpu_per_s': steppers,
+            'stepper_policy': sorted({names.get(p, str(p)) for p in c1[2]}),
+            'wait': os.environ.get('BMPOW_WAIT', 'block'),
+            'what': 'getrusage(RUSAGE_SELF) over the timed region (every thread of this process) and each '
+                    'stepper thread\'s CLOCK_THREAD_CPUTIME_ID (bmpow_get_thread_info), per wall-second'}
+
+
+def prove_sample(lib, objs, nonce, idx, k, seed):
+    """Exactness of k answers (a seeded sample of idx) at any size: each nonce n is the _doSafePoW
+    answer (src/proofofwork.py:100-111) iff trial(n) <= target (re-checked with hashlib by the
+    caller) and min{trial(m) : 1 <= m < n} > target -- the min-trial probe (bmpow_min_trial_batch), a
+    kernel apart from the search's hit logic, hashes every nonce below each answer.  Outside the
+    timed region."""
+    import numpy as np
+    from pybitmessage_amd import _lib
+    pick = sorted(random.Random(seed).sample(idx, min(k, len(idx))))
+    if not pick:
+        return None
+    n = len(pick)
+    p64 = ctypes.POINTER(ctypes.c_uint64)
+    st = np.ones(n, dtype=np.uint64)
+    ct = np.array([int(nonce[i]) - 1 for i in pick], dtype=np.uint64)
+    mn, arg = np.zeros(n, dtype=np.uint64), np.zeros(n, dtype=np.uint64)
+    t0 = time.perf_counter()
+    _lib.check(lib, lib.bmpow_min_trial_batch(n, b''.join(objs[i][1] for i in pick), st.ctypes.data_as(p64),
+                                              ct.ctypes.data_as(p64), mn.ctypes.data_as(p64),
+                                              arg.ctypes.data_as(p64)), 'bmpow_min_trial_batch')
+    ok = sum(1 for j, i in enumerate(pick) if int(mn[j]) > objs[i][0])
+    return {'exact': ok, 'of': n, 'trials_rehashed': int(ct.sum()), 'seconds': round(time.perf_counter() - t0, 2),
+            'how': 'bmpow_min_trial_batch over [1, nonce) of each sampled answer: min > target'}
+
+
 def solve_claimed(lib, h, claimer, tag, low_water):
     """Solve the pieces of the global batch this rank claims: the whole table is resident and
     parked; pieces are scheduled (bmpow_batch_set_pending) whenever fewer than low_water objects
@@ -237,12 +283,14 @@ def run_batch_bench(args, dist):
             solve_claimed(lib, h, claimer, 'w%d' % w, low_water)
         dist.barrier()
         lib.bmpow_reset_stats()
+        c0 = cpu_snapshot(lib)
         t0 = time.perf_counter()
         mine = []
         for k in range(args.steps):
             mine = solve_claimed(lib, h, claimer, 's%d' % k, low_water)
         dist.barrier()
         elapsed = time.perf_counter() - t0
+        host_cpu = cpu_delta(c0, cpu_snapshot(lib), elapsed)
         st = _lib.BmpowStats()
         lib.bmpow_get_stats(ctypes.byref(st))
         nonce = np.zeros(n, dtype=np.uint64)
@@ -260,8 +308,12 @@ def run_batch_bench(args, dist):
     useful = float(sum(int(nonce[i]) for i in idx)) * args.steps
     if dist.world > 1:
         desc += ' (global batch of %d, pieces of %d claimed on demand)' % (n, chunk)
+    # exactness of a seeded sample of the answers, proven at full size outside the timed region
+    # (1,000 of C5's 100k; 64 elsewhere)
+    exact = None if args.no_exact else prove_sample(lib, objs, nonce, idx, 1000 if args.config == 'c5' else 64,
+                                                   SEED + dist.rank)
     return {'desc': desc, 'objects': len(idx) * args.steps, 'useful': useful, 'elapsed': elapsed, 'stats': st,
-            'nonces_sum': int(sum(int(nonce[i]) for i in idx))}
+            'nonces_sum': int(sum(int(nonce[i]) for i in idx)), 'host_cpu': host_cpu, 'exact_sample': exact}
 
 
 def run_service_bench(args, dist):
@@ -294,16 +346,19 @@ def run_service_bench(args, dist):
         once()
     dist.barrier()
     lib.bmpow_reset_stats()
+    c0 = cpu_snapshot(lib)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = once()
     dist.barrier()
     elapsed = time.perf_counter() - t0
+    host_cpu = cpu_delta(c0, cpu_snapshot(lib), elapsed)
     st = _lib.BmpowStats()
     lib.bmpow_get_stats(ctypes.byref(st))
     useful = float(sum(n for _, n in res)) * args.steps
     return {'desc': desc + ' via worker.PowService (native stepping thread)', 'objects': len(objs) * args.steps,
-            'useful': useful, 'elapsed': elapsed, 'stats': st}
+            'useful': useful, 'elapsed': elapsed, 'stats': st,
+            'host_cpu': host_cpu}
 
 
 def run_runbatch_bench(args, dist):
@@ -317,16 +372,19 @@ def run_runbatch_bench(args, dist):
         proofofwork.run_batch(objs)
     dist.barrier()
     lib.bmpow_reset_stats()
+    c0 = cpu_snapshot(lib)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         res = proofofwork.run_batch(objs)
     dist.barrier()
     elapsed = time.perf_counter() - t0
+    host_cpu = cpu_delta(c0, cpu_snapshot(lib), elapsed)
     st = _lib.BmpowStats()
     lib.bmpow_get_stats(ctypes.byref(st))
     useful = float(sum(n for _, n in res)) * args.steps
     return {'desc': desc + ' via proofofwork.run_batch', 'objects': len(objs) * args.steps,
-            'useful': useful, 'elapsed': elapsed, 'stats': st}
+            'useful': useful, 'elapsed': elapsed, 'stats': st,
+            'host_cpu': host_cpu}
 
 
 def run_c3_bench(args, dist):
@@ -348,16 +406,18 @@ def run_c3_bench(args, dist):
         sweep()
     dist.barrier()
     lib.bmpow_reset_stats()
+    c0 = cpu_snapshot(lib)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         sweep()
     dist.barrier()
     elapsed = time.perf_counter() - t0
+    host_cpu = cpu_delta(c0, cpu_snapshot(lib), elapsed)
     st = _lib.BmpowStats()
     lib.bmpow_get_stats(ctypes.byref(st))
     desc = 'C3: fixed initialHash, target=0, 2^%d nonces split over %d GPU(s)' % (args.c3_log2, dist.world)
     return {'desc': desc, 'objects': 0, 'useful': float(share) * args.steps, 'elapsed': elapsed, 'stats': st,
-            'scaling': 'strong'}
+            'scaling': 'strong', 'host_cpu': host_cpu}
 
 
 def run_c1_bench(args, dist):
@@ -371,15 +431,19 @@ def run_c1_bench(args, dist):
     for _ in range(args.warmup):
         proofofwork.run(target, ih)
     lib.bmpow_reset_stats()
+    c0 = cpu_snapshot(lib)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         tv, nonce = proofofwork.run(target, ih)
     elapsed = time.perf_counter() - t0
+    host_cpu = cpu_delta(c0, cpu_snapshot(lib), elapsed)
     assert nonce == 10909138, nonce
     st = _lib.BmpowStats()
     lib.bmpow_get_stats(ctypes.byref(st))
     return {'desc': 'C1: one 1 KB msg at defaults via proofofwork.run (golden nonce 10909138)',
-            'objects': args.steps, 'useful': float(nonce) * args.steps, 'elapsed': elapsed, 'stats': st}
+            'objects': args.steps, 'useful': float(nonce) * args.steps, 'elapsed': elapsed, 'stats': st,
+            'host_cpu': host_cpu, 'call_ms': round(elapsed * 1e3 / args.steps, 4),
+            'path': 'engine' if os.environ.get('BMPOW_ONE') == '0' or args.devices > 1 else 'single-object (bm_search1_kernel)'}
 
 
 def verify_objects(n, rank):
@@ -800,6 +864,10 @@ def main():
     ap.add_argument('--service', action='store_true',
                     help='c2/c5: feed the objects through worker.PowService (the library\'s continuous-batching '
                          'service, bmpow_service_submit/poll) instead of one batch')
+    ap.add_argument('--no-exact', action='store_true',
+                    help='skip the min-trial proof of a seeded sample of the answers (after the timed region)')
+    ap.add_argument('--throttle', default=None,
+                    help='--devices A/B: "shard:ms" -- that shard\'s stepper sleeps ms before each launch')
     ap.add_argument('--cpu-baseline-worker', action='store_true', help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_baseline_worker:
@@ -819,6 +887,9 @@ def main():
     lib = _lib.get()
     if args.step_trials:
         lib.bmpow_set_step_trials(args.step_trials)
+    if args.throttle:
+        shard, ms = args.throttle.split(':')
+        _lib.check(lib, lib.bmpow_set_shard_throttle(int(shard), float(ms)), 'bmpow_set_shard_throttle')
 
     if args.config == 'addrgen':
         r = run_addr_bench(args, dist)
@@ -905,7 +976,6 @@ def summarize(args, dist, r, lib_version):
             'kernel_ghs': round(kernel_ghs, 4),
             'avg_launch_ms': round(kernel_ms / max(launches, 1), 3), 'launches': int(launches),
             'kernel_busy_frac': round(kernel_ms * 1e-3 / r['elapsed'], 4),
-            'frac_vs_baseline_md_peak': round(achieved / BASELINE_MD_PEAK_TOPS, 4),
         }
         pmc = pmc_counters()
         if pmc:
@@ -936,32 +1006,45 @@ def summarize(args, dist, r, lib_version):
                     'basis': 'one issue slot per quad-cycle for each VALU instruction but a pair of v_bitop3_b32 '
                              '(%d per trial, tools/isa_census.py) sharing one: (VALU per trial - %d / 2) slots'
                              % (BITOP3_PER_TRIAL, BITOP3_PER_TRIAL)}
-                mix = mix_ceiling()
+                mix = free_running_mix()
                 if mix:
-                    # the free-running instruction-mix microbenchmark: measured, but below what the
-                    # kernel issues since round 3 (the queue's barrier phases the waves better)
-                    mceil = ceil * mix['valu_per_simd_quadcycle']
-                    line['roofline']['mix_ceiling'] = dict(mix, ghs=round(mceil, 4))
-                    line['roofline']['frac_vs_mix_ceiling'] = round(kernel_ghs / mceil, 4)
+                    # what the kernel's instruction mix issues free-running (no dependences, no
+                    # barriers): a measured reference point, not a ceiling -- the kernel itself issues
+                    # more, its per-block barrier phasing the waves better
+                    line['roofline']['free_running_mix'] = dict(mix, ghs=round(ceil * mix['valu_per_simd_quadcycle'], 4))
+    if r.get('host_cpu'):
+        line['host_cpu_per_s'] = r['host_cpu']['process_cpu_per_s']
+        line['host_cpu'] = r['host_cpu']
+    if r.get('exact_sample'):
+        line['exact_sample'] = r['exact_sample']
+    for k in ('call_ms', 'path'):
+        if r.get(k) is not None:
+            line[k] = r[k]
     if r.get('devices'):
-        line['config']['parallelism'] = ('in-process nonce/object sharding over %d devices (bmpow_set_devices, '
-                                         'rate-weighted slices, host min-reduction, no collective)' % r['devices'])
+        line['config']['parallelism'] = ('in-process over %d devices: one stepper thread and stream per device '
+                                         'claiming windows from the objects\' frontiers (bmsched::Engine), '
+                                         'host min-reduction, no collective' % r['devices'])
         line['n_gpus'] = r['devices']
         import ctypes
 
         from pybitmessage_amd import _lib
+        lib = _lib.get()
         rates = (ctypes.c_double * 64)()
-        n = _lib.get().bmpow_get_shard_rates(rates, 64)
+        n = lib.bmpow_get_shard_rates(rates, 64)
         line['shard_rates_ghs'] = [round(rates[i] * 1e3 / 1e9, 4) for i in range(min(n, 64))]
+        tr, ms = (ctypes.c_uint64 * 64)(), (ctypes.c_double * 64)()
+        n = lib.bmpow_get_shard_stats(tr, ms, 64)
+        line['shard_stats'] = [{'trials': int(tr[i]), 'kernel_ms': round(ms[i], 2),
+                                'busy_frac': round(ms[i] * 1e-3 / r['elapsed'], 4)} for i in range(min(n, 64))]
     return line
 
 
-def mix_ceiling():
-    """The issue ceiling of bm_search_kernel's own instruction mix (profiles/mix_ceiling.json, from
-    tools/ubench_mix.py on the GPU box): the kernel's nonce-loop VALU stream, opcode for opcode, with
-    its data dependences removed and every v_bitop3_b32 bank-split, at the kernel's 5 waves per SIMD
-    -- the most that mix can issue per SIMD per quad-cycle (best of the compiler's order, an even
-    spread and grouped bitop3)."""
+def free_running_mix():
+    """bm_search_kernel's nonce-loop VALU stream issued free-running (profiles/mix_ceiling.json, from
+    tools/ubench_mix.py on the GPU box): opcode for opcode, data dependences removed, every
+    v_bitop3_b32 bank-split, best of the compiler's order, an even spread and grouped bitop3.  The
+    kernel issues more per quad-cycle than this stream (round 3), so it is reported as a measured
+    reference point, not as a ceiling."""
     path = os.path.join(ROOT, 'profiles', 'mix_ceiling.json')
     if not os.path.exists(path):
         return None

@@ -355,6 +355,21 @@ typedef struct bmpow_stats {
 BMPOW_API int bmpow_get_stats(bmpow_stats *out);
 BMPOW_API void bmpow_reset_stats(void);
 
+/* Per-shard search work since the last bmpow_reset_stats: trials hashed and summed search-kernel
+ * time (HIP events) of each shard's launches, into trials[0..cap) / kernel_ms[0..cap) (either may be
+ * NULL).  Returns the shard count. */
+BMPOW_API int bmpow_get_shard_stats(uint64_t *trials, double *kernel_ms, int cap);
+
+/* The per-shard stepper threads (one per shard, bmsched::Engine): CPU seconds each has used so far
+ * (CLOCK_THREAD_CPUTIME_ID) and its scheduling policy (sched_getscheduler: SCHED_IDLE by default, as
+ * the reference's PoW threads, src/bitmsghash/bitmsghash.cpp:149; BMPOW_THREAD_POLICY=batch|normal
+ * overrides).  Either output may be NULL.  Returns the shard count (0 before bmpow_init). */
+BMPOW_API int bmpow_get_thread_info(double *cpu_s, int *policy, int cap);
+
+/* A/B and test knob: shard `shard`'s stepper sleeps `ms` before each launch (a slow device); 0 turns
+ * it off.  Returns 0 or < 0. */
+BMPOW_API int bmpow_set_shard_throttle(int shard, double ms);
+
 /* Per-shard trial budget of one step (one kernel launch), default 2^29 (~80 ms on one MI355X: the
  * interrupt granularity of a batch); set 0 to restore the default.  At least one chunk (8,192). */
 BMPOW_API uint64_t bmpow_get_step_trials(void);

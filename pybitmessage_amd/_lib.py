@@ -107,6 +107,9 @@ SIGNATURES = [
     ('bmpow_service_destroy', None, [_vp]),
     ('bmpow_get_stats', ctypes.c_int, [ctypes.POINTER(BmpowStats)]),
     ('bmpow_reset_stats', None, []),
+    ('bmpow_get_shard_stats', ctypes.c_int, [_p64, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
+    ('bmpow_get_thread_info', ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ('bmpow_set_shard_throttle', ctypes.c_int, [ctypes.c_int, ctypes.c_double]),
     ('bmpow_get_step_trials', _u64, []),
     ('bmpow_set_step_trials', None, [_u64]),
     ('bmpow_pow_values', ctypes.c_int, [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64]),

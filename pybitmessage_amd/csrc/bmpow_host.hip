@@ -545,6 +545,10 @@ int batch_add_locked(std::unique_lock<std::mutex>& lk, bmpow_batch* b, size_t m,
     return rc;
   }
   int rc = sync_vpool(lk, b);  // before the slots that use the new words are handed to the steppers' kernels
+  if (rc == 0 && !b->vmoved.empty()) {  // a compaction moved live objects' words (sync_vpool drained)
+    rc = init_slots(b, b->vmoved.data(), b->vmoved.size());
+    b->vmoved.clear();
+  }
   if (rc == 0) rc = init_slots(b, slots.data(), slots.size());
   if (g_engine) g_engine->notify();
   return rc;
@@ -2190,6 +2194,42 @@ void bmpow_reset_stats(void) {
     es.shard_ms.assign(S, 0.0);
     es.shard_trials.assign(S, 0);
   }
+}
+
+int bmpow_get_shard_stats(uint64_t* trials, double* kernel_ms, int cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_engine) return 0;
+  std::lock_guard<std::mutex> el(g_engine->mu);
+  const bmsched::EngineStats& es = g_engine->stats;
+  for (int i = 0; i < (int)es.shard_ms.size() && i < cap; ++i) {
+    if (trials) trials[i] = es.shard_trials[i];
+    if (kernel_ms) kernel_ms[i] = es.shard_ms[i];
+  }
+  return (int)g_shards.size();
+}
+
+int bmpow_get_thread_info(double* cpu_s, int* policy, int cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_engine) return 0;
+  std::vector<double> c;
+  std::vector<int> p;
+  {
+    std::lock_guard<std::mutex> el(g_engine->mu);
+    g_engine->thread_info(c, p);
+  }
+  for (int i = 0; i < (int)c.size() && i < cap; ++i) {
+    if (cpu_s) cpu_s[i] = c[i];
+    if (policy) policy[i] = p[i];
+  }
+  return (int)c.size();
+}
+
+int bmpow_set_shard_throttle(int shard, double ms) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (!g_engine) return set_err(BMPOW_E_STATE, "library not initialised");
+  if (shard < 0 || shard >= (int)g_shards.size() || !(ms >= 0)) return set_err(BMPOW_E_ARG, "bad shard or delay");
+  g_engine->set_throttle((size_t)shard, ms);
+  return 0;
 }
 
 uint64_t bmpow_get_step_trials(void) { return g_step_trials.load(); }

@@ -103,7 +103,11 @@ __device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const 
       const uint64_t off = blk * BM_BLOCK;
       const uint64_t first = it.start + off;
       const uint64_t nonce = first + threadIdx.x;
+#ifdef BM_HETERO  // A/B variant: odd waves run the other instruction order (sha512_dev.h)
+      const uint64_t tv = ((threadIdx.x >> 6) & 1) ? trial_of_b(ihw, nonce) : trial_of(ihw, nonce);
+#else
       const uint64_t tv = trial_of(ihw, nonce);
+#endif
       const bool live = off + threadIdx.x < it.count;
       // Wavefront min-reduction of the hits: a wave's 64 nonces are consecutive, so its smallest hit
       // is its lowest hitting lane -- one atomicMin per wave instead of one per hitting lane.  Same

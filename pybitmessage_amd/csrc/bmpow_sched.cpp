@@ -167,7 +167,10 @@ void init(BatchState& b, size_t n, const uint8_t* ihs, const uint64_t* targets, 
   grow_slots(b, n);
   for (size_t i = 0; i < n; ++i) {
     pack_var(ih_ptr(ihs, ih_off, i), ih_len(ih_off, i), targets[i], &b.objs[i], b.vpool);
-    if (b.objs[i].ihlen != BM_IH_MAIN) b.nvar_slots++;
+    if (b.objs[i].ihlen != BM_IH_MAIN) {
+      b.nvar_slots++;
+      b.vlive += bm_var_words(b.objs[i].ihlen);
+    }
     b.done[i] = BMPOW_PENDING;
     restart_slot(b, i, start ? start[i] : 1);
   }
@@ -187,11 +190,34 @@ void mark_finished(BatchState& b, uint32_t slot) {
 
 }  // namespace
 
+namespace {
+
+// Repack vpool to the words of the slots that still hold a var-form object (see add()).
+void compact_vpool(BatchState& b) {
+  std::vector<uint64_t> pool;
+  pool.reserve(b.vlive);
+  for (size_t k = 0; k < b.n; ++k) {
+    bm_obj& o = b.objs[k];
+    if (b.done[k] == BMPOW_FREE || o.ihlen == BM_IH_MAIN) continue;
+    const uint64_t w = bm_var_words(o.ihlen);
+    const uint64_t at = pool.size();
+    pool.insert(pool.end(), b.vpool.begin() + (ptrdiff_t)o.vword, b.vpool.begin() + (ptrdiff_t)(o.vword + w));
+    if (o.vword != at) b.vmoved.push_back((uint32_t)k);
+    o.vword = at;
+  }
+  b.vpool.swap(pool);
+  b.vpool_epoch++;
+}
+
+}  // namespace
+
 bool add(BatchState& b, size_t m, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
          std::vector<uint32_t>& slots, const uint64_t* ih_off) {
   if (b.nvar_slots == 0 && !b.vpool.empty()) {  // nothing refers to the old words any more
     b.vpool.clear();
     b.vpool_epoch++;
+  } else if (b.vpool.size() > 2 * b.vlive && b.vpool.size() - b.vlive > ((size_t)1 << 16)) {
+    compact_vpool(b);
   }
   slots.resize(m);
   const size_t n0 = b.n;
@@ -207,7 +233,10 @@ bool add(BatchState& b, size_t m, const uint8_t* ihs, const uint64_t* targets, c
   for (size_t i = 0; i < m; ++i) {
     const uint32_t k = slots[i];
     pack_var(ih_ptr(ihs, ih_off, i), ih_len(ih_off, i), targets[i], &b.objs[k], b.vpool);
-    if (b.objs[k].ihlen != BM_IH_MAIN) b.nvar_slots++;
+    if (b.objs[k].ihlen != BM_IH_MAIN) {
+      b.nvar_slots++;
+      b.vlive += bm_var_words(b.objs[k].ihlen);
+    }
     restart_slot(b, k, start ? start[i] : 1);
     b.done[k] = BMPOW_PENDING;
     b.pending++;
@@ -226,7 +255,10 @@ size_t take_done(BatchState& b, size_t cap, uint32_t* slot_out, uint64_t* nonce_
     if (trial_out) trial_out[k] = b.trial[s];
     if (done_out) done_out[k] = b.done[s];
     b.done[s] = BMPOW_FREE;
-    if (b.objs[s].ihlen != BM_IH_MAIN) b.nvar_slots--;
+    if (b.objs[s].ihlen != BM_IH_MAIN) {
+      b.nvar_slots--;
+      b.vlive -= bm_var_words(b.objs[s].ihlen);
+    }
     b.free_slots.push_back(s);
     ++k;
   }
@@ -1206,10 +1238,22 @@ bool Engine::can_plan() const {
   return b_ && !b_->broken && !error_ && !stop_ && claimed_ < limit_ && !(ops_.aborted && ops_.aborted());
 }
 
+void Engine::thread_info(std::vector<double>& cpu_s, std::vector<int>& policy) {
+  cpu_s.assign(S_, 0.0);
+  policy.assign(S_, -2);
+  for (size_t s = 0; s < S_; ++s) {
+    policy[s] = sh_[s].policy;
+    timespec ts;
+    if (sh_[s].have_clock && clock_gettime(sh_[s].cpu_clock, &ts) == 0) cpu_s[s] = (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+  }
+}
+
 void Engine::stepper(size_t s) {
   if (ops_.thread_init) ops_.thread_init(s);
   std::unique_lock<std::mutex> lk(mu);
   EShard& e = sh_[s];
+  e.policy = sched_getscheduler(0);
+  e.have_clock = pthread_getcpuclockid(pthread_self(), &e.cpu_clock) == 0;
   for (;;) {
     // 1. while fewer than two launches are in flight, plan the next one (it queues behind the
     //    running one on the shard's stream)

@@ -17,6 +17,8 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <time.h>
+
 #include <atomic>
 #include <condition_variable>
 #include <deque>
@@ -82,7 +84,11 @@ struct BatchState {
   // no slot holds a var object any more (vpool_epoch then counts up, so the device copy restarts)
   std::vector<uint64_t> vpool;
   size_t nvar_slots = 0;  // non-free slots holding a var-form object
+  size_t vlive = 0;       // words of vpool those slots use (the rest belong to released slots)
   uint64_t vpool_epoch = 0;
+  // slots whose var-form words add() moved (a compaction of vpool, which also starts a new epoch):
+  // their device records (vword) must be rewritten before the next launch
+  std::vector<uint32_t> vmoved;
   // ---- the claim frontier of per-device stepping (Engine, plan_launch / apply_launch) ----
   std::vector<uint32_t> gen;     // bumped whenever the slot's search restarts: older launches are stale
   std::vector<uint64_t> lim;     // last nonce a window may reach (inclusive): a bounded search's end
@@ -101,6 +107,10 @@ void init(BatchState& b, size_t n, const uint8_t* ihs, const uint64_t* targets, 
 
 // Append m objects (slots reused first).  slots[i] = object i's slot.  Returns true when the table
 // outgrew b.cap (the caller reallocates and re-uploads); false when only `slots` need uploading.
+// Var-form words of released slots are reclaimed: once they outnumber the live ones (and 64 Ki
+// words), the pool is repacked -- live objects' words moved down, their vword updated and their
+// slots listed in b.vmoved, a new vpool_epoch -- so a service fed steady non-64-byte objects keeps
+// a pool of about twice its live words.
 bool add(BatchState& b, size_t m, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
          std::vector<uint32_t>& slots, const uint64_t* ih_off = nullptr);
 
@@ -302,6 +312,9 @@ class Engine {
   EngineStats stats; // under mu
   int error() const { return error_; }
   void clear_error() { error_ = 0; err_.clear(); }
+  // Each stepper thread's CPU seconds so far (CLOCK_THREAD_CPUTIME_ID) and scheduling policy
+  // (sched_getscheduler as the thread set it; -2 before it ran).
+  void thread_info(std::vector<double>& cpu_s, std::vector<int>& policy);
 
  private:
   struct EShard {
@@ -309,6 +322,9 @@ class Engine {
     Launch buf[2];
     int next = 0;
     double throttle_ms = 0;
+    int policy = -2;       // the stepper's scheduling policy
+    clockid_t cpu_clock{}; // its CPU-time clock
+    bool have_clock = false;
   };
   void stepper(size_t s);
   bool can_plan() const;

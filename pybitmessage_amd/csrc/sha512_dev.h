@@ -236,6 +236,45 @@ BM_DEV void rounds(uint64_t (&s)[8], uint64_t (&w)[16]) {
   }
 }
 
+#ifdef BM_HETERO
+// A/B variant (BM_HETERO): the same dataflow in another instruction order, for
+// the odd waves of each workgroup, so the waves sharing a SIMD run different streams.  Rounds 16..79
+// go in groups of 8: the group's eight schedule words first (sigma0 / sigma1: rotates and shifts),
+// then its eight rounds (Sigma, Ch, Maj: the v_bitop3_b32-rich part), with scheduling barriers
+// between the phases so the compiler keeps them apart.
+template <int T, int END, bool kTrial1>
+BM_DEV void sched_words(uint64_t (&w)[16]) {
+  if constexpr (T < END) {
+    constexpr bool kU0 = kTrial1 && T <= 23;
+    constexpr bool kU1 = kTrial1 && (T == 19 || T == 21 || T == 23);
+    w[T & 15] = (w[(T - 7) & 15] + sig0<kU0>(w[(T - 15) & 15]) + w[(T - 16) & 15]) + sig1<kU1>(w[(T - 2) & 15]);
+    sched_words<T + 1, END, kTrial1>(w);
+  }
+}
+template <int T, int END>
+BM_DEV void rounds_only(uint64_t (&s)[8], const uint64_t (&w)[16]) {
+  if constexpr (T < END) {
+    constexpr int A = (8 - (T & 7)) & 7;
+    constexpr int B = (A + 1) & 7, C = (A + 2) & 7, D = (A + 3) & 7;
+    constexpr int E = (A + 4) & 7, F = (A + 5) & 7, G = (A + 6) & 7, H = (A + 7) & 7;
+    const uint64_t t1 = add64(add64(add64(s[H], Sig1(s[E])), Ch(s[E], s[F], s[G])), K(T) + w[T & 15]);
+    s[D] = add64(s[D], t1);
+    s[H] = add64(add64(t1, Sig0(s[A])), Maj(s[A], s[B], s[C]));
+    rounds_only<T + 1, END>(s, w);
+  }
+}
+template <int T, bool kTrial1>
+BM_DEV void rounds_grouped(uint64_t (&s)[8], uint64_t (&w)[16]) {
+  if constexpr (T < 80) {
+    sched_words<T, T + 8, kTrial1>(w);
+    __builtin_amdgcn_sched_barrier(0);
+    rounds_only<T, T + 8>(s, w);
+    __builtin_amdgcn_sched_barrier(0);
+    rounds_grouped<T + 8, kTrial1>(s, w);
+  }
+}
+#endif
+
 // Rounds of a block whose whole message schedule is per-object: kw[t] = K[t] + W[t] precomputed on
 // the host (the later blocks of a long initialHash's first hash, bmsched::pack_var), read with
 // uniform (scalar) loads, so a round is its state update alone.
@@ -281,6 +320,34 @@ BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
   rounds<1, 80>(s2, w2);
   return s2[0] + IV(0);
 }
+
+#ifdef BM_HETERO
+// trial_of with rounds 16..79 of both blocks in rounds_grouped's order (the A/B variant above).
+BM_DEV uint64_t trial_of_b(const uint64_t (&ihw)[8], uint64_t nonce) {
+  uint64_t w[16];
+  w[0] = nonce;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[1 + i] = ihw[i];
+  w[9] = PAD;
+#pragma unroll
+  for (int i = 10; i < 15; ++i) w[i] = 0;
+  w[15] = 72 * 8;
+  uint64_t s[8] = {IV(0), IV(1), IV(2), nonce + E1C, IV(4), IV(5), IV(6), nonce + A1C};
+  rounds<1, 16, true>(s, w);
+  rounds_grouped<16, true>(s, w);
+  uint64_t w2[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w2[i] = s[i] + IV(i);
+  w2[8] = PAD;
+#pragma unroll
+  for (int i = 9; i < 15; ++i) w2[i] = 0;
+  w2[15] = 64 * 8;
+  uint64_t s2[8] = {IV(0), IV(1), IV(2), w2[0] + E1C, IV(4), IV(5), IV(6), w2[0] + A1C};
+  rounds<1, 16>(s2, w2);
+  rounds_grouped<16, false>(s2, w2);
+  return s2[0] + IV(0);
+}
+#endif
 
 // trial(n, ih) for an initialHash of any length L != 64 (the reference hashes pack('>Q', n) + ih as
 // given, src/proofofwork.py:104-107).  The first hash's message BE64(n) || ih || padding is

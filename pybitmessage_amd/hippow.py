@@ -34,6 +34,11 @@ ALIASES = ('HIP', 'hip', 'gfx950', 'MI355X', VENDOR)
 gpus = []
 enabledGpus = []
 vendors = []
+#: the keys.dat ``opencl`` value of the last :func:`initCL` call that named one; :func:`initCL`
+#: without an argument (``proofofwork.resetPoW``) applies it again, as the reference's initCL re-reads
+#: the setting from the config every time (``openclpow.py:45``)
+_setting = None
+_UNSET = object()
 
 #: trials per bounded device call in ``do_opencl_pow`` (its shutdown-poll interval)
 CALL_TRIALS = 1 << 30
@@ -50,12 +55,18 @@ class Device(object):
         return '<hippow.Device %s>' % self.name
 
 
-def initCL(setting=None):
+def initCL(setting=_UNSET):
     """Discover gfx950 devices and enable them (reference ``initCL``, ``openclpow.py:31-64``).
 
     ``setting`` is the keys.dat ``[bitmessagesettings] opencl`` value; ``None`` or any of
     :data:`ALIASES` enables every visible device, another vendor name leaves them disabled
-    (the reference enables only the platform whose vendor matches)."""
+    (the reference enables only the platform whose vendor matches).  Omitted, the last setting
+    given applies (``None`` before any)."""
+    global _setting
+    if setting is _UNSET:
+        setting = _setting
+    else:
+        _setting = setting
     del enabledGpus[:]
     del vendors[:]
     del gpus[:]

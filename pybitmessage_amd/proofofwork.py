@@ -329,7 +329,9 @@ def _device_count():
 
 def resetPoW():
     """Re-select devices and re-enable the backend after :func:`gpu_failed` (reference
-    ``:328-330`` re-ran ``openclpow.initCL``, which re-enables the GPUs)."""
+    ``:328-330`` re-ran ``openclpow.initCL``, which re-reads the keys.dat ``opencl`` setting: the
+    GPUs come back only when the configured vendor is this backend -- :func:`hippow.initCL` applies
+    the last setting it was given)."""
     global _disabled
     _disabled = None
     _lib.reset()

@@ -60,5 +60,6 @@ def _reenable_backend():
     """A test that feeds a wrong GPU answer disables the backend process-wide (proofofwork.gpu_failed,
     as the reference's _doGPUPoW clears openclpow.enabledGpus); the next test starts enabled."""
     yield
-    from pybitmessage_amd import proofofwork
+    from pybitmessage_amd import hippow, proofofwork
     proofofwork._disabled = None
+    hippow._setting = None  # the keys.dat opencl value hippow.initCL remembers

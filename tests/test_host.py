@@ -43,9 +43,9 @@ def test_header_declares_the_boundary():
               'bmpow_service_submit', 'bmpow_service_poll', 'bmpow_service_cancel', 'bmpow_service_outstanding',
               'bmpow_service_stop', 'bmpow_service_destroy', 'bmpow_set_device_count', 'bmpow_trials_len',
               'bmpow_search_len', 'bmpow_min_trial_var', 'bmpow_batch_add_var', 'bmpow_service_submit_var',
-              'bmpow_get_shard_rates']:
+              'bmpow_get_shard_rates', 'bmpow_get_shard_stats', 'bmpow_get_thread_info', 'bmpow_set_shard_throttle']:
         assert s in syms
-    assert len(syms) == 54
+    assert len(syms) == 57
 
 
 def test_library_exports_every_declared_symbol(rawlib):
@@ -87,6 +87,10 @@ def test_shard_rates_without_devices():
     assert list(rates) == [-1, -1, -1, -1]
     assert lib.bmpow_get_shard_rates(None, 4) == _lib.E_ARG
     assert lib.bmpow_get_shard_rates(None, 0) == 0
+    # the per-shard stats and the stepper threads' info are host state too (no stepper yet)
+    assert lib.bmpow_get_shard_stats(None, None, 4) == 0
+    assert lib.bmpow_get_thread_info(None, None, 4) == 0
+    assert lib.bmpow_set_shard_throttle(0, 1.0) == _lib.E_STATE
 
 
 @pytest.mark.skipif(os.path.exists('/dev/kfd'), reason='a GPU is present')
@@ -267,6 +271,22 @@ def test_wrong_gpu_answer_disables_the_backend(scripted, monkeypatch, caplog):
         assert proofofwork.run(2 ** 64 // 1000, ih) == [2417842470843601, 1315]
     finally:
         proofofwork._disabled = None
+
+
+def test_reset_pow_keeps_the_configured_vendor(scripted, monkeypatch):
+    """resetPoW after the user picked another vendor in the settings (bitmessageqt/settings.py:452-458
+    puts it in keys.dat, then resetPoW -> initCL re-reads it, src/proofofwork.py:328-330,
+    src/openclpow.py:45): the HIP devices stay present but disabled; picking HIP again enables them."""
+    from pybitmessage_amd import hippow
+    scripted()
+    monkeypatch.setattr(_lib, 'reset', lambda: None)
+    hippow.initCL('NVIDIA Corporation')
+    assert hippow.openclAvailable() and not hippow.openclEnabled()
+    proofofwork.resetPoW()
+    assert hippow.openclAvailable() and not hippow.openclEnabled()
+    hippow.initCL('HIP')
+    proofofwork.resetPoW()
+    assert hippow.openclEnabled()
 
 
 def test_do_opencl_pow_any_length_and_negative_target(scripted, golden):

@@ -15,6 +15,8 @@
 #   c1-columns       tools/diag/c1_columns.py (C1 waste by column count)
 #   atomic-rate      tools/diag/atomic_rate (single-address atomic rate)
 #   ubench-mix       tools/ubench_mix (the search kernel's instruction-mix issue ceiling)
+#   ab:V1,V2,...     tools/cmp_variants.sh over the variants (default | variants/<name>), CONFIGS=AB_CONFIGS
+#   c1-one-vs-engine C1 through run(): the single-object path (spin, then block wait) vs the engine
 #   rehearse-n2 | rehearse-n8   the driver's N-rank bench command with every rank on GPU 0
 #                    (--share-device: launch, claiming, barriers, one JSON line; not a scaling number)
 set -euo pipefail
@@ -47,6 +49,11 @@ for step in "$@"; do
       timeout -k 10 500 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$n" --master-addr 127.0.0.1 \
         --master-port $((29500 + n)) bench.py --gpus "$n" --steps 1 --warmup 1 --share-device \
         > "$OUT/bench_n$n.json" 2> "$OUT/bench_n$n.err" ;;
+    ab:*) CONFIGS=${AB_CONFIGS:-c3} timeout -k 10 900 bash tools/cmp_variants.sh "$OUT/ab" $(echo "${step#ab:}" | tr ',' ' ') \
+            > "$OUT/ab.txt" 2> "$OUT/ab.err" ;;
+    c1-one-vs-engine) timeout -k 10 200 python3 bench.py --config c1 --steps 40 --warmup 3 --no-cpu-baseline > "$OUT/c1_one.json" 2> "$OUT/c1_one.err" &&
+      BMPOW_ONE=0 timeout -k 10 200 python3 bench.py --config c1 --steps 40 --warmup 3 --no-cpu-baseline > "$OUT/c1_engine.json" 2> "$OUT/c1_engine.err" &&
+      BMPOW_WAIT1=block timeout -k 10 200 python3 bench.py --config c1 --steps 40 --warmup 3 --no-cpu-baseline > "$OUT/c1_one_block.json" 2> "$OUT/c1_one_block.err" ;;
     *) echo "unknown step $step" >&2; exit 2 ;;
   esac
 done
