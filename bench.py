@@ -192,7 +192,7 @@ def cpu_delta(c0, c1, elapsed):
     steppers = [round((b - a) / elapsed, 5) for a, b in zip(c0[1], c1[1])] if len(c0[1]) == len(c1[1]) else []
     return {'process_cpu_per_s': round((c1[0] - c0[0]) / elapsed, 5), 'stepper_cpu_per_s': steppers,
             'stepper_policy': sorted({names.get(p, str(p)) for p in c1[2]}),
-            'wait': os.environ.get('BMPOW_WAIT', 'block'),
+            'wait': os.environ.get('BMPOW_WAIT', 'sleep'),
             'what': 'getrusage(RUSAGE_SELF) over the timed region (every thread of this process) and each '
                     'stepper thread\'s CLOCK_THREAD_CPUTIME_ID (bmpow_get_thread_info), per wall-second'}
 
@@ -432,17 +432,33 @@ def run_c1_bench(args, dist):
         proofofwork.run(target, ih)
     lib.bmpow_reset_stats()
     c0 = cpu_snapshot(lib)
+    # per call: wall time and trials hashed (the stats counters are read between calls, outside the
+    # call, so the distribution shows a slow or wasteful call without slowing the others)
+    per_ms, per_trials, prev = [], [], 0
+    cst = _lib.BmpowStats()
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        c = time.perf_counter()
         tv, nonce = proofofwork.run(target, ih)
+        per_ms.append((time.perf_counter() - c) * 1e3)
+        lib.bmpow_get_stats(ctypes.byref(cst))
+        per_trials.append(cst.trials - prev)
+        prev = cst.trials
     elapsed = time.perf_counter() - t0
     host_cpu = cpu_delta(c0, cpu_snapshot(lib), elapsed)
     assert nonce == 10909138, nonce
     st = _lib.BmpowStats()
     lib.bmpow_get_stats(ctypes.byref(st))
+
+    def dist(xs, nd):
+        xs = sorted(xs)
+        return {'min': round(xs[0], nd), 'median': round(xs[len(xs) // 2], nd), 'p90': round(xs[int(0.9 * (len(xs) - 1))], nd),
+                'max': round(xs[-1], nd)}
     return {'desc': 'C1: one 1 KB msg at defaults via proofofwork.run (golden nonce 10909138)',
             'objects': args.steps, 'useful': float(nonce) * args.steps, 'elapsed': elapsed, 'stats': st,
             'host_cpu': host_cpu, 'call_ms': round(elapsed * 1e3 / args.steps, 4),
+            'per_call': {'ms': dist(per_ms, 4), 'trials': dist(per_trials, 0),
+                         'past_answer_frac': dist([(x - nonce) / x for x in per_trials], 5)},
             'path': 'engine' if os.environ.get('BMPOW_ONE') == '0' or args.devices > 1 else 'single-object (bm_search1_kernel)'}
 
 
@@ -854,8 +870,11 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--share-device', action='store_true', help=argparse.SUPPRESS)
     ap.add_argument('--devices', type=int, default=0,
-                    help='one process driving this many GPUs in-process (bmpow_set_devices: one object\'s '
-                         'nonce space sharded over them, host min-reduction); 0 = one GPU per rank')
+                    help='one process driving this many GPUs in-process (bmpow_set_devices: one stepper thread '
+                         'per device claiming windows of the objects, host min-reduction); 0 = one GPU per rank')
+    ap.add_argument('--shards-per-device', type=int, default=1,
+                    help='--devices: this many shards (streams, each with its own stepper) per device -- on a '
+                         'one-GPU box, a rehearsal of the multi-device path, not a scaling number')
     ap.add_argument('--test-mode', action='store_true',
                     help='c5: the reference\'s test-mode difficulty (ntpb and extra / 100): 100k objects of '
                          '~2e4 trials each, so per-object host and launch costs dominate')
@@ -880,7 +899,7 @@ def main():
     if args.devices:
         if dist.world > 1:
             raise SystemExit('--devices drives several GPUs from one process: run it without torch.distributed')
-        os.environ['BMPOW_DEVICES'] = ','.join(str(i) for i in range(args.devices))
+        os.environ['BMPOW_DEVICES'] = ','.join(str(i) for i in range(args.devices) for _ in range(args.shards_per_device))
     else:
         os.environ['BMPOW_DEVICES'] = '0' if args.share_device else str(dist.local_rank)
     from pybitmessage_amd import _lib
@@ -917,8 +936,8 @@ def main():
         runner = run_service_bench if args.service else run_runbatch_bench
     if args.devices:
         n = lib.bmpow_get_devices((ctypes.c_int * 64)(), 64)
-        if n != args.devices:
-            raise SystemExit('asked for %d devices, the library selected %d' % (args.devices, n))
+        if n != args.devices * args.shards_per_device:
+            raise SystemExit('asked for %d shards, the library selected %d' % (args.devices * args.shards_per_device, n))
     r = runner(args, dist)
     r['devices'] = args.devices
     line = summarize(args, dist, r, lib.bmpow_version().decode())
@@ -958,6 +977,12 @@ def summarize(args, dist, r, lib_version):
         'performed_ghs': round(performed / el_max / 1e9, 4),
         'wasted_frac': round(1.0 - useful / performed, 5) if performed else None,
     }
+    cut = dist.reduce(getattr(st, 'cut_trials', 0), 'sum')
+    if cut:
+        # run()'s kernel: nonces that hashed only their first compression before the call's answer
+        # was published below them (not in performed); as half-trials, the work they cost
+        line['cut_trials'] = int(cut)
+        line['wasted_frac_incl_cut'] = round(1.0 - useful / (performed + 0.5 * cut), 5)
     # per-GPU kernel rate, averaged over the ranks (each rank's device-counted trials over its own
     # summed kernel time, HIP events on the launching stream); one rank: that GPU's
     rank_ghs = st.trials / (kernel_ms * 1e-3) / 1e9 if kernel_ms > 0 else 0.0
@@ -1017,14 +1042,19 @@ def summarize(args, dist, r, lib_version):
         line['host_cpu'] = r['host_cpu']
     if r.get('exact_sample'):
         line['exact_sample'] = r['exact_sample']
-    for k in ('call_ms', 'path'):
+    for k in ('call_ms', 'path', 'per_call'):
         if r.get(k) is not None:
             line[k] = r[k]
     if r.get('devices'):
-        line['config']['parallelism'] = ('in-process over %d devices: one stepper thread and stream per device '
-                                         'claiming windows from the objects\' frontiers (bmsched::Engine), '
-                                         'host min-reduction, no collective' % r['devices'])
+        spd = getattr(args, 'shards_per_device', 1)
+        line['config']['parallelism'] = ('in-process over %d device(s) x %d shard(s): one stepper thread and stream '
+                                         'per shard claiming windows from the objects\' frontiers (bmsched::Engine), '
+                                         'host min-reduction, no collective%s'
+                                         % (r['devices'], spd, '; shards share a GPU: a rehearsal of the multi-device '
+                                            'path, not a scaling number' if spd > 1 else ''))
         line['n_gpus'] = r['devices']
+        if args.throttle:
+            line['config']['throttle'] = args.throttle
         import ctypes
 
         from pybitmessage_amd import _lib

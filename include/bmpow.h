@@ -350,6 +350,9 @@ typedef struct bmpow_stats {
     double verify_host_build_ms;    /* sort, layout, padding into pinned staging, PCIe upload issued */
     double verify_host_run_ms;      /* kernel + results back (waits for the uploads) */
     double verify_host_verdict_ms;  /* IEEE-double verdicts */
+    /* run()'s single-object kernel: nonces whose trial stopped after the first of its two SHA-512
+       compressions, the call's answer having been published below them meanwhile (not in trials) */
+    uint64_t cut_trials;
 } bmpow_stats;
 
 BMPOW_API int bmpow_get_stats(bmpow_stats *out);

@@ -53,7 +53,8 @@ class BmpowStats(ctypes.Structure):
                 ('addr_tries', ctypes.c_uint64), ('addr_kernel_ms', ctypes.c_double),
                 ('probe_trials', ctypes.c_uint64), ('probe_kernel_ms', ctypes.c_double),
                 ('verify_host_build_ms', ctypes.c_double), ('verify_host_run_ms', ctypes.c_double),
-                ('verify_host_verdict_ms', ctypes.c_double)]
+                ('verify_host_verdict_ms', ctypes.c_double),
+                ('cut_trials', ctypes.c_uint64)]
 
 
 class BmpowAddress(ctypes.Structure):

@@ -61,11 +61,16 @@ int set_err(int code, const std::string& msg) {
       return set_err(BMPOW_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));           \
   } while (0)
 
-// How a stepper waits for its launch (BMPOW_WAIT, read once): "block" (default) sleeps in
-// hipEventSynchronize on an event created with hipEventBlockingSync -- the thread uses no CPU while
-// the GPU works; "spin" is HIP's default wait (busy); "poll" queries the event every 50 us.
-enum WaitMode { kWaitBlock, kWaitSpin, kWaitPoll };
-WaitMode g_wait = kWaitBlock;
+// How a stepper waits for its launch (BMPOW_WAIT, read once):
+//   "sleep" (default): query the launch's event and sleep between queries for 1/32 of the time waited
+//     so far (20 us .. 1 ms) -- a few hundred queries per second of launch, and while two launches
+//     are in flight a late wake-up costs the GPU nothing (the next launch is already queued);
+//   "block": hipEventSynchronize on an event created with hipEventBlockingSync, with the device's
+//     hipDeviceScheduleBlockingSync flag set (measured on MI355X: without the flag the wait spins at
+//     one CPU per stepper, profiles/r04/);
+//   "spin": HIP's default wait (busy); "poll": query the event every 50 us.
+enum WaitMode { kWaitSleep, kWaitBlock, kWaitSpin, kWaitPoll };
+WaitMode g_wait = kWaitSleep;
 // run()'s single-object path (search_one): BMPOW_WAIT1 "spin" (default) polls the result word,
 // "block" sleeps in hipEventSynchronize on a blocking-sync event first; BMPOW_ONE=0 sends run()
 // through the engine instead (A/B).
@@ -293,6 +298,7 @@ void make_engine() {
   ops.aborted = [] { return g_abort.load() != 0; };
   ops.thread_init = [](size_t s) {
     (void)hipSetDevice(g_shards[s].dev);
+    if (g_wait == kWaitBlock) (void)hipSetDeviceFlags(hipDeviceScheduleBlockingSync);
     bmsched::set_thread_background();
   };
   g_engine.reset(new bmsched::Engine(ops, g_shards.size(), g_resident, g_step_trials.load()));
@@ -342,7 +348,10 @@ int select_devices(const std::vector<int>& ids) {
 int init_locked() {
   if (g_inited) return (int)g_shards.size();
   if (const char* w = std::getenv("BMPOW_WAIT"))
-    g_wait = std::strcmp(w, "spin") == 0 ? kWaitSpin : (std::strcmp(w, "poll") == 0 ? kWaitPoll : kWaitBlock);
+    g_wait = std::strcmp(w, "spin") == 0    ? kWaitSpin
+             : std::strcmp(w, "poll") == 0  ? kWaitPoll
+             : std::strcmp(w, "block") == 0 ? kWaitBlock
+                                            : kWaitSleep;
   if (const char* w = std::getenv("BMPOW_WAIT1")) g_one_block = std::strcmp(w, "block") == 0;
   if (const char* w = std::getenv("BMPOW_ONE")) g_one_enabled = std::atoi(w) != 0;
   const auto vis = visible_gfx950();
@@ -635,7 +644,13 @@ int engine_wait(bmsched::Launch& L, std::string& err) {
   LaunchBuf& lb = sh.lb[L.buf];
   hipError_t e = hipSetDevice(sh.dev);
   if (e == hipSuccess) {
-    if (g_wait == kWaitPoll) {
+    if (g_wait == kWaitSleep) {
+      const auto t0 = std::chrono::steady_clock::now();
+      while ((e = hipEventQuery(lb.evd)) == hipErrorNotReady) {
+        const int64_t waited = std::chrono::duration_cast<std::chrono::microseconds>(std::chrono::steady_clock::now() - t0).count();
+        std::this_thread::sleep_for(std::chrono::microseconds(std::min<int64_t>(1000, std::max<int64_t>(20, waited / 32))));
+      }
+    } else if (g_wait == kWaitPoll) {
       while ((e = hipEventQuery(lb.evd)) == hipErrorNotReady) std::this_thread::sleep_for(std::chrono::microseconds(50));
     } else {
       e = hipEventSynchronize(lb.evd);
@@ -926,6 +941,7 @@ int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
     g_stats.launches++;
     g_stats.steps++;
     g_stats.trials += o.trials;
+    g_stats.cut_trials += o.cut;
     const double ms = (double)(o.t1 - o.t0) * 1e-5;  // s_memrealtime: 100 MHz
     g_stats.kernel_ms += ms;
     g_stats.max_shard_kernel_ms += ms;

@@ -46,18 +46,25 @@ using namespace bm;
 #ifndef BM_SEARCH_WAVES
 #define BM_SEARCH_WAVES 4
 #endif
+#ifndef BM_CUT  // the single-object kernel's mid-trial bound check (sweep's kCut); 0 for A/B builds
+#define BM_CUT 1
+#endif
 // One workgroup's sweep of a work item: it takes the item's blocks from the item's queue (bm_block_of),
 // in order, until the window ends or the next block lies above the running minimum.
 // kX: the launch holds items with a cross-shard bound slot, whose hits are published there.
 // log (the single-object kernel): each hit's trial value is logged, so the result needs no re-hash.
+// kCut (the single-object kernel): the running minimum is read again between a block's two
+// compressions; a block that starts above it skips its second (every nonce of it lies above a hit),
+// so a wave stops half a trial sooner after the answer is published.  Such lanes are counted in *cut,
+// not in the trials hashed.
 // Returns the trials this wave hashed (its own lanes: every wave counts itself, whichever of the
 // workgroup's waves leaves first).
-template <bool kX>
+template <bool kX, bool kCut = false>
 __device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const uint64_t* __restrict__ wsrc,
                                           uint64_t target, unsigned long long* __restrict__ bestp,
                                           uint32_t* __restrict__ foundp, unsigned long long* __restrict__ queue,
                                           unsigned long long* __restrict__ xb, uint32_t xrows,
-                                          bm_one_call* __restrict__ log) {
+                                          bm_one_call* __restrict__ log, uint32_t* cut = nullptr) {
   const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;  // blocks of the window
   // the queue hands out units of BM_GRAB blocks (1 by default; larger is an A/B knob)
   const uint64_t nunit = (nblk + BM_GRAB - 1) / BM_GRAB;
@@ -103,12 +110,25 @@ __device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const 
       const uint64_t off = blk * BM_BLOCK;
       const uint64_t first = it.start + off;
       const uint64_t nonce = first + threadIdx.x;
+      bool live = off + threadIdx.x < it.count;
 #ifdef BM_HETERO  // A/B variant: odd waves run the other instruction order (sha512_dev.h)
       const uint64_t tv = ((threadIdx.x >> 6) & 1) ? trial_of_b(ihw, nonce) : trial_of(ihw, nonce);
 #else
-      const uint64_t tv = trial_of(ihw, nonce);
+      uint64_t tv;
+      if constexpr (kCut) {
+        uint64_t st[8];
+        trial_first(ihw, nonce, st);
+        if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < first) {
+          *cut += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(live));
+          live = false;
+          tv = ~0ULL;
+        } else {
+          tv = trial_second(st);
+        }
+      } else {
+        tv = trial_of(ihw, nonce);
+      }
 #endif
-      const bool live = off + threadIdx.x < it.count;
       // Wavefront min-reduction of the hits: a wave's 64 nonces are consecutive, so its smallest hit
       // is its lowest hitting lane -- one atomicMin per wave instead of one per hitting lane.  Same
       // box (profiles/r03/waves_queue_ab/wave_min_ab.txt): C3 6.713-6.718 against 6.709-6.718 GH/s
@@ -250,9 +270,12 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search1_kernel(c
   it.nwg = a.nwg;
   it.xslot = BM_NO_XSLOT;
   it.pad = 0;
-  const uint32_t done = sweep<false>(it, 0, w, a.target, &call->best, &call->found, &ctr->queue, nullptr, 0, call);
+  uint32_t cut = 0;
+  const uint32_t done = sweep<false, BM_CUT>(it, 0, w, a.target, &call->best, &call->found, &ctr->queue, nullptr, 0,
+                                             call, &cut);
   if ((threadIdx.x & 63) != 0) return;
   if (done) atomicAdd(&ctr->trials, (unsigned long long)done);
+  if (cut) atomicAdd(&ctr->cut, cut);
   const uint32_t waves = a.nwg * (BM_BLOCK / 64);
   if (__hip_atomic_fetch_add(&ctr->waves_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) != waves - 1) return;
   // the last wave (lane 0): every other wave's hits and counts are visible (acq_rel above)
@@ -270,17 +293,20 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search1_kernel(c
   bm_one_out* const o = a.out;
   const uint64_t t0 = __hip_atomic_load(&ctr->t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint64_t tr = __hip_atomic_load(&ctr->trials, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t nc = __hip_atomic_load(&ctr->cut, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __hip_atomic_store(&o->nonce, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&o->trial, trial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&o->trials, tr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&o->t0, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&o->t1, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&o->found, found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&o->cut, nc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // the launch's counters, for the launch that next uses this ring entry
   ctr->queue = 0;
   ctr->trials = 0;
   ctr->t0 = 0;
   ctr->waves_done = 0;
+  ctr->cut = 0;
   __hip_atomic_store(&o->seq, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

@@ -96,12 +96,14 @@ struct bm_one_ctr {
   unsigned long long queue;   // the block queue
   unsigned long long trials;  // trials hashed (each wave adds its own)
   unsigned long long t0;      // s_memrealtime of the first workgroup (0 = unset)
-  uint32_t waves_done, pad;   // waves that have left the sweep
+  uint32_t waves_done;        // waves that have left the sweep
+  uint32_t cut;               // lanes whose block skipped its second compression (a hit below it)
 };
 // The launch's result, host-mapped; seq is written last (release), the host polls it.
 struct bm_one_out {
   uint64_t nonce, trial, trials, t0, t1;  // t0, t1: s_memrealtime (100 MHz) at the first start, last exit
-  uint32_t found, pad;
+  uint32_t found;
+  uint32_t cut;  // lanes that hashed only the first compression of their trial (bm_one_ctr.cut)
   uint64_t seq;
 };
 // The kernel's arguments (by value).

@@ -291,9 +291,10 @@ BM_DEV void rounds_kw(uint64_t (&s)[8], const uint64_t* __restrict__ kw) {
   }
 }
 
-// trial(n, ih) with ih given as 8 big-endian words.  Round 0 of each block is folded:
-// from the IV with W0 unknown, a1 = W0 + A1C and e1 = W0 + E1C.
-BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
+// trial(n, ih) with ih given as 8 big-endian words, in two halves: the first hash's compression
+// (trial_first, s = its 80-round state) and the second hash (trial_second).  Round 0 of each block is
+// folded: from the IV with W0 unknown, a1 = W0 + A1C and e1 = W0 + E1C.
+BM_DEV void trial_first(const uint64_t (&ihw)[8], uint64_t nonce, uint64_t (&s)[8]) {
   uint64_t w[16];
   w[0] = nonce;
 #pragma unroll
@@ -303,11 +304,18 @@ BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
   for (int i = 10; i < 15; ++i) w[i] = 0;
   w[15] = 72 * 8;
   // state after the folded round 0 (round 1 has A = 7: a=s7 b=s0 c=s1 d=s2 e=s3 f=s4 g=s5 h=s6)
-  uint64_t s[8] = {IV(0), IV(1), IV(2), nonce + E1C, IV(4), IV(5), IV(6), nonce + A1C};
+  s[0] = IV(0);
+  s[1] = IV(1);
+  s[2] = IV(2);
+  s[3] = nonce + E1C;
+  s[4] = IV(4);
+  s[5] = IV(5);
+  s[6] = IV(6);
+  s[7] = nonce + A1C;
   rounds<1, 80, true>(s, w);
-#ifdef BM_TRIAL_MID
-  BM_TRIAL_MID();  // A/B hook of the search kernel (bmpow_kernels.hip), nothing elsewhere
-#endif
+}
+
+BM_DEV uint64_t trial_second(const uint64_t (&s)[8]) {
   // after 80 rounds A = 0: s[i] holds a..h in order
   uint64_t w2[16];
 #pragma unroll
@@ -319,6 +327,15 @@ BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
   uint64_t s2[8] = {IV(0), IV(1), IV(2), w2[0] + E1C, IV(4), IV(5), IV(6), w2[0] + A1C};
   rounds<1, 80>(s2, w2);
   return s2[0] + IV(0);
+}
+
+BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
+  uint64_t s[8];
+  trial_first(ihw, nonce, s);
+#ifdef BM_TRIAL_MID
+  BM_TRIAL_MID();  // A/B hook of the search kernel (bmpow_kernels.hip), nothing elsewhere
+#endif
+  return trial_second(s);
 }
 
 #ifdef BM_HETERO

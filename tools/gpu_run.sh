@@ -11,12 +11,17 @@
 #   c1 | c3 | c4 | c5 | verify | addrgen      bench.py --config X (short runs, no CPU baseline)
 #   rocprof-bench    rocprofv3 --kernel-trace --stats over the default bench (3 steps)
 #   pmc              tools/profile_pmc.sh OUT/pmc (C3 2^33, one counter group per pass)
+#   pmc:V            the same with the variant build variants/<name> (OUT/pmc_<name>)
 #   shard-latency    tools/shard_latency.py
 #   c1-columns       tools/diag/c1_columns.py (C1 waste by column count)
 #   atomic-rate      tools/diag/atomic_rate (single-address atomic rate)
 #   ubench-mix       tools/ubench_mix (the search kernel's instruction-mix issue ceiling)
 #   ab:V1,V2,...     tools/cmp_variants.sh over the variants (default | variants/<name>), CONFIGS=AB_CONFIGS
 #   c1-one-vs-engine C1 through run(): the single-object path (spin, then block wait) vs the engine
+#   c1-dist:V        C1 through run(), 300 calls with the variant's library (default | variants/<name>):
+#                    the per-call distribution of wall time and trials past the answer
+#   c2-wait:MODE     bench-quick with BMPOW_WAIT=MODE (sleep | block | spin | poll): the steppers' CPU
+#   devices:N:K[:T]  C3 and C4 via --devices N --shards-per-device K (throttle shard 0 by T ms)
 #   rehearse-n2 | rehearse-n8   the driver's N-rank bench command with every rank on GPU 0
 #                    (--share-device: launch, claiming, barriers, one JSON line; not a scaling number)
 set -euo pipefail
@@ -27,9 +32,24 @@ PYT=(python3 -u -m pytest --timeout 300 --timeout-method thread -v)
 for step in "$@"; do
   echo "[gpu_run] $(date +%T) $step" >&2
   case "$step" in
-    suite) timeout -k 10 1000 "${PYT[@]}" tests -m "gpu and not slow" > "$OUT/pytest_gpu.log" 2>&1 ;;
-    suite-slow) timeout -k 10 600 "${PYT[@]}" tests -m "gpu and slow" > "$OUT/pytest_gpu_slow.log" 2>&1 ;;
-    tests:*) timeout -k 10 900 "${PYT[@]}" -x tests -m gpu -k "${step#tests:}" > "$OUT/pytest_k.log" 2>&1 ;;
+    # test failures (pytest exit 1) are recorded and the call goes on; anything else ends it
+    suite) rc=0; timeout -k 10 1000 "${PYT[@]}" tests -m "gpu and not slow" > "$OUT/pytest_gpu.log" 2>&1 || rc=$?
+      [ $rc -le 1 ] || exit $rc ;;
+    suite-slow) rc=0; timeout -k 10 600 "${PYT[@]}" tests -m "gpu and slow" > "$OUT/pytest_gpu_slow.log" 2>&1 || rc=$?
+      [ $rc -le 1 ] || exit $rc ;;
+    tests:*) rc=0; timeout -k 10 900 "${PYT[@]}" tests -m gpu -k "${step#tests:}" > "$OUT/pytest_k.log" 2>&1 || rc=$?
+      [ $rc -le 1 ] || exit $rc ;;
+    c1-dist:*) v=${step#c1-dist:}; if [ "$v" = default ]; then L=pybitmessage_amd/lib/libbmpow_hip.so; else L=$v/libbmpow_hip.so; fi
+      BMPOW_LIB=$L timeout -k 10 200 python3 bench.py --config c1 --steps 300 --warmup 5 --no-cpu-baseline \
+        > "$OUT/c1_dist_$(basename "$v").json" 2> "$OUT/c1_dist_$(basename "$v").err" ;;
+    c2-wait:*) m=${step#c2-wait:}
+      BMPOW_WAIT=$m timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/c2_wait_$m.json" 2> "$OUT/c2_wait_$m.err" ;;
+    devices:*) IFS=: read -r _ n k t <<< "$step"; t=${t:-0}; tag="n${n}_k${k}_t${t}"
+      thr=(); [ "$t" = 0 ] || thr=(--throttle "0:$t")
+      timeout -k 10 300 python3 bench.py --config c3 --c3-log2 36 --steps 1 --warmup 0 --no-cpu-baseline --devices "$n" \
+        --shards-per-device "$k" "${thr[@]}" > "$OUT/c3_dev_$tag.json" 2> "$OUT/c3_dev_$tag.err" &&
+      timeout -k 10 300 python3 bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline --devices "$n" \
+        --shards-per-device "$k" "${thr[@]}" > "$OUT/c4_dev_$tag.json" 2> "$OUT/c4_dev_$tag.err" ;;
     bench) timeout -k 10 600 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
     bench-quick) timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/c2.json" 2> "$OUT/c2.err" ;;
     c1) timeout -k 10 200 python3 bench.py --config c1 --steps 20 --warmup 2 --no-cpu-baseline > "$OUT/c1.json" 2> "$OUT/c1.err" ;;
@@ -41,6 +61,8 @@ for step in "$@"; do
     rocprof-bench) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof" -o run -- \
                      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/rocprof_bench.json" 2> "$OUT/rocprof_bench.err" ;;
     pmc) bash tools/profile_pmc.sh "$OUT/pmc" 33 > "$OUT/pmc.log" 2>&1 ;;
+    pmc:*) v=${step#pmc:}; BMPOW_LIB=$v/libbmpow_hip.so bash tools/profile_pmc.sh "$OUT/pmc_$(basename "$v")" 33 \
+             > "$OUT/pmc_$(basename "$v").log" 2>&1 ;;
     shard-latency) timeout -k 10 200 python3 tools/shard_latency.py > "$OUT/shard_latency.json" 2> "$OUT/shard_latency.err" ;;
     c1-columns) timeout -k 10 300 python3 tools/diag/c1_columns.py parent 0 1024 512 > "$OUT/c1_columns.jsonl" 2> "$OUT/c1_columns.err" ;;
     atomic-rate) timeout -k 10 120 ./tools/diag/atomic_rate > "$OUT/atomic_rate.jsonl" 2> "$OUT/atomic_rate.err" ;;

@@ -2,14 +2,17 @@
 # PMC passes for bm_search_kernel on the GPU box (one counter group per rocprofv3 run, no
 # tracing domains beside --pmc).  Workload: C3 sweep (target 0, fixed initialHash) of
 # 2^LOG2 nonces = 2^(LOG2-28) full launches of 2^28 trials each (--step-trials: the PMC method
-# stays at 2^28-trial launches whatever the library default).
-#   usage: tools/profile_pmc.sh OUTDIR [LOG2]
+# stays at 2^28-trial launches whatever the library default).  BMPOW_ONE=0 sends the C3 sweep through
+# the engine's bm_search_kernel (the default bench's kernel) rather than run()'s bm_search1_kernel;
+# BMPOW_LIB selects a variant build (tools/cmp_variants.sh's variants/<name>).
+#   usage: [BMPOW_LIB=variants/x/libbmpow_hip.so] tools/profile_pmc.sh OUTDIR [LOG2]
 set -euo pipefail
 OUT=${1:?outdir}
 LOG2=${2:-33}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-md5sum pybitmessage_amd/lib/libbmpow_hip.so > "$OUT/lib.md5"
+export BMPOW_ONE=0
+md5sum "${BMPOW_LIB:-pybitmessage_amd/lib/libbmpow_hip.so}" > "$OUT/lib.md5"
 CMD=(python3 bench.py --config c3 --c3-log2 "$LOG2" --steps 1 --warmup 0 --no-cpu-baseline --step-trials 268435456)
 if [ -n "${PMC_DEFAULT_BENCH:-}" ]; then CMD=(python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline); fi
 pass() {
