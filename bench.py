@@ -182,7 +182,7 @@ def cpu_snapshot(lib):
     ru = resource.getrusage(resource.RUSAGE_SELF)
     cpu = (ctypes.c_double * 64)()
     pol = (ctypes.c_int * 64)()
-    n = lib.bmpow_get_thread_info(cpu, pol, 64)
+    n = lib.bmpow_get_thread_info(cpu, pol, 64) if hasattr(lib, 'bmpow_get_thread_info') else 0  # (older A/B builds)
     return ru.ru_utime + ru.ru_stime, [cpu[i] for i in range(min(n, 64))], [pol[i] for i in range(min(n, 64))]
 
 
@@ -356,9 +356,12 @@ def run_service_bench(args, dist):
     st = _lib.BmpowStats()
     lib.bmpow_get_stats(ctypes.byref(st))
     useful = float(sum(n for _, n in res)) * args.steps
+    nonce = [n for _, n in res]
+    exact = None if args.no_exact else prove_sample(lib, objs, nonce, list(range(len(objs))),
+                                                   1000 if args.config == 'c5' else 64, SEED + dist.rank)
     return {'desc': desc + ' via worker.PowService (native stepping thread)', 'objects': len(objs) * args.steps,
             'useful': useful, 'elapsed': elapsed, 'stats': st,
-            'host_cpu': host_cpu}
+            'host_cpu': host_cpu, 'exact_sample': exact}
 
 
 def run_runbatch_bench(args, dist):
@@ -417,7 +420,14 @@ def run_c3_bench(args, dist):
     lib.bmpow_get_stats(ctypes.byref(st))
     desc = 'C3: fixed initialHash, target=0, 2^%d nonces split over %d GPU(s)' % (args.c3_log2, dist.world)
     return {'desc': desc, 'objects': 0, 'useful': float(share) * args.steps, 'elapsed': elapsed, 'stats': st,
-            'scaling': 'strong', 'host_cpu': host_cpu}
+            'scaling': 'strong', 'host_cpu': host_cpu,
+            'kernel': 'bm_search1_kernel' if single_object_path(args) else 'bm_search_kernel'}
+
+
+def single_object_path(args):
+    """run()/bmpow_search on one shard take the single-object kernel (bmpow_host.hip search_one)
+    unless BMPOW_ONE=0; several shards (--devices) take the engine."""
+    return os.environ.get('BMPOW_ONE') != '0' and max(1, args.devices) * args.shards_per_device == 1
 
 
 def run_c1_bench(args, dist):
@@ -459,7 +469,8 @@ def run_c1_bench(args, dist):
             'host_cpu': host_cpu, 'call_ms': round(elapsed * 1e3 / args.steps, 4),
             'per_call': {'ms': dist(per_ms, 4), 'trials': dist(per_trials, 0),
                          'past_answer_frac': dist([(x - nonce) / x for x in per_trials], 5)},
-            'path': 'engine' if os.environ.get('BMPOW_ONE') == '0' or args.devices > 1 else 'single-object (bm_search1_kernel)'}
+            'path': 'single-object (bm_search1_kernel)' if single_object_path(args) else 'engine (bm_search_kernel)',
+            'kernel': 'bm_search1_kernel' if single_object_path(args) else 'bm_search_kernel'}
 
 
 def verify_objects(n, rank):
@@ -992,7 +1003,7 @@ def summarize(args, dist, r, lib_version):
         kernel_ghs = mean_ghs
         achieved = OPS_PER_TRIAL * kernel_ghs * 1e9 / 1e12
         line['roofline'] = {
-            'bound': 'valu', 'kernel': 'bm_search_kernel',
+            'bound': 'valu', 'kernel': r.get('kernel', 'bm_search_kernel'),
             'achieved': round(achieved, 3), 'peak': round(PEAK_TOPS, 3),
             'unit': 'T int32 lane-ops/s (8,288 algorithmic ops per trial)',
             'frac': round(achieved / PEAK_TOPS, 4), 'traffic': None,
@@ -1097,7 +1108,8 @@ def pmc_counters():
     with open(path) as f:
         full = json.load(f)
     d = full['derived']
-    out = {'traffic': d.get('hbm_bytes_per_launch_upper'), 'source': 'profiles/pmc_latest.json (C3, 2^28-trial launches)',
+    out = {'traffic': d.get('hbm_bytes_per_launch_upper'),
+           'source': 'profiles/pmc_latest.json (bm_search_kernel, C3, 2^28-trial launches)',
            'build': full.get('build'), 'trials_per_launch': full.get('raw', {}).get('trials_per_launch')}
     for k in ('valu_instr_per_trial', 'valu_issue_util', 'valu_instr_per_simd_quad_cycle', 'dual_issue_share',
               'simd_busy_frac', 'wave_issue_stall_share', 'wave_wait_share', 'eff_clock_ghz'):

@@ -149,7 +149,12 @@ def load(path=None):
                                         'or make -C pybitmessage_amd/csrc)' % path)
     lib = ctypes.CDLL(path)
     for name, res, args in SIGNATURES:
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if os.path.abspath(path) == os.path.abspath(DEFAULT_PATH):
+                raise
+            continue  # an A/B build of an earlier round (BMPOW_LIB) may lack later entry points
         fn.restype = res
         fn.argtypes = args
     return lib

@@ -911,8 +911,20 @@ int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
   const uint64_t bpw = bmsched::kBlocksPerWorker;
   uint64_t next = start;
   bool top = false;
-  uint64_t fly[4];  // sequence numbers in flight, oldest first
+  uint64_t fly[4], fly_n[4];  // sequence numbers in flight, oldest first, and their windows' nonces
   int nfly = 0;
+  // The next window is queued behind the running one only while the windows in flight may well hold
+  // no hit (fewer than kAheadE x E nonces, E = 2^64 / (target + 1): P(no hit) > e^-8): a C1 object
+  // (E ~ 1.3e7 against a 2^29 window) then costs one launch, and no idle lookahead launch sits in the
+  // next call's way; a hard object (C4, E ~ 1.5e9) or a sweep (C3) keeps two windows in flight.
+  constexpr double kAheadE = 8.0;
+  const double expect = 18446744073709551616.0 / ((double)target + 1.0);
+  auto in_flight = [&]() {
+    double n = 0;
+    for (int i = 0; i < nfly; ++i) n += (double)fly_n[i];
+    return n;
+  };
+  auto want_next = [&]() { return !top && nfly < 2 && (nfly == 0 || in_flight() < kAheadE * expect); };
   auto launch = [&]() -> int {
     const uint64_t room = end - next;  // nonces after next, up to end
     const uint64_t count = room >= step ? step : room + 1;
@@ -926,13 +938,14 @@ int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
     a.out = g_one.d_out + r;
     HIPTRY(bm_launch_search1(sh.stream, a));
     HIPTRY(hipEventRecord(g_one.ev[a.seq % kOneEvents], sh.stream));
-    fly[nfly++] = a.seq;
+    fly[nfly] = a.seq;
+    fly_n[nfly++] = count;
     if (room < step) top = true;
     else next += count;
     return 0;
   };
   rc = launch();
-  if (rc == 0 && !top) rc = launch();  // the next window, queued behind
+  while (rc == 0 && want_next()) rc = launch();  // the next window, queued behind
   while (rc == 0) {
     const uint64_t seq = fly[0];
     rc = wait_one(seq);
@@ -950,10 +963,13 @@ int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
       *trial_out = o.trial;
       return BMPOW_FOUND;  // a window still queued stops at its first block (the call's best)
     }
-    for (int i = 1; i < nfly; ++i) fly[i - 1] = fly[i];
+    for (int i = 1; i < nfly; ++i) {
+      fly[i - 1] = fly[i];
+      fly_n[i - 1] = fly_n[i];
+    }
     --nfly;
     if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
-    if (!top) rc = launch();
+    while (rc == 0 && want_next()) rc = launch();
     if (nfly == 0) return BMPOW_NOT_FOUND;
   }
   return rc;
@@ -1568,7 +1584,9 @@ const char* bmpow_last_error(void) { return g_err.c_str(); }
 
 const char* bmpow_version(void) {
   static char buf[128];
-  std::snprintf(buf, sizeof buf, "bmpow %d gfx950 block=%d iters=%d", BMPOW_ABI_VERSION, BM_BLOCK, BM_ITERS);
+  // the build time identifies the library a bench line or profile came from
+  std::snprintf(buf, sizeof buf, "bmpow %d gfx950 block=%d iters=%d built %s %s", BMPOW_ABI_VERSION, BM_BLOCK, BM_ITERS,
+                __DATE__, __TIME__);
   return buf;
 }
 

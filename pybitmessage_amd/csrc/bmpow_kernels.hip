@@ -46,6 +46,9 @@ using namespace bm;
 #ifndef BM_SEARCH_WAVES
 #define BM_SEARCH_WAVES 4
 #endif
+#ifndef BM_LAG_PRIO  // issue priority for workgroups behind the queue (sweep); 0 for A/B builds
+#define BM_LAG_PRIO 1
+#endif
 #ifndef BM_CUT  // the single-object kernel's mid-trial bound check (sweep's kCut); 0 for A/B builds
 #define BM_CUT 1
 #endif
@@ -72,6 +75,9 @@ __device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const 
   __shared__ unsigned long long s_k[2];  // the unit taken, alternating slots (one barrier per unit)
   if (threadIdx.x == 0) s_k[0] = atomicAdd(qp, 1ull);
   __syncthreads();
+#if BM_LAG_PRIO
+  unsigned long long kprev = s_k[0];
+#endif
   uint64_t unit = bm_block_of(it, s_k[0]);
   if (unit >= nunit) return 0;
   if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it.start + unit * (BM_GRAB * BM_BLOCK))
@@ -177,6 +183,19 @@ __device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const 
     const uint64_t seen = __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (threadIdx.x == 0) s_k[slot] = kn;
     __syncthreads();
+#if BM_LAG_PRIO
+    {
+      // A workgroup that fell behind -- more of the queue's units taken by the item's workgroups
+      // during its last unit than 5/4 of their count -- issues first for its next unit.  The SIMD
+      // arbiter otherwise favours older waves, and a starved workgroup holding the unit with the
+      // answer delays the answer by its whole unit time (the long tail of C1 calls).
+      const unsigned long long kr = s_k[slot];
+      const uint32_t taken = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(kr - kprev));
+      kprev = kr;
+      if (taken > it.nwg + (it.nwg >> 2)) __builtin_amdgcn_s_setprio(2);
+      else __builtin_amdgcn_s_setprio(0);
+    }
+#endif
     const uint64_t nu = bm_block_of(it, s_k[slot]);
     // a unit taken and not hashed lies past the window or above a hit: no nonce below the answer
     // is skipped

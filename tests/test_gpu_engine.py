@@ -8,7 +8,7 @@
 * The steppers run at SCHED_IDLE, as the reference's PoW threads (src/bitmsghash/bitmsghash.cpp:149),
   and sleep while the GPU works (bmpow_get_thread_info).
 * The single-object path: exact at the edges of a bounded call, with the hit log overflowing, and
-  one launch's lookahead behind another call.
+  one call's queued next window behind another call.
 Answers are proven exact with the min-trial probe and, on samples, the C oracle.
 """
 import ctypes
@@ -120,18 +120,24 @@ def test_single_object_path_edges(gpulib, coracle):
     assert gpulib.bmpow_search(ih, U64 // 40000, 1, want_n - 1, ctypes.byref(n), ctypes.byref(t)) == _lib.NOT_FOUND
     assert gpulib.bmpow_search(ih, U64 // 40000, want_n, 5, ctypes.byref(n), ctypes.byref(t)) == _lib.FOUND
     assert (t.value, n.value) == (want_t, want_n)
-    # many short calls back to back (each leaves its lookahead window queued behind it)
+    # many short calls back to back; with 2^20-trial windows and E = 2^18 .. 2^19 the next window is
+    # queued behind the first (fewer than 8 E nonces in flight), so most calls return with it still
+    # queued and the next call's launches run behind it
     rng = random.Random(9)
-    for _ in range(40):
-        x = rng.randbytes(64)
-        tg = U64 // rng.choice([10, 700, 30000])
-        assert proofofwork.run(tg, x) == list(coracle.search(x, tg))
+    gpulib.bmpow_set_step_trials(1 << 20)
+    try:
+        for i in range(40):
+            x = rng.randbytes(64)
+            tg = U64 // rng.choice([10, 700, 30000] if i % 2 else [1 << 18, 1 << 19])
+            assert proofofwork.run(tg, x) == list(coracle.search(x, tg))
+    finally:
+        gpulib.bmpow_set_step_trials(0)
 
 
 def test_single_object_golden_c1(gpulib, golden):
     """The golden C1 object (nonce 10,909,138) through run() on one shard (the single-object path):
-    the answer, and the trials hashed within a few block rows of it (the lookahead window queued
-    behind the first stops at its first block)."""
+    the answer, and the trials hashed within a few block rows of it (one launch: with E ~ 1.3e7 no
+    window is queued behind the first 2^29)."""
     k = [k for k in golden('first_nonce_kats.json')['kats'] if k['nonce'] == 10909138][0]
     ih = bytes.fromhex(k['ih'])
     gpulib.bmpow_reset_stats()

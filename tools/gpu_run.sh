@@ -9,6 +9,9 @@
 #   bench            default bench line (C2, 20 steps, CPU baseline legs)
 #   bench-quick      C2, 3 steps, no CPU baseline
 #   c1 | c3 | c4 | c5 | verify | addrgen      bench.py --config X (short runs, no CPU baseline)
+#   c1-trace         rocprofv3 kernel + HIP API trace of 50 C1 calls -> tools/c1_timeline.py
+#   c5-full | c5-full-service   C5: 100,000 objects at default difficulty as one batch / through PowService
+#                    (~6 min each; a seeded 1,000 of the answers proven minimal)
 #   rocprof-bench    rocprofv3 --kernel-trace --stats over the default bench (3 steps)
 #   pmc              tools/profile_pmc.sh OUT/pmc (C3 2^33, one counter group per pass)
 #   pmc:V            the same with the variant build variants/<name> (OUT/pmc_<name>)
@@ -56,10 +59,16 @@ for step in "$@"; do
     c3) timeout -k 10 200 python3 bench.py --config c3 --c3-log2 36 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/c3.json" 2> "$OUT/c3.err" ;;
     c4) timeout -k 10 300 python3 bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/c4.json" 2> "$OUT/c4.err" ;;
     c5) timeout -k 10 300 python3 bench.py --config c5 --objects 4096 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/c5.json" 2> "$OUT/c5.err" ;;
+    c5-full) timeout -k 10 700 python3 bench.py --config c5 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/c5_full_default.json" 2> "$OUT/c5_full_default.err" ;;
+    c5-full-service) timeout -k 10 700 python3 bench.py --config c5 --service --objects 100000 --steps 1 --warmup 0 --no-cpu-baseline \
+                       > "$OUT/c5_full_default_service.json" 2> "$OUT/c5_full_default_service.err" ;;
     verify) timeout -k 10 300 python3 bench.py --config verify --no-cpu-baseline > "$OUT/verify.json" 2> "$OUT/verify.err" ;;
     addrgen) timeout -k 10 300 python3 bench.py --config addrgen --no-cpu-baseline > "$OUT/addrgen.json" 2> "$OUT/addrgen.err" ;;
     rocprof-bench) timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/rocprof" -o run -- \
                      python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/rocprof_bench.json" 2> "$OUT/rocprof_bench.err" ;;
+    c1-trace) timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --output-format csv -d "$OUT/c1_trace" -o run -- \
+                python3 bench.py --config c1 --steps 50 --warmup 3 --no-cpu-baseline > "$OUT/c1_trace.json" 2> "$OUT/c1_trace.err" &&
+              python3 tools/c1_timeline.py "$OUT/c1_trace" > "$OUT/c1_timeline.json" ;;
     pmc) bash tools/profile_pmc.sh "$OUT/pmc" 33 > "$OUT/pmc.log" 2>&1 ;;
     pmc:*) v=${step#pmc:}; BMPOW_LIB=$v/libbmpow_hip.so bash tools/profile_pmc.sh "$OUT/pmc_$(basename "$v")" 33 \
              > "$OUT/pmc_$(basename "$v").log" 2>&1 ;;

@@ -20,12 +20,14 @@ pass() {
   timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d "$OUT/$name" -o run -- "${CMD[@]}" \
     > "$OUT/$name.bench.json" 2> "$OUT/$name.err"
 }
-pass instr SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM GRBM_GUI_ACTIVE
-pass issue SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_INST_ANY \
-  SQ_WAIT_ANY GRBM_GUI_ACTIVE
-pass valu SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE
-pass fetch FETCH_SIZE
-pass write WRITE_SIZE
-timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- "${CMD[@]}" \
-  > "$OUT/kt.bench.json" 2> "$OUT/kt.err"
+# PASSES: a subset of "instr issue valu fetch write kt" (default: all)
+want() { [ -z "${PASSES:-}" ] || [[ " $PASSES " == *" $1 "* ]]; }
+if want instr; then pass instr SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM GRBM_GUI_ACTIVE; fi
+if want issue; then pass issue SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VALU2 SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_WAVE_CYCLES \
+  SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE; fi
+if want valu; then pass valu SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_INT64 SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE; fi
+if want fetch; then pass fetch FETCH_SIZE; fi
+if want write; then pass write WRITE_SIZE; fi
+if want kt; then timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- "${CMD[@]}" \
+  > "$OUT/kt.bench.json" 2> "$OUT/kt.err"; fi
 echo "pmc passes done: $OUT"
