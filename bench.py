@@ -468,7 +468,10 @@ def run_c1_bench(args, dist):
             'objects': args.steps, 'useful': float(nonce) * args.steps, 'elapsed': elapsed, 'stats': st,
             'host_cpu': host_cpu, 'call_ms': round(elapsed * 1e3 / args.steps, 4),
             'per_call': {'ms': dist(per_ms, 4), 'trials': dist(per_trials, 0),
-                         'past_answer_frac': dist([(x - nonce) / x for x in per_trials], 5)},
+                         'past_answer_frac': dist([(x - nonce) / x for x in per_trials], 5),
+                         'calls_by_past_answer': {k: sum(1 for x in per_trials if lo <= (x - nonce) / x < hi)
+                                                  for k, lo, hi in (('<1%', -1, 0.01), ('1-5%', 0.01, 0.05),
+                                                                    ('5-20%', 0.05, 0.2), ('>=20%', 0.2, 2))}},
             'path': 'single-object (bm_search1_kernel)' if single_object_path(args) else 'engine (bm_search_kernel)',
             'kernel': 'bm_search1_kernel' if single_object_path(args) else 'bm_search_kernel'}
 

@@ -907,7 +907,7 @@ int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
   const uint64_t call = ++g_one.call;  // every call launches at least once (it resets call + 2's state)
   a.call = g_one.d_calls + call % BM_ONE_CALLS;
   a.reset = g_one.d_calls + (call + 2) % BM_ONE_CALLS;
-  const uint64_t step = g_step_trials.load();
+  const uint64_t step = std::min<uint64_t>(g_step_trials.load(), BM_ONE_MAX_WINDOW);  // bm_one_ctr.acc's field
   const uint64_t bpw = bmsched::kBlocksPerWorker;
   uint64_t next = start;
   bool top = false;
@@ -931,7 +931,8 @@ int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
     const uint64_t nblk = count / BM_BLOCK + (count % BM_BLOCK ? 1 : 0);
     a.start = next;
     a.count = count;
-    a.nwg = (uint32_t)std::min<uint64_t>(g_resident, std::max<uint64_t>(1, (nblk + bpw - 1) / bpw));
+    a.nwg = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(g_resident, BM_ONE_MAX_WG),
+                                         std::max<uint64_t>(1, (nblk + bpw - 1) / bpw));
     a.seq = ++g_one.seq;
     const uint32_t r = (uint32_t)(a.seq % BM_ONE_RING);
     a.ctr = g_one.d_ctr + r;

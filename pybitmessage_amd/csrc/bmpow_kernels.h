@@ -40,7 +40,7 @@ __device__ __forceinline__ void bm_publish(unsigned long long* bestp, unsigned l
 // published into the device's own running minimum (atomicMin on best[obj]), which every column already
 // reads once per block from L2.  A value it folds in is a real hit of the window: the columns above it
 // stop, and the found[] flag stays the device's own, so the step's results are unchanged.  Exit: every
-// column wave has finished (cols_done, counted by each wave of the column workgroups as it ends), or
+// column wave has finished (cols_done, counted by each wave of the column workgroups as it leaves), or
 // 2^24 polls.
 __device__ __forceinline__ void bm_relay(const bm_item* __restrict__ items, uint32_t nitems,
                                          unsigned long long* __restrict__ best, unsigned long long* xb,
@@ -61,6 +61,46 @@ __device__ __forceinline__ void bm_relay(const bm_item* __restrict__ items, uint
     }
     __builtin_amdgcn_s_sleep(4);
   }
+}
+
+// A workgroup's totals at the end of its sweep (the single-object kernel).  Its waves leave at
+// different blocks (a wave that saw a hit stops while a sibling may go on for a block), so they cannot
+// meet at a barrier: each wave adds its counts to the workgroup's LDS fold as it leaves, and the last
+// one to leave carries the workgroup's totals -- one device atomic per workgroup at the end of a launch
+// instead of two per wave.  A C1 launch lasts 1.7 ms and drains in ~20 us, into which 8,192 atomics on
+// two addresses (~100 us at 83 M atomics/s) would not fit: the kernel's C1 span fell from 1.775 to
+// 1.70 ms with the fold (profiles/r04/eng7/).
+struct bm_fold {
+  uint32_t done;  // trials hashed
+  uint32_t cut;   // lanes whose block skipped its second compression
+  uint32_t hits;  // waves that published a hit
+  uint32_t left;  // waves that have left
+};
+__device__ __forceinline__ bm_fold& bm_fold_lds() {
+  __shared__ bm_fold f;
+  return f;
+}
+// Thread 0, before the sweep's first barrier.
+__device__ __forceinline__ void bm_fold_init() {
+  bm_fold& f = bm_fold_lds();
+  f.done = 0;
+  f.cut = 0;
+  f.hits = 0;
+  f.left = 0;
+}
+// Lane 0 of each wave as it leaves; true in the workgroup's last wave, with the totals in tot.
+__device__ __forceinline__ bool bm_fold_leave(uint32_t done, uint32_t cut, uint32_t hit, bm_fold& tot) {
+  bm_fold& f = bm_fold_lds();
+  if (done) __hip_atomic_fetch_add(&f.done, done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (cut) __hip_atomic_fetch_add(&f.cut, cut, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  if (hit) __hip_atomic_fetch_add(&f.hits, hit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  // acq_rel: the last wave sees the others' counts (and their hits' memory effects at workgroup scope)
+  if (__hip_atomic_fetch_add(&f.left, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_WORKGROUP) != BM_BLOCK / 64 - 1)
+    return false;
+  tot.done = __hip_atomic_load(&f.done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  tot.cut = __hip_atomic_load(&f.cut, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  tot.hits = __hip_atomic_load(&f.hits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return true;
 }
 
 // The block queue of a work item (round 3).  A static column layout (column c hashing blocks c,

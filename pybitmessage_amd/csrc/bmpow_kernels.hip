@@ -46,42 +46,57 @@ using namespace bm;
 #ifndef BM_SEARCH_WAVES
 #define BM_SEARCH_WAVES 4
 #endif
-#ifndef BM_LAG_PRIO  // issue priority for workgroups behind the queue (sweep); 0 for A/B builds
-#define BM_LAG_PRIO 1
+#ifndef BM_PAD
+#define BM_PAD 0
 #endif
-#ifndef BM_CUT  // the single-object kernel's mid-trial bound check (sweep's kCut); 0 for A/B builds
+#ifndef BM_LOG_RELEASE
+#define BM_LOG_RELEASE 0
+#endif
+#ifndef BM_LAG_PRIO  // A/B knob: issue priority for workgroups behind the queue (sweep)
+#define BM_LAG_PRIO 0
+#endif
+#ifndef BM_CUT  // the single-object kernel's mid-trial bound check (sweep's kOne); 0 for A/B builds
 #define BM_CUT 1
 #endif
 // One workgroup's sweep of a work item: it takes the item's blocks from the item's queue (bm_block_of),
 // in order, until the window ends or the next block lies above the running minimum.
 // kX: the launch holds items with a cross-shard bound slot, whose hits are published there.
 // log (the single-object kernel): each hit's trial value is logged, so the result needs no re-hash.
-// kCut (the single-object kernel): the running minimum is read again between a block's two
-// compressions; a block that starts above it skips its second (every nonce of it lies above a hit),
-// so a wave stops half a trial sooner after the answer is published.  Such lanes are counted in *cut,
-// not in the trials hashed.
-// Returns the trials this wave hashed (its own lanes: every wave counts itself, whichever of the
-// workgroup's waves leaves first).
-template <bool kX, bool kCut = false>
-__device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const uint64_t* __restrict__ wsrc,
+// kOne (the single-object kernel): the running minimum is read again between a block's two
+// compressions (BM_CUT); a block that starts above it skips its second (every nonce of it lies above
+// a hit), so a wave stops half a trial sooner after the answer is published.  Such lanes are counted
+// in cut, not in the trials hashed.  The kernel folds its waves' counts per workgroup (bm_fold_leave).
+// Returns this wave's own counts (every wave counts itself, whichever of the workgroup's waves leaves
+// first).
+struct bm_swept {
+  uint32_t done;  // trials hashed by this wave's lanes
+  uint32_t cut;   // lanes whose block skipped its second compression
+  uint32_t hit;   // 1: this wave published a hit
+};
+template <bool kX, bool kOne = false>
+__device__ __forceinline__ bm_swept sweep(const bm_item& it, uint32_t qi, const uint64_t* __restrict__ wsrc,
                                           uint64_t target, unsigned long long* __restrict__ bestp,
                                           uint32_t* __restrict__ foundp, unsigned long long* __restrict__ queue,
                                           unsigned long long* __restrict__ xb, uint32_t xrows,
-                                          bm_one_call* __restrict__ log, uint32_t* cut = nullptr) {
+                                          bm_one_call* __restrict__ log) {
   const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;  // blocks of the window
   // the queue hands out units of BM_GRAB blocks (1 by default; larger is an A/B knob)
   const uint64_t nunit = (nblk + BM_GRAB - 1) / BM_GRAB;
   unsigned long long* qp = queue + qi;
   __shared__ unsigned long long s_k[2];  // the unit taken, alternating slots (one barrier per unit)
-  if (threadIdx.x == 0) s_k[0] = atomicAdd(qp, 1ull);
+  if (threadIdx.x == 0) {
+    s_k[0] = atomicAdd(qp, 1ull);
+    if constexpr (kOne) bm_fold_init();
+  }
   __syncthreads();
+  bm_swept r = {0, 0, 0};
 #if BM_LAG_PRIO
   unsigned long long kprev = s_k[0];
 #endif
   uint64_t unit = bm_block_of(it, s_k[0]);
-  if (unit >= nunit) return 0;
+  if (unit >= nunit) return r;
   if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < it.start + unit * (BM_GRAB * BM_BLOCK))
-    return 0;
+    return r;
 
 #ifdef BM_PRIO_MOD
   if (blockIdx.x % BM_PRIO_MOD == 0) __builtin_amdgcn_s_setprio(2);  // A/B knob: a share of the waves issue first
@@ -98,7 +113,11 @@ __device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const 
 #endif
   }
 
-  uint32_t done = 0;
+#if BM_PAD > 0  // A/B knob: shifts the hot loop's code address by 4 B per s_nop (instruction-fetch alignment)
+#define BM_PAD_STR2(n) #n
+#define BM_PAD_STR(n) BM_PAD_STR2(n)
+  asm volatile(".rept " BM_PAD_STR(BM_PAD) "\n s_nop 0\n .endr" ::: "memory");
+#endif
   for (uint32_t slot = 1;; slot ^= 1) {
     // the next unit, taken while this one is hashed (its latency hides behind ~6,200 VALU
     // instructions per block)
@@ -121,15 +140,13 @@ __device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const 
       const uint64_t tv = ((threadIdx.x >> 6) & 1) ? trial_of_b(ihw, nonce) : trial_of(ihw, nonce);
 #else
       uint64_t tv;
-      if constexpr (kCut) {
-        uint64_t st[8];
-        trial_first(ihw, nonce, st);
-        if (__hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < first) {
-          *cut += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(live));
+      if constexpr (kOne && BM_CUT) {
+        bool c = false;
+        tv = trial_of_cut(
+            ihw, nonce, [&] { return __hip_atomic_load(bestp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < first; }, c);
+        if (c) {
+          r.cut += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(live));
           live = false;
-          tv = ~0ULL;
-        } else {
-          tv = trial_second(st);
         }
       } else {
         tv = trial_of(ihw, nonce);
@@ -142,6 +159,7 @@ __device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const 
       // difficulty 5.816-5.837 against 5.761-5.835.
       const uint64_t hits = __builtin_amdgcn_ballot_w64(live && tv <= target);
       if (hits) {
+        r.hit = 1;
         const uint32_t lane = (uint32_t)__builtin_ctzll(hits);
         const uint64_t wmin = first + (threadIdx.x & ~63u) + lane;
         uint64_t wtv = 0;
@@ -154,14 +172,20 @@ __device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const 
           if (log) {
             const uint32_t k = atomicAdd(&log->nhits, 1u);
             if (k < BM_ONE_LOG) {
+              // plain stores: the workgroup's fold and its release at the end carry them to the
+              // launch's last workgroup (bm_search1_kernel)
               log->hit_trial[k] = wtv;
+#if BM_LOG_RELEASE  // A/B knob: a release per logged hit
               __hip_atomic_store(&log->hit_nonce[k], (unsigned long long)wmin, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+#else
+              __hip_atomic_store(&log->hit_nonce[k], (unsigned long long)wmin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
             }
           }
           if (kX && it.xslot != BM_NO_XSLOT) bm_publish(bestp, xb, it.xslot, xrows, prev < wmin ? prev : wmin);
         }
       }
-      done += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(live));
+      r.done += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(live));
     }
     // Early exit: the running minimum (for a shared object also the other shards' hits, folded in by
     // the launch's relay) is tested against the next unit.  It is read after the hash, so a hit
@@ -202,7 +226,7 @@ __device__ __forceinline__ uint32_t sweep(const bm_item& it, uint32_t qi, const 
     if (nu >= nunit || seen < it.start + nu * (BM_GRAB * BM_BLOCK)) break;
     unit = nu;
   }
-  return done;
+  return r;
 }
 
 // One workgroup of a batch launch: the item holding workgroup b (the largest item index with
@@ -220,14 +244,21 @@ __device__ __forceinline__ void search_column(const bm_obj* __restrict__ objs, c
   }
   const bm_item it = items[lo];
   const bm_obj* o = objs + it.obj;
-  const uint32_t done = sweep<kX>(it, lo, o->w, o->target, best + it.obj, found + it.obj, queue, xb, xrows, nullptr);
-  if ((threadIdx.x & 63) == 0 && done) atomicAdd(trials_done, (unsigned long long)done);
+  const bm_swept r = sweep<kX>(it, lo, o->w, o->target, best + it.obj, found + it.obj, queue, xb, xrows, nullptr);
+  // Each wave adds its own count: no workgroup fold here.  The fold of the single-object kernel,
+  // though it runs only as the waves leave, cut this kernel's VALU dual issue from 6.1 % to 1.6 % of
+  // its instructions and its rate by 4.7 % (PMC, same box: profiles/r04/eng9/) -- a launch-long effect
+  // of a change outside the loop, measured, not understood -- while 4,096 atomics at the end of an
+  // 80 ms launch cost it ~0.06 %.
+  if ((threadIdx.x & 63) == 0) {
+    if (r.done) atomicAdd(trials_done, (unsigned long long)r.done);
+    if (kX) atomicAdd(trials_done + 1, 1ull);  // a column wave has finished (bm_relay)
+  }
 }
 
 // kX = false: every launch without shared objects -- the hot loop carries nothing of the
 // cross-shard bound.  kX = true: workgroup 0 is the relay (bm_relay), columns are workgroups 1..,
-// and each of their waves counts itself in trials_done[1] as it ends (waves of one workgroup may
-// leave at different blocks, so no barrier after the sweep).
+// and each of their waves counts itself in trials_done[1] as it leaves (search_column).
 template <bool kX>
 __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(const bm_obj* __restrict__ objs,
                                                              const bm_item* __restrict__ items,
@@ -244,7 +275,6 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search_kernel(co
       return;
     }
     search_column<true>(objs, items, nitems, best, found, trials_done, queue, xb, xrows, blockIdx.x - 1);
-    if ((threadIdx.x & 63) == 0) atomicAdd(trials_done + 1, 1ull);
   } else {
     search_column<false>(objs, items, nitems, best, found, trials_done, queue, nullptr, 0, blockIdx.x);
   }
@@ -270,14 +300,14 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search1_kernel(c
   uint64_t w[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) w[i] = a.w[i];
-  if (threadIdx.x == 0) {
-    if (blockIdx.x == 0) {  // the call two ahead starts from "no hit" (no launch in flight uses it)
-      bm_one_call* const r = a.reset;
-      r->best = ~0ULL;
-      r->found = 0;
-      r->nhits = 0;
-    }
-    atomicCAS(&ctr->t0, 0ull, (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    // the call two ahead starts from "no hit" (no launch in flight uses it)
+    bm_one_call* const r = a.reset;
+    r->best = ~0ULL;
+    r->found = 0;
+    r->nhits = 0;
+    __hip_atomic_store(&ctr->t0, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
   bm_item it;
   it.start = a.start;
@@ -289,43 +319,46 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search1_kernel(c
   it.nwg = a.nwg;
   it.xslot = BM_NO_XSLOT;
   it.pad = 0;
-  uint32_t cut = 0;
-  const uint32_t done = sweep<false, BM_CUT>(it, 0, w, a.target, &call->best, &call->found, &ctr->queue, nullptr, 0,
-                                             call, &cut);
+  const bm_swept r = sweep<false, true>(it, 0, w, a.target, &call->best, &call->found, &ctr->queue, nullptr, 0, call);
   if ((threadIdx.x & 63) != 0) return;
-  if (done) atomicAdd(&ctr->trials, (unsigned long long)done);
-  if (cut) atomicAdd(&ctr->cut, cut);
-  const uint32_t waves = a.nwg * (BM_BLOCK / 64);
-  if (__hip_atomic_fetch_add(&ctr->waves_done, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) != waves - 1) return;
-  // the last wave (lane 0): every other wave's hits and counts are visible (acq_rel above)
+  bm_fold tot;
+  if (!bm_fold_leave(r.done, r.cut, r.hit, tot)) return;
+  // one device atomic per workgroup (bm_one_ctr.acc: trials << 31 | cut << 12 | workgroups); a release
+  // only from a workgroup whose waves published hits, so the last workgroup's acquire sees them all
+  const uint64_t add = ((uint64_t)tot.done << 31) | ((uint64_t)tot.cut << 12) | 1u;
+  uint64_t old;
+  if (tot.hits) old = __hip_atomic_fetch_add(&ctr->acc, add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  else old = __hip_atomic_fetch_add(&ctr->acc, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if ((old & 0xfffu) != a.nwg - 1) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  // the last workgroup's last wave (lane 0): every workgroup's counts and hits are in
+  const uint64_t acc = old + add;
   const uint64_t best = __hip_atomic_load(&call->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t found = __hip_atomic_load(&call->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t nh = __hip_atomic_load(&call->nhits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   uint64_t trial = 0;
   bool have = false;
   for (uint32_t k = 0; found && k < nh && k < BM_ONE_LOG && !have; ++k)
-    if (__hip_atomic_load(&call->hit_nonce[k], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == best) {
+    if (__hip_atomic_load(&call->hit_nonce[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == best) {
       trial = call->hit_trial[k];
       have = true;
     }
   if (found && !have) trial = trial_one(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], best);  // log overflowed
   bm_one_out* const o = a.out;
-  const uint64_t t0 = __hip_atomic_load(&ctr->t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint64_t tr = __hip_atomic_load(&ctr->trials, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t nc = __hip_atomic_load(&ctr->cut, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t t1 = (uint64_t)__builtin_amdgcn_s_memrealtime();
+  uint64_t t0 = __hip_atomic_load(&ctr->t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t0 == 0 || t0 > t1) t0 = t1;  // workgroup 0 not seen yet: no span rather than a wrong one
   __hip_atomic_store(&o->nonce, best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&o->trial, trial, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&o->trials, tr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&o->trials, acc >> 31, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&o->t0, t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&o->t1, (uint64_t)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&o->t1, t1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&o->found, found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  __hip_atomic_store(&o->cut, nc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&o->cut, (uint32_t)((acc >> 12) & 0x7ffffu), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   // the launch's counters, for the launch that next uses this ring entry
   ctr->queue = 0;
-  ctr->trials = 0;
+  ctr->acc = 0;
   ctr->t0 = 0;
-  ctr->waves_done = 0;
-  ctr->cut = 0;
   __hip_atomic_store(&o->seq, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 

@@ -92,18 +92,22 @@ struct bm_one_call {
 };
 // Per launch (a ring of BM_ONE_RING; reset by the launch's last wave once it has used them).
 #define BM_ONE_RING 256
+// acc packs, per launch, the sums of every workgroup's one atomic as it finishes: trials hashed
+// (bits 31..63; a window is at most 2^32 nonces, bmpow_host.hip search_one), lanes whose block skipped
+// its second compression (bits 12..30; at most one block per wave), workgroups done (bits 0..11).
+#define BM_ONE_MAX_WINDOW (1ULL << 32)
+#define BM_ONE_MAX_WG 4095u
 struct bm_one_ctr {
-  unsigned long long queue;   // the block queue
-  unsigned long long trials;  // trials hashed (each wave adds its own)
-  unsigned long long t0;      // s_memrealtime of the first workgroup (0 = unset)
-  uint32_t waves_done;        // waves that have left the sweep
-  uint32_t cut;               // lanes whose block skipped its second compression (a hit below it)
+  unsigned long long queue;  // the block queue
+  unsigned long long acc;    // trials << 31 | cut << 12 | workgroups done
+  unsigned long long t0;     // s_memrealtime at workgroup 0's start (0 = unset)
+  unsigned long long pad;
 };
 // The launch's result, host-mapped; seq is written last (release), the host polls it.
 struct bm_one_out {
-  uint64_t nonce, trial, trials, t0, t1;  // t0, t1: s_memrealtime (100 MHz) at the first start, last exit
+  uint64_t nonce, trial, trials, t0, t1;  // t0, t1: s_memrealtime (100 MHz) at workgroup 0's start, last exit
   uint32_t found;
-  uint32_t cut;  // lanes that hashed only the first compression of their trial (bm_one_ctr.cut)
+  uint32_t cut;  // lanes that hashed only the first compression of their trial (bm_one_ctr.acc)
   uint64_t seq;
 };
 // The kernel's arguments (by value).

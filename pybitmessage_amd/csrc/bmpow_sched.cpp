@@ -134,6 +134,7 @@ void restart_slot(BatchState& b, size_t k, uint64_t st) {
   b.nfly[k] = 0;
   b.xs[k] = 0;
   b.open[k].clear();
+  b.wseq[k] = 0;
 }
 
 void grow_slots(BatchState& b, size_t n) {
@@ -150,6 +151,7 @@ void grow_slots(BatchState& b, size_t n) {
   b.nfly.resize(n, 0);
   b.xs.resize(n, 0);
   b.open.resize(n);
+  b.wseq.resize(n, 0);
 }
 
 }  // namespace
@@ -431,7 +433,13 @@ bool claimable(const BatchState& b, size_t o) {
   const std::vector<OpenWin>& w = b.open[o];
   // pieces of the latest window left to hand out, needed unless a hit lies below that window
   if (!w.empty() && w.back().claimed < w.back().P && (!b.hit[o] || w.back().start <= b.nonce[o])) return true;
-  return !b.hit[o] && !b.top[o];
+  // A new window only while it is fewer than kMaxOpen windows past the oldest open one: the running
+  // window and the one staged behind it.  Without the cap a shard with nothing of its own kept opening
+  // windows of an object whose answer another shard had found but not yet reported (its device knew
+  // the bound, so each launch ended at once): a stream of empty launches that used up the run's
+  // budget and, in the host-only unit, kept the engine's mutex from the reporting shard's SCHED_IDLE
+  // stepper for seconds (tests/native/sched_sim.cpp, scenario batches).
+  return !b.hit[o] && !b.top[o] && (w.empty() || (uint16_t)(b.wseq[o] - w.front().seq) < kMaxOpen);
 }
 
 namespace {
@@ -501,6 +509,10 @@ bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L) {
   const uint64_t chunk = (uint64_t)BM_BLOCK * iters;
   const uint64_t budget_chunks = std::max<uint64_t>(1, c.budget / chunk);
   const uint64_t k = std::max<uint64_t>(1, budget_chunks / take.size());
+  // the budget's remainder chunks, one each to the first objects: a launch claims its whole budget, so
+  // the claims stay aligned to the run's limit and no small remainder launch follows
+  const uint64_t spare = budget_chunks > k * take.size() ? budget_chunks - k * take.size() : 0;
+  size_t nth = 0;
   const uint64_t bpw = blocks_per_worker(chunk);
   // columns of a split window's piece: the shard's resident workgroups (less the relay's) over the
   // split objects, at least 4 blocks per column
@@ -532,7 +544,7 @@ bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L) {
     } else {
       const uint64_t st = b.next[o], lim = b.lim[o];
       const uint16_t P = split ? (uint16_t)S : 1;
-      uint64_t want = k * chunk;
+      uint64_t want = (k + (nth++ < spare ? 1 : 0)) * chunk;
       if (split) {
         const uint64_t cap = expect_cap(b.objs[o].target, S, chunk);
         want = std::min<uint64_t>(cap, (k * chunk > kU64Max / S) ? kU64Max : k * chunk * S);
@@ -554,7 +566,7 @@ bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L) {
       } else {
         G = std::max<uint64_t>(1, std::min<uint64_t>(share, (nblk + 4 * P - 1) / (4 * P)));
       }
-      ow.push_back(OpenWin{st, want, (uint32_t)G, P, 1, 0});
+      ow.push_back(OpenWin{st, want, (uint32_t)G, P, 1, 0, b.wseq[o]++});
       cl.start = st;
       cl.count = want;
       cl.G = (uint32_t)G;
@@ -1362,7 +1374,12 @@ int Engine::run(std::unique_lock<std::mutex>& lk, uint64_t budget, bool lookahea
     return BMPOW_E_STATE;
   }
   const uint64_t a0 = applied_;
-  const uint64_t extra = lookahead ? S_ * step_ : 0;
+  // Lookahead: with at least as many pending objects as shards, two launches per shard -- when a launch
+  // completes and run() returns, the stepper stages its next launch at once, before the caller's next
+  // call raises the limit (with one, it went on to wait for its other launch, and its device idled while
+  // the host planned: C2 ran 2^28-trial launches at 99.78 % busy, profiles/r04/); with fewer (split
+  // windows, each piece a fraction of 2E) one, since a piece claimed past the answer is waste.
+  const uint64_t extra = lookahead ? (b_->pending >= S_ ? 2 : 1) * S_ * step_ : 0;
   const bool unbounded = budget == kU64Max || a0 + budget < a0 || a0 + budget + extra < a0 + budget;
   limit_ = unbounded ? kU64Max : a0 + budget + extra;
   cv_.notify_all();

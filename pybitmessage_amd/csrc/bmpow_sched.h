@@ -59,6 +59,7 @@ struct OpenWin {
   uint64_t start, count;
   uint32_t G;                 // columns per piece
   uint16_t P, claimed, done;  // pieces: in all, handed out, applied
+  uint16_t seq;               // the object's window number (BatchState::wseq; claimable's cap)
 };
 
 // Holder of an object's in-flight windows (BatchState::holder): none, one shard (its index), or
@@ -98,6 +99,7 @@ struct BatchState {
   std::vector<uint32_t> nfly;    // the object's items in flight
   std::vector<uint8_t> xs;       // cross-shard bound slot + 1 while the object is shared, 0 none
   std::vector<std::vector<OpenWin>> open;  // windows not yet fully applied, ascending start
+  std::vector<uint16_t> wseq;    // the number the object's next window gets (wraps; only differences count)
   bool broken = false;           // a launch was lost to a device error: only reset() continues it
 };
 
@@ -245,6 +247,9 @@ struct PlanCtx {
 };
 
 // Objects a launch may take a window or a piece from.
+// A new window of an object only while it is fewer than kMaxOpen windows past the object's oldest
+// open one (claimable): the running window and the one staged behind it.
+constexpr uint16_t kMaxOpen = 2;
 bool claimable(const BatchState& b, size_t o);
 
 // Plan the next launch of shard c.s from the claimable objects (slot order):

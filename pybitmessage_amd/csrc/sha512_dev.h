@@ -291,10 +291,9 @@ BM_DEV void rounds_kw(uint64_t (&s)[8], const uint64_t* __restrict__ kw) {
   }
 }
 
-// trial(n, ih) with ih given as 8 big-endian words, in two halves: the first hash's compression
-// (trial_first, s = its 80-round state) and the second hash (trial_second).  Round 0 of each block is
-// folded: from the IV with W0 unknown, a1 = W0 + A1C and e1 = W0 + E1C.
-BM_DEV void trial_first(const uint64_t (&ihw)[8], uint64_t nonce, uint64_t (&s)[8]) {
+// trial(n, ih) with ih given as 8 big-endian words.  Round 0 of each block is folded:
+// from the IV with W0 unknown, a1 = W0 + A1C and e1 = W0 + E1C.
+BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
   uint64_t w[16];
   w[0] = nonce;
 #pragma unroll
@@ -304,18 +303,11 @@ BM_DEV void trial_first(const uint64_t (&ihw)[8], uint64_t nonce, uint64_t (&s)[
   for (int i = 10; i < 15; ++i) w[i] = 0;
   w[15] = 72 * 8;
   // state after the folded round 0 (round 1 has A = 7: a=s7 b=s0 c=s1 d=s2 e=s3 f=s4 g=s5 h=s6)
-  s[0] = IV(0);
-  s[1] = IV(1);
-  s[2] = IV(2);
-  s[3] = nonce + E1C;
-  s[4] = IV(4);
-  s[5] = IV(5);
-  s[6] = IV(6);
-  s[7] = nonce + A1C;
+  uint64_t s[8] = {IV(0), IV(1), IV(2), nonce + E1C, IV(4), IV(5), IV(6), nonce + A1C};
   rounds<1, 80, true>(s, w);
-}
-
-BM_DEV uint64_t trial_second(const uint64_t (&s)[8]) {
+#ifdef BM_TRIAL_MID
+  BM_TRIAL_MID();  // A/B hook of the search kernel (bmpow_kernels.hip), nothing elsewhere
+#endif
   // after 80 rounds A = 0: s[i] holds a..h in order
   uint64_t w2[16];
 #pragma unroll
@@ -329,13 +321,34 @@ BM_DEV uint64_t trial_second(const uint64_t (&s)[8]) {
   return s2[0] + IV(0);
 }
 
-BM_DEV uint64_t trial_of(const uint64_t (&ihw)[8], uint64_t nonce) {
-  uint64_t s[8];
-  trial_first(ihw, nonce, s);
-#ifdef BM_TRIAL_MID
-  BM_TRIAL_MID();  // A/B hook of the search kernel (bmpow_kernels.hip), nothing elsewhere
-#endif
-  return trial_second(s);
+// trial_of with a test between its two compressions: when stop() (wave-uniform) holds, the second is
+// skipped and *cut is set (the single-object kernel's mid-trial bound check, bmpow_kernels.hip sweep).
+// Kept apart from trial_of: passing the state between two halves through an array made the compiler
+// emit ~105 more VALU per trial in every caller (PMC, profiles/r04/eng6/).
+template <class Stop>
+BM_DEV uint64_t trial_of_cut(const uint64_t (&ihw)[8], uint64_t nonce, Stop&& stop, bool& cut) {
+  uint64_t w[16];
+  w[0] = nonce;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[1 + i] = ihw[i];
+  w[9] = PAD;
+#pragma unroll
+  for (int i = 10; i < 15; ++i) w[i] = 0;
+  w[15] = 72 * 8;
+  uint64_t s[8] = {IV(0), IV(1), IV(2), nonce + E1C, IV(4), IV(5), IV(6), nonce + A1C};
+  rounds<1, 80, true>(s, w);
+  cut = stop();
+  if (cut) return ~0ULL;
+  uint64_t w2[16];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w2[i] = s[i] + IV(i);
+  w2[8] = PAD;
+#pragma unroll
+  for (int i = 9; i < 15; ++i) w2[i] = 0;
+  w2[15] = 64 * 8;
+  uint64_t s2[8] = {IV(0), IV(1), IV(2), w2[0] + E1C, IV(4), IV(5), IV(6), w2[0] + A1C};
+  rounds<1, 80>(s2, w2);
+  return s2[0] + IV(0);
 }
 
 #ifdef BM_HETERO

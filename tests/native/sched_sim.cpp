@@ -412,8 +412,15 @@ static void scenario_batches() {
       for (size_t i = 0; i < c.n; ++i) CHECK(b.nfly[i] == 0 && b.holder[i] == kNoHolder, "object %zu still held", i);
       CHECK(lib.eng().stats.launches > 0, "no launch counted");
     }
-    fprintf(stderr, "batches: n=%zu S=%zu budget=%llu: %d calls, %llu launches\n", c.n, c.S,
-            (unsigned long long)c.budget, calls, (unsigned long long)lib.eng().stats.launches);
+    const double per_launch =
+        (double)lib.eng().stats.planned / (double)std::max<uint64_t>(1, lib.eng().stats.launches) / (double)c.step;
+    fprintf(stderr, "batches: n=%zu S=%zu budget=%llu: %d calls, %llu launches, %.2f steps planned per launch\n", c.n,
+            c.S, (unsigned long long)c.budget, calls, (unsigned long long)lib.eng().stats.launches, per_launch);
+    // Budgets of a step or more finish in a few calls (a shard opening windows past an answer another
+    // shard had not yet reported once made this thousands, kMaxOpen), and a launch claims its whole
+    // step (the remainder chunks are dealt out, not dropped).
+    if (c.budget == 0 || c.budget >= (1u << 16)) CHECK(calls <= 20, "n=%zu S=%zu: %d calls", c.n, c.S, calls);
+    if (c.budget == 0 && c.S == 1) CHECK(per_launch > 0.99, "n=%zu: %.2f steps per launch", c.n, per_launch);
   }
 }
 
@@ -1250,14 +1257,18 @@ static void scenario_service() {
   fprintf(stderr, "service: %zu objects from 4 producers, cancel and error recovery\n", total);
 }
 
+static const char* g_only = nullptr;  // sched_sim NAME: that scenario alone
+
 template <typename F>
 static void timed(const char* name, F f) {
+  if (g_only && std::strcmp(g_only, name) != 0) return;
   const auto t0 = std::chrono::steady_clock::now();
   f();
   fprintf(stderr, "  [%s: %.1f s]\n", name, std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
 }
 
-int main() {
+int main(int argc, char** argv) {
+  if (argc > 1) g_only = argv[1];
   init_k();
   timed("batches", scenario_batches);
   timed("var", scenario_var);
