@@ -140,9 +140,13 @@ def test_single_object_golden_c1(gpulib, golden):
     window is queued behind the first 2^29)."""
     k = [k for k in golden('first_nonce_kats.json')['kats'] if k['nonce'] == 10909138][0]
     ih = bytes.fromhex(k['ih'])
-    gpulib.bmpow_reset_stats()
-    assert proofofwork.run(k['target'], ih) == [k['trial'], k['nonce']]
-    st = _lib.BmpowStats()
-    gpulib.bmpow_get_stats(ctypes.byref(st))
-    assert k['nonce'] - 1 <= st.trials <= k['nonce'] + 4 * 1024 * 256, st.trials
-    assert st.kernel_ms > 0
+    hashed = []
+    for _ in range(5):
+        gpulib.bmpow_reset_stats()
+        assert proofofwork.run(k['target'], ih) == [k['trial'], k['nonce']]
+        st = _lib.BmpowStats()
+        gpulib.bmpow_get_stats(ctypes.byref(st))
+        assert st.trials >= k['nonce'] - 1 and st.launches == 1 and st.kernel_ms > 0, (st.trials, st.launches)
+        hashed.append(st.trials)
+    # the median call within a few block rows of the answer (a rare call runs on: test_gpu_configs)
+    assert sorted(hashed)[2] <= k['nonce'] + 4 * 1024 * 256, hashed
