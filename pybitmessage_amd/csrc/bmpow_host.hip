@@ -337,9 +337,16 @@ int select_devices(const std::vector<int>& ids) {
     void* dp = nullptr;
     HIPTRY(hipHostGetDevicePointer(&dp, g_xb, 0));
     sh.d_xb = (unsigned long long*)dp;
+    // Shards sharing a device split its resident workgroups -- over the kernels that can run at once:
+    // the device's hardware queues (GPU_MAX_HW_QUEUES, HIP's default 4) bound the streams whose
+    // kernels overlap, so 8 shards on one GPU get a quarter of it each, not an eighth (an eighth left 2
+    // waves per SIMD while 4 shards ran: 5.5 against 6.7 GH/s, profiles/r04/final/).
     const uint32_t same = (uint32_t)std::count_if(g_shards.begin(), g_shards.end(),
                                                   [&](const Shard& o) { return o.dev == sh.dev; });
-    g_resident = std::min<uint32_t>(g_resident, std::max<uint32_t>(1, sh.resident / same));
+    uint32_t hwq = 4;
+    if (const char* e = std::getenv("GPU_MAX_HW_QUEUES"))
+      if (std::atoi(e) > 0) hwq = (uint32_t)std::atoi(e);
+    g_resident = std::min<uint32_t>(g_resident, std::max<uint32_t>(1, sh.resident / std::min(same, hwq)));
   }
   make_engine();
   return (int)g_shards.size();
