@@ -46,9 +46,6 @@ using namespace bm;
 #ifndef BM_SEARCH_WAVES
 #define BM_SEARCH_WAVES 4
 #endif
-#ifndef BM_PAD
-#define BM_PAD 0
-#endif
 #ifndef BM_LOG_RELEASE
 #define BM_LOG_RELEASE 0
 #endif
@@ -113,11 +110,6 @@ __device__ __forceinline__ bm_swept sweep(const bm_item& it, uint32_t qi, const 
 #endif
   }
 
-#if BM_PAD > 0  // A/B knob: shifts the hot loop's code address by 4 B per s_nop (instruction-fetch alignment)
-#define BM_PAD_STR2(n) #n
-#define BM_PAD_STR(n) BM_PAD_STR2(n)
-  asm volatile(".rept " BM_PAD_STR(BM_PAD) "\n s_nop 0\n .endr" ::: "memory");
-#endif
   for (uint32_t slot = 1;; slot ^= 1) {
     // the next unit, taken while this one is hashed (its latency hides behind ~6,200 VALU
     // instructions per block)

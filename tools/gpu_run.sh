@@ -7,6 +7,7 @@
 #   suite-slow       pytest -m "gpu and slow" (C3 at 2^38)
 #   tests:EXPR       pytest -m gpu -k EXPR over tests/
 #   bench            default bench line (C2, 20 steps, CPU baseline legs)
+#   smoke            __graft_entry__.smoke()
 #   bench-quick      C2, 3 steps, no CPU baseline
 #   c1 | c3 | c4 | c5 | verify | addrgen      bench.py --config X (short runs, no CPU baseline)
 #   c1-trace         rocprofv3 kernel + HIP API trace of 50 C1 calls -> tools/c1_timeline.py
@@ -54,6 +55,7 @@ for step in "$@"; do
       timeout -k 10 300 python3 bench.py --config c4 --steps 1 --warmup 0 --no-cpu-baseline --devices "$n" \
         --shards-per-device "$k" "${thr[@]}" > "$OUT/c4_dev_$tag.json" 2> "$OUT/c4_dev_$tag.err" ;;
     bench) timeout -k 10 600 python3 bench.py > "$OUT/bench.json" 2> "$OUT/bench.err" ;;
+    smoke) timeout -k 10 300 python3 -c 'import __graft_entry__ as g; g.smoke()' > "$OUT/smoke.log" 2>&1 ;;
     bench-quick) timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/c2.json" 2> "$OUT/c2.err" ;;
     c1) timeout -k 10 200 python3 bench.py --config c1 --steps 20 --warmup 2 --no-cpu-baseline > "$OUT/c1.json" 2> "$OUT/c1.err" ;;
     c3) timeout -k 10 200 python3 bench.py --config c3 --c3-log2 36 --steps 1 --warmup 0 --no-cpu-baseline > "$OUT/c3.json" 2> "$OUT/c3.err" ;;
