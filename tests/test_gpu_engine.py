@@ -150,3 +150,26 @@ def test_single_object_golden_c1(gpulib, golden):
         hashed.append(st.trials)
     # the median call within a few block rows of the answer (a rare call runs on: test_gpu_configs)
     assert sorted(hashed)[2] <= k['nonce'] + 4 * 1024 * 256, hashed
+
+
+def test_no_empty_launch_stream_behind_a_slow_shard(gpulib, shards, coracle):
+    """Two shards on this device, shard 0's stepper sleeping 150 ms before each launch, a batch of easy
+    objects (E = 2^12 .. 2^16) with 2^20-trial launches: shard 1 finishes its own objects and takes
+    over shard 0's, but opens no object's window more than two past the object's oldest open one
+    (bmsched::kMaxOpen) -- before that cap it streamed thousands of launches that ended at once on a
+    bound its device already held while shard 0's report of the answer was queued.  Answers exact."""
+    shards([0, 0])
+    gpulib.bmpow_set_step_trials(1 << 20)
+    rng = random.Random(31)
+    objs = [(U64 >> rng.choice([12, 14, 16]), rng.randbytes(64)) for _ in range(40)]
+    assert gpulib.bmpow_set_shard_throttle(0, 150.0) == 0
+    try:
+        gpulib.bmpow_reset_stats()
+        res = proofofwork.run_batch(objs)
+        st = _lib.BmpowStats()
+        gpulib.bmpow_get_stats(ctypes.byref(st))
+    finally:
+        gpulib.bmpow_set_shard_throttle(0, 0.0)
+    for (t, ih), r in zip(objs, res):
+        assert tuple(r) == coracle.search(ih, t), t
+    assert st.launches < 200, st.launches
