@@ -24,6 +24,8 @@
 #   c1-one-vs-engine C1 through run(): the single-object path (spin, then block wait) vs the engine
 #   c1-dist:V        C1 through run(), 300 calls with the variant's library (default | variants/<name>):
 #                    the per-call distribution of wall time and trials past the answer
+#   c1-engine        C1 through the engine (BMPOW_ONE=0), 300 calls
+#   c1-shards:K      C1 with K shards on device 0 (the engine's split windows), 300 calls
 #   c2-wait:MODE     bench-quick with BMPOW_WAIT=MODE (sleep | block | spin | poll): the steppers' CPU
 #   devices:N:K[:T]  C3 and C4 via --devices N --shards-per-device K (throttle shard 0 by T ms)
 #   rehearse-n2 | rehearse-n8   the driver's N-rank bench command with every rank on GPU 0
@@ -46,6 +48,11 @@ for step in "$@"; do
     c1-dist:*) v=${step#c1-dist:}; if [ "$v" = default ]; then L=pybitmessage_amd/lib/libbmpow_hip.so; else L=$v/libbmpow_hip.so; fi
       BMPOW_LIB=$L timeout -k 10 200 python3 bench.py --config c1 --steps 300 --warmup 5 --no-cpu-baseline \
         > "$OUT/c1_dist_$(basename "$v").json" 2> "$OUT/c1_dist_$(basename "$v").err" ;;
+    c1-engine) BMPOW_ONE=0 timeout -k 10 200 python3 bench.py --config c1 --steps 300 --warmup 5 --no-cpu-baseline \
+        > "$OUT/c1_engine.json" 2> "$OUT/c1_engine.err" ;;
+    c1-shards:*) k=${step#c1-shards:}
+      timeout -k 10 200 python3 bench.py --config c1 --steps 300 --warmup 5 --no-cpu-baseline --devices 1 \
+        --shards-per-device "$k" > "$OUT/c1_shards_$k.json" 2> "$OUT/c1_shards_$k.err" ;;
     c2-wait:*) m=${step#c2-wait:}
       BMPOW_WAIT=$m timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/c2_wait_$m.json" 2> "$OUT/c2_wait_$m.err" ;;
     devices:*) IFS=: read -r _ n k t <<< "$step"; t=${t:-0}; tag="n${n}_k${k}_t${t}"
