@@ -113,3 +113,32 @@ def test_c2_workload_is_deterministic():
     rng = random.Random(bench.SEED)
     L = rng.randrange(512, 16385)
     assert a[0][0] == int(object_target(L, 345600))
+
+
+def test_single_rank_line_carries_the_round4_fields(monkeypatch):
+    """One rank (no process group): the C1 line names the kernel it timed, carries the per-call
+    distribution, the cut lanes and the host CPU figures; `single_object_path` follows BMPOW_ONE and
+    the shard count."""
+    monkeypatch.delenv('WORLD_SIZE', raising=False)
+    monkeypatch.delenv('RANK', raising=False)
+    d = bench.Dist()
+    assert d.world == 1
+    stats = types.SimpleNamespace(trials=11_000_000, kernel_ms=1.65, launches=1, cut_trials=40_000)
+    per_call = {'ms': {'min': 1.6, 'median': 1.67, 'p90': 1.7, 'max': 1.8}}
+    host = {'process_cpu_per_s': 0.9, 'stepper_cpu_per_s': [], 'stepper_policy': [], 'wait': 'sleep', 'what': ''}
+    r = {'desc': 'C1', 'objects': 1, 'useful': 10_909_138.0, 'elapsed': 0.0017, 'stats': stats,
+         'kernel': 'bm_search1_kernel', 'call_ms': 1.7, 'path': 'single-object', 'per_call': per_call,
+         'host_cpu': host}
+    args = types.SimpleNamespace(steps=1, warmup=0, devices=0, shards_per_device=1, throttle=None)
+    line = bench.summarize(args, d, r, 'test-lib')
+    assert line['roofline']['kernel'] == 'bm_search1_kernel'
+    assert line['per_call'] == per_call and line['call_ms'] == 1.7 and line['path'] == 'single-object'
+    assert line['cut_trials'] == 40_000
+    assert line['wasted_frac_incl_cut'] == round(1.0 - 10_909_138.0 / (11_000_000 + 20_000), 5)
+    assert line['host_cpu_per_s'] == 0.9
+    assert 'frac_vs_mix_ceiling' not in line['roofline'] and 'frac_vs_baseline_md_peak' not in line['roofline']
+    monkeypatch.setenv('BMPOW_ONE', '1')
+    assert bench.single_object_path(args)
+    assert not bench.single_object_path(types.SimpleNamespace(devices=1, shards_per_device=8))
+    monkeypatch.setenv('BMPOW_ONE', '0')
+    assert not bench.single_object_path(args)
