@@ -53,6 +53,23 @@ def test_library_exports_every_declared_symbol(rawlib):
         assert hasattr(rawlib, s), s
 
 
+def test_stats_struct_matches_the_header(tmp_path):
+    """The ctypes mirror of bmpow_stats has the C struct's size and field offsets (a field added
+    on one side only would make bmpow_get_stats write past the Python buffer)."""
+    import subprocess
+    fields = [f for f, _ in _lib.BmpowStats._fields_]
+    src = tmp_path / 'sz.c'
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "bmpow.h"\nint main(void) {\n'
+                   '  printf("%zu", sizeof(bmpow_stats));\n' +
+                   ''.join('  printf(" %%zu", offsetof(bmpow_stats, %s));\n' % f for f in fields) +
+                   '  return 0;\n}\n')
+    exe = tmp_path / 'sz'
+    subprocess.check_call(['gcc', '-I', os.path.join(ROOT, 'include'), str(src), '-o', str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).split()]
+    assert got[0] == ctypes.sizeof(_lib.BmpowStats)
+    assert got[1:] == [getattr(_lib.BmpowStats, f).offset for f in fields]
+
+
 def test_python_binding_covers_header():
     bound = sorted(n for n, _, _ in _lib.SIGNATURES)
     assert bound == declared_symbols()
