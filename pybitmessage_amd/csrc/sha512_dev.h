@@ -347,7 +347,14 @@ BM_DEV uint64_t trial_of_cut(const uint64_t (&ihw)[8], uint64_t nonce, Stop&& st
   for (int i = 9; i < 15; ++i) w2[i] = 0;
   w2[15] = 64 * 8;
   uint64_t s2[8] = {IV(0), IV(1), IV(2), w2[0] + E1C, IV(4), IV(5), IV(6), w2[0] + A1C};
+#ifdef BM_CUT2  // A/B variant: a second test halfway through the second compression
+  rounds<1, 40>(s2, w2);
+  cut = stop();
+  if (cut) return ~0ULL;
+  rounds<40, 80>(s2, w2);
+#else
   rounds<1, 80>(s2, w2);
+#endif
   return s2[0] + IV(0);
 }
 
