@@ -1051,6 +1051,14 @@ def summarize(args, dist, r, lib_version):
                     # barriers): a measured reference point, not a ceiling -- the kernel itself issues
                     # more, its per-block barrier phasing the waves better
                     line['roofline']['free_running_mix'] = dict(mix, ghs=round(ceil * mix['valu_per_simd_quadcycle'], 4))
+                    if mix.get('phased_valu_per_simd_quadcycle'):
+                        # the same multiset with every bitop3 first and the waves of a SIMD meeting at a
+                        # barrier before them: the most the mix has been measured to issue, a ceiling
+                        # for this instruction stream
+                        pg = ceil * mix['phased_valu_per_simd_quadcycle']
+                        line['roofline']['phased_mix_ceiling'] = {
+                            'valu_per_simd_quadcycle': mix['phased_valu_per_simd_quadcycle'], 'ghs': round(pg, 4),
+                            'frac': round(kernel_ghs / pg, 4), 'source': mix['source']}
     if r.get('host_cpu'):
         line['host_cpu_per_s'] = r['host_cpu']['process_cpu_per_s']
         line['host_cpu'] = r['host_cpu']
@@ -1095,7 +1103,8 @@ def free_running_mix():
     with open(path) as f:
         d = json.load(f)
     return {'valu_per_simd_quadcycle': d['ceiling_valu_per_simd_quadcycle'], 'waves_per_simd': d['waves_per_simd'],
-            'source': 'profiles/mix_ceiling.json (%s)' % d['source']}
+            'source': 'profiles/mix_ceiling.json (%s)' % d['source'],
+            'phased_valu_per_simd_quadcycle': d.get('phased_valu_per_simd_quadcycle')}
 
 
 def pmc_counters():

@@ -18,6 +18,12 @@ __launch_bounds__ does):
            as v_mov_b32);
   spread   the same multiset with the bitop3 spaced evenly among the half-rate ops;
   grouped  the same multiset with each round's bitop3 issued back to back (BM_GROUP_BITOP3's shape).
+  phased   (round 4) every bitop3 of the iteration first, then the single-issue ops, in 1,024-lane
+           workgroups (all 4 waves of a SIMD from one workgroup) that meet at a barrier each
+           iteration, so the waves sharing a SIMD run their bitop3 at the same time: what the mix
+           issues when every bitop3 finds a partner -- the all-pairs bound, measured, not argued;
+  phased_nobar  the same stream without the barrier (the waves drift apart);
+  order_bar  the compiler's order in the phased workgroups (phasing without regrouping).
 Reported: VALU instructions per SIMD per quad-cycle (IPQ) = waves x instructions / (SIMDs x cycles
 / 4), cycles from the kernel time and the s_memtime / s_memrealtime clock of block 0.
 """
@@ -153,25 +159,32 @@ def grouped(kinds, per=8):
     return out + ['B'] * held
 
 
-def kernel_src(name, lines, waves):
+def phased(kinds):
+    return ['B'] * kinds.count('B') + [k for k in kinds if k != 'B']
+
+
+def kernel_src(name, lines, waves, threads=256, barrier=False):
     regs_needed = WAVES[waves]
     clob = ', '.join('"v%d"' % i for i in range(POOL)) + ', "v%d"' % (regs_needed - 1)
     body = '\\n\\t'.join(lines)
     return '''
-__global__ __launch_bounds__(256, %(w)d) void %(name)s(uint64_t* clk, int iters) {
+__global__ __launch_bounds__(%(t)d, %(wb)d) void %(name)s(uint64_t* clk, int iters) {
   uint64_t t0 = 0, r0 = 0;
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     t0 = __builtin_amdgcn_s_memtime();
     r0 = __builtin_amdgcn_s_memrealtime();
   }
-  for (int it = 0; it < iters; ++it)
+  for (int it = 0; it < iters; ++it) {
+    %(bar)s
     asm volatile("%(body)s" ::: %(clob)s);
+  }
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     clk[0] = __builtin_amdgcn_s_memtime() - t0;
     clk[1] = __builtin_amdgcn_s_memrealtime() - r0;
   }
 }
-''' % {'w': waves, 'name': name, 'body': body, 'clob': clob}
+''' % {'t': threads, 'wb': max(1, waves * 256 // threads), 'name': name, 'body': body, 'clob': clob,
+       'bar': '__syncthreads();' if barrier else ''}
 
 
 def main():
@@ -190,12 +203,23 @@ def main():
         for w in sorted(WAVES):
             kn = 'mix_%s_w%d' % (vname, w)
             src.append(kernel_src(kn, lines, w))
-            table.append((kn, vname, w))
+            table.append((kn, vname, w, 256))
+    ph = phased(kinds)
+    assert sorted(ph) == sorted(kinds)
+    lines = emit(ph)
+    for vname, bar in (('phased', True), ('phased_nobar', False)):
+        kn = 'mix_%s_w4' % vname
+        src.append(kernel_src(kn, lines, 4, threads=1024, barrier=bar))
+        table.append((kn, vname, 4, 1024))
+    # the compiler's order in the same phased workgroups: does phasing alone help a spread-out mix?
+    kn = 'mix_order_bar_w4'
+    src.append(kernel_src(kn, emit(kinds), 4, threads=1024, barrier=True))
+    table.append((kn, 'order_bar', 4, 1024))
     src.append('''
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \\
   fprintf(stderr, "HIP error %%s at %%s:%%d\\n", hipGetErrorString(e_), __FILE__, __LINE__); return 1; } } while (0)
 typedef void (*kfn)(uint64_t*, int);
-struct Var { kfn f; const char* name; const char* variant; int waves; };
+struct Var { kfn f; const char* name; const char* variant; int waves; int threads; };
 static const Var kVars[] = {
 %s
 };
@@ -211,11 +235,11 @@ int main() {
   CHECK(hipEventCreate(&e1));
   printf("{\\"device\\": \\"%%s\\", \\"cus\\": %%d, \\"valu_per_iter\\": %%d, \\"mix\\": %s}\\n", p.gcnArchName, cus, nvalu);
   for (const Var& v : kVars) {
-    const int iters = 16, blocks = cus * v.waves * 6;  // 6 rounds of resident workgroups
+    const int iters = 16, blocks = cus * v.waves * 6 * 256 / v.threads;  // 6 rounds of resident workgroups
     for (int rep = 0; rep < 2; ++rep) {
-      hipLaunchKernelGGL(v.f, dim3(blocks), dim3(256), 0, 0, d_clk, 1);
+      hipLaunchKernelGGL(v.f, dim3(blocks), dim3(v.threads), 0, 0, d_clk, 1);
       CHECK(hipEventRecord(e0, 0));
-      hipLaunchKernelGGL(v.f, dim3(blocks), dim3(256), 0, 0, d_clk, iters);
+      hipLaunchKernelGGL(v.f, dim3(blocks), dim3(v.threads), 0, 0, d_clk, iters);
       CHECK(hipEventRecord(e1, 0));
       CHECK(hipEventSynchronize(e1));
       float ms = 0;
@@ -224,7 +248,7 @@ int main() {
       CHECK(hipMemcpy(clk, d_clk, 16, hipMemcpyDeviceToHost));
       const double ghz = clk[1] ? (double)clk[0] / (double)clk[1] * 0.1 : 0.0;  // memrealtime: 100 MHz
       const double cycles = ms * 1e-3 * ghz * 1e9;
-      const double wave_instr = (double)blocks * 4.0 * iters * nvalu;
+      const double wave_instr = (double)blocks * (v.threads / 64) * iters * nvalu;
       const double ipq = wave_instr / (simds * cycles / 4.0);
       printf("{\\"kernel\\": \\"%%s\\", \\"variant\\": \\"%%s\\", \\"waves_per_simd\\": %%d, \\"rep\\": %%d, \\"ms\\": %%.3f, "
              "\\"clock_ghz\\": %%.3f, \\"valu_per_simd_quadcycle\\": %%.4f}\\n", v.name, v.variant, v.waves, rep, ms, ghz, ipq);
@@ -233,7 +257,7 @@ int main() {
   }
   return 0;
 }
-''' % (',\n'.join('  {%s, "%s", "%s", %d}' % (kn, kn, vn, w) for kn, vn, w in table), len(kinds),
+''' % (',\n'.join('  {%s, "%s", "%s", %d, %d}' % (kn, kn, vn, w, t) for kn, vn, w, t in table), len(kinds),
        str(counts).replace("'", '\\"')))
     dst = os.path.join(HERE, 'ubench_mix.hip')
     with open(dst, 'w') as f:
