@@ -1053,10 +1053,12 @@ def summarize(args, dist, r, lib_version):
                     line['roofline']['free_running_mix'] = dict(mix, ghs=round(ceil * mix['valu_per_simd_quadcycle'], 4))
                     if mix.get('phased_valu_per_simd_quadcycle'):
                         # the same multiset with every bitop3 first and the waves of a SIMD meeting at a
-                        # barrier before them: the most the mix has been measured to issue, a ceiling
-                        # for this instruction stream
+                        # barrier before them: the most the multiset has been measured to issue.  SHA-512's
+                        # dependences fix where the bitop3 sit, and no order that keeps them issues above
+                        # 1.05 (order / spread / grouped / order_bar) -- an upper bound for the multiset,
+                        # not a target for this dataflow
                         pg = ceil * mix['phased_valu_per_simd_quadcycle']
-                        line['roofline']['phased_mix_ceiling'] = {
+                        line['roofline']['phased_mix_bound'] = {
                             'valu_per_simd_quadcycle': mix['phased_valu_per_simd_quadcycle'], 'ghs': round(pg, 4),
                             'frac': round(kernel_ghs / pg, 4), 'source': mix['source']}
     if r.get('host_cpu'):
