@@ -36,7 +36,7 @@ sys.path.insert(0, HERE)
 from isa_census import kernel_lines  # noqa: E402
 
 POOL = 48  # 32-bit registers v0..v47 take the stream's results (v48.. stay the compiler's)
-WAVES = {4: 128, 5: 96, 6: 80, 7: 72, 8: 64}  # waves/SIMD -> VGPRs that give that occupancy
+WAVES = {2: 256, 4: 128, 5: 96, 6: 80, 7: 72, 8: 64}  # waves/SIMD -> VGPRs that give that occupancy
 
 
 def loop_ops(path, name='bm_search_kernel'):
@@ -215,11 +215,24 @@ def main():
     kn = 'mix_order_bar_w4'
     src.append(kernel_src(kn, emit(kinds), 4, threads=1024, barrier=True))
     table.append((kn, 'order_bar', 4, 1024))
+    # each round's bitop3 moved to the front of its round (about 11 in a run), and two trials per lane
+    # interleaved round by round (about 22 in a run, 2 waves per SIMD at twice the registers): how much
+    # of the phased pairing survives clusters a dataflow could form
+    per = len(kinds) / 160.0
+    chunks = [kinds[int(i * per):int((i + 1) * per)] for i in range(160)]
+    roundcl = [k for c in chunks for k in (['B'] * c.count('B') + [x for x in c if x != 'B'])]
+    roundcl2 = [k for c in chunks for k in (['B'] * (2 * c.count('B')) + [x for x in c + c if x != 'B'])]
+    assert sorted(roundcl) == sorted(kinds) and len(roundcl2) == 2 * len(kinds)
+    for vname, vk, w, t in (('roundcl_bar', roundcl, 4, 1024), ('roundcl', roundcl, 4, 256),
+                            ('roundcl2_bar', roundcl2, 2, 512), ('roundcl2', roundcl2, 2, 128)):
+        kn = 'mix_%s_w%d' % (vname, w)
+        src.append(kernel_src(kn, emit(vk), w, threads=t, barrier=vname.endswith('_bar')))
+        table.append((kn, vname, w, t))
     src.append('''
 #define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \\
   fprintf(stderr, "HIP error %%s at %%s:%%d\\n", hipGetErrorString(e_), __FILE__, __LINE__); return 1; } } while (0)
 typedef void (*kfn)(uint64_t*, int);
-struct Var { kfn f; const char* name; const char* variant; int waves; int threads; };
+struct Var { kfn f; const char* name; const char* variant; int waves; int threads; int nvalu; };
 static const Var kVars[] = {
 %s
 };
@@ -248,7 +261,7 @@ int main() {
       CHECK(hipMemcpy(clk, d_clk, 16, hipMemcpyDeviceToHost));
       const double ghz = clk[1] ? (double)clk[0] / (double)clk[1] * 0.1 : 0.0;  // memrealtime: 100 MHz
       const double cycles = ms * 1e-3 * ghz * 1e9;
-      const double wave_instr = (double)blocks * (v.threads / 64) * iters * nvalu;
+      const double wave_instr = (double)blocks * (v.threads / 64) * iters * v.nvalu;
       const double ipq = wave_instr / (simds * cycles / 4.0);
       printf("{\\"kernel\\": \\"%%s\\", \\"variant\\": \\"%%s\\", \\"waves_per_simd\\": %%d, \\"rep\\": %%d, \\"ms\\": %%.3f, "
              "\\"clock_ghz\\": %%.3f, \\"valu_per_simd_quadcycle\\": %%.4f}\\n", v.name, v.variant, v.waves, rep, ms, ghz, ipq);
@@ -257,7 +270,7 @@ int main() {
   }
   return 0;
 }
-''' % (',\n'.join('  {%s, "%s", "%s", %d, %d}' % (kn, kn, vn, w, t) for kn, vn, w, t in table), len(kinds),
+''' % (',\n'.join('  {%s, "%s", "%s", %d, %d, %d}' % (kn, kn, vn, w, t, len(kinds) * (2 if '2' in vn else 1)) for kn, vn, w, t in table), len(kinds),
        str(counts).replace("'", '\\"')))
     dst = os.path.join(HERE, 'ubench_mix.hip')
     with open(dst, 'w') as f:
