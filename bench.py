@@ -132,6 +132,14 @@ class Dist(object):
         self.dist.all_reduce(t, op={'max': self.dist.ReduceOp.MAX, 'sum': self.dist.ReduceOp.SUM}[op])
         return float(t.item())
 
+    def gather(self, obj):
+        """Every rank's obj, in rank order (gloo all_gather_object; host-side, outside the timed region)."""
+        if not self.dist:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
     def store(self):
         """The process group's TCP store (host-side key/value; used for work claiming)."""
         from torch.distributed import distributed_c10d
@@ -192,9 +200,20 @@ def cpu_delta(c0, c1, elapsed):
     steppers = [round((b - a) / elapsed, 5) for a, b in zip(c0[1], c1[1])] if len(c0[1]) == len(c1[1]) else []
     return {'process_cpu_per_s': round((c1[0] - c0[0]) / elapsed, 5), 'stepper_cpu_per_s': steppers,
             'stepper_policy': sorted({names.get(p, str(p)) for p in c1[2]}),
-            'wait': os.environ.get('BMPOW_WAIT', 'sleep'),
+            'wait': {'steppers': os.environ.get('BMPOW_WAIT', 'sleep')},
             'what': 'getrusage(RUSAGE_SELF) over the timed region (every thread of this process) and each '
                     'stepper thread\'s CLOCK_THREAD_CPUTIME_ID (bmpow_get_thread_info), per wall-second'}
+
+
+def one_wait(st, elapsed):
+    """How run()'s single-object path waited (bmpow_stats.one_wait_*): wall time the calling thread spun
+    on a result word (a short call's last window) and slept between polls, per wall-second."""
+    spin, sleep = getattr(st, 'one_wait_spin_ms', 0.0), getattr(st, 'one_wait_sleep_ms', 0.0)
+    if spin + sleep <= 0:
+        return None
+    return {'mode': os.environ.get('BMPOW_WAIT1', 'auto'), 'spin_s_per_s': round(spin * 1e-3 / elapsed, 5),
+            'sleep_poll_s_per_s': round(sleep * 1e-3 / elapsed, 5),
+            'spin_share': round(spin / (spin + sleep), 5)}
 
 
 def prove_sample(lib, objs, nonce, idx, k, seed):
@@ -390,6 +409,35 @@ def run_runbatch_bench(args, dist):
             'host_cpu': host_cpu}
 
 
+def run_serial_bench(args, dist):
+    """C2/C4/C5 objects solved ONE AFTER ANOTHER through proofofwork.run -- every call site of the
+    reference is such a serial call (class_singleWorker.py:236,1276, api.py:1304,1350) -- on the
+    single-object path (pieces over the devices); the host CPU the calls take is in host_cpu."""
+    from pybitmessage_amd import _lib, proofofwork
+    per_gpu = args.objects or {'c2': 64, 'c4': 8, 'c5': 256}[args.config]
+    objs, desc = make_objects(args.config, dist.rank, per_gpu, test_mode=args.test_mode)
+    lib = _lib.get()
+    for t, ih in objs[:args.warmup]:
+        proofofwork.run(t, ih)
+    dist.barrier()
+    lib.bmpow_reset_stats()
+    c0 = cpu_snapshot(lib)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = [proofofwork.run(t, ih) for t, ih in objs]
+    dist.barrier()
+    elapsed = time.perf_counter() - t0
+    host_cpu = cpu_delta(c0, cpu_snapshot(lib), elapsed)
+    st = _lib.BmpowStats()
+    lib.bmpow_get_stats(ctypes.byref(st))
+    nonce = [n for _, n in res]
+    exact = None if args.no_exact else prove_sample(lib, objs, nonce, list(range(len(objs))), 64, SEED + dist.rank)
+    return {'desc': desc + ', one proofofwork.run call after another', 'objects': len(objs) * args.steps,
+            'useful': float(sum(nonce)) * args.steps, 'elapsed': elapsed, 'stats': st, 'host_cpu': host_cpu,
+            'exact_sample': exact, 'path': one_path_desc(args, lib), 'call_ms': round(elapsed * 1e3 / len(objs) / args.steps, 3),
+            'kernel': 'bm_search1_kernel' if single_object_path(args) else 'bm_search_kernel'}
+
+
 def run_c3_bench(args, dist):
     """C3: fixed initialHash, target 0 (no hit), 2^log2 nonces split contiguously over ranks."""
     import ctypes
@@ -420,14 +468,33 @@ def run_c3_bench(args, dist):
     lib.bmpow_get_stats(ctypes.byref(st))
     desc = 'C3: fixed initialHash, target=0, 2^%d nonces split over %d GPU(s)' % (args.c3_log2, dist.world)
     return {'desc': desc, 'objects': 0, 'useful': float(share) * args.steps, 'elapsed': elapsed, 'stats': st,
-            'scaling': 'strong', 'host_cpu': host_cpu,
+            'scaling': 'strong', 'host_cpu': host_cpu, 'path': one_path_desc(args, lib),
             'kernel': 'bm_search1_kernel' if single_object_path(args) else 'bm_search_kernel'}
 
 
 def single_object_path(args):
-    """run()/bmpow_search on one shard take the single-object kernel (bmpow_host.hip search_one)
-    unless BMPOW_ONE=0; several shards (--devices) take the engine."""
-    return os.environ.get('BMPOW_ONE') != '0' and max(1, args.devices) * args.shards_per_device == 1
+    """run()/bmpow_search take the single-object kernel (bmpow_host.hip search_one) on any number of
+    shards unless BMPOW_ONE=0 (round 5: several devices each run one interleaved piece of a window)."""
+    return os.environ.get('BMPOW_ONE') != '0'
+
+
+def run_pieces(lib):
+    """The shards carrying run()'s pieces (bmpow_get_run_pieces) and the devices they are on."""
+    ids = (ctypes.c_int * 64)()
+    n = lib.bmpow_get_run_pieces(ids, 64) if hasattr(lib, 'bmpow_get_run_pieces') else 1
+    dev = (ctypes.c_int * 64)()
+    lib.bmpow_get_devices(dev, 64)
+    return [{'shard': ids[i], 'device': dev[ids[i]]} for i in range(max(0, min(n, 64)))]
+
+
+def one_path_desc(args, lib):
+    if not single_object_path(args):
+        return 'engine (bm_search_kernel)'
+    p = run_pieces(lib)
+    if len(p) <= 1:
+        return 'single-object (bm_search1_kernel)'
+    return ('single-object split into %d pieces, one per %s (bm_search1_kernel + relay, cross-device bound)'
+            % (len(p), 'shard (forced, bmpow_set_run_split)' if args.run_split else 'device'))
 
 
 def run_c1_bench(args, dist):
@@ -472,7 +539,7 @@ def run_c1_bench(args, dist):
                          'calls_by_past_answer': {k: sum(1 for x in per_trials if lo <= (x - nonce) / x < hi)
                                                   for k, lo, hi in (('<1%', -1, 0.01), ('1-5%', 0.01, 0.05),
                                                                     ('5-20%', 0.05, 0.2), ('>=20%', 0.2, 2))}},
-            'path': 'single-object (bm_search1_kernel)' if single_object_path(args) else 'engine (bm_search_kernel)',
+            'path': one_path_desc(args, lib),
             'kernel': 'bm_search1_kernel' if single_object_path(args) else 'bm_search_kernel'}
 
 
@@ -899,6 +966,12 @@ def main():
                          'service, bmpow_service_submit/poll) instead of one batch')
     ap.add_argument('--no-exact', action='store_true',
                     help='skip the min-trial proof of a seeded sample of the answers (after the timed region)')
+    ap.add_argument('--run-split', action='store_true',
+                    help='run() legs (c1, c3, --serial): one piece per shard even where shards share a device '
+                         '(bmpow_set_run_split; the multi-device path rehearsed on one GPU)')
+    ap.add_argument('--serial', action='store_true',
+                    help='c2/c4/c5: the objects one after another through proofofwork.run (the reference\'s '
+                         'serial call sites), not as one batch')
     ap.add_argument('--throttle', default=None,
                     help='--devices A/B: "shard:ms" -- that shard\'s stepper sleeps ms before each launch')
     ap.add_argument('--cpu-baseline-worker', action='store_true', help=argparse.SUPPRESS)
@@ -920,6 +993,8 @@ def main():
     lib = _lib.get()
     if args.step_trials:
         lib.bmpow_set_step_trials(args.step_trials)
+    if args.run_split:
+        lib.bmpow_set_run_split(1)
     if args.throttle:
         shard, ms = args.throttle.split(':')
         _lib.check(lib, lib.bmpow_set_shard_throttle(int(shard), float(ms)), 'bmpow_set_shard_throttle')
@@ -948,18 +1023,36 @@ def main():
         if args.config not in ('c2', 'c5'):
             raise SystemExit('--service / --run-batch apply to c2 and c5')
         runner = run_service_bench if args.service else run_runbatch_bench
+    if args.serial:
+        if args.config not in ('c2', 'c4', 'c5'):
+            raise SystemExit('--serial applies to c2, c4 and c5')
+        runner = run_serial_bench
     if args.devices:
         n = lib.bmpow_get_devices((ctypes.c_int * 64)(), 64)
         if n != args.devices * args.shards_per_device:
             raise SystemExit('asked for %d shards, the library selected %d' % (args.devices * args.shards_per_device, n))
     r = runner(args, dist)
     r['devices'] = args.devices
+    r['pci_bus_id'] = device_pci_bus_id(lib)
     line = summarize(args, dist, r, lib.bmpow_version().decode())
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_threads or None)
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     dist.close()
+
+
+def device_pci_bus_id(lib, shard=0):
+    """PCI bus id of the device a shard runs on (bmpow_device_pci_bus_id), or None."""
+    if not hasattr(lib, 'bmpow_device_pci_bus_id'):
+        return None
+    ids = (ctypes.c_int * 64)()
+    if lib.bmpow_get_devices(ids, 64) <= shard:
+        return None
+    buf = ctypes.create_string_buffer(64)
+    if lib.bmpow_device_pci_bus_id(ids[shard], buf, 64) < 0:
+        return None
+    return buf.value.decode()
 
 
 def summarize(args, dist, r, lib_version):
@@ -1051,21 +1144,21 @@ def summarize(args, dist, r, lib_version):
                     # barriers): a measured reference point, not a ceiling -- the kernel itself issues
                     # more, its per-block barrier phasing the waves better
                     line['roofline']['free_running_mix'] = dict(mix, ghs=round(ceil * mix['valu_per_simd_quadcycle'], 4))
-                    if mix.get('phased_valu_per_simd_quadcycle'):
-                        # the same multiset with every bitop3 first and the waves of a SIMD meeting at a
-                        # barrier before them: the most the multiset has been measured to issue.  SHA-512's
-                        # dependences fix where the bitop3 sit, and no order that keeps them issues above
-                        # 1.05 (order / spread / grouped / order_bar) -- an upper bound for the multiset,
-                        # not a target for this dataflow
-                        pg = ceil * mix['phased_valu_per_simd_quadcycle']
-                        line['roofline']['phased_mix_bound'] = {
-                            'valu_per_simd_quadcycle': mix['phased_valu_per_simd_quadcycle'], 'ghs': round(pg, 4),
-                            'frac': round(kernel_ghs / pg, 4), 'source': mix['source']}
     if r.get('host_cpu'):
         line['host_cpu_per_s'] = r['host_cpu']['process_cpu_per_s']
         line['host_cpu'] = r['host_cpu']
+        w1 = one_wait(st, r['elapsed'])
+        if w1:
+            line['host_cpu']['wait']['run_calls'] = w1
     if r.get('exact_sample'):
         line['exact_sample'] = r['exact_sample']
+    if dist.world > 1:
+        # which physical GPU each rank drove, and its work: a reader can see that N distinct devices
+        # (PCI bus ids) did the job -- the one-GPU rehearsals (--share-device) show one id
+        line['per_rank'] = dist.gather({'rank': dist.rank, 'local_rank': dist.local_rank,
+                                        'device_pci_bus_id': r.get('pci_bus_id'), 'trials': int(st.trials),
+                                        'kernel_ms': round(float(kernel_ms), 3),
+                                        'elapsed_s': round(float(r['elapsed']), 4)})
     for k in ('call_ms', 'path', 'per_call'):
         if r.get(k) is not None:
             line[k] = r[k]
@@ -1105,8 +1198,16 @@ def free_running_mix():
     with open(path) as f:
         d = json.load(f)
     return {'valu_per_simd_quadcycle': d['ceiling_valu_per_simd_quadcycle'], 'waves_per_simd': d['waves_per_simd'],
-            'source': 'profiles/mix_ceiling.json (%s)' % d['source'],
-            'phased_valu_per_simd_quadcycle': d.get('phased_valu_per_simd_quadcycle')}
+            'source': 'profiles/mix_ceiling.json (%s)' % d['source']}
+
+
+def lib_md5(path):
+    import hashlib as hl
+    try:
+        with open(path, 'rb') as f:
+            return hl.md5(f.read()).hexdigest()
+    except OSError:
+        return None
 
 
 def pmc_counters():
@@ -1125,6 +1226,11 @@ def pmc_counters():
     out = {'traffic': d.get('hbm_bytes_per_launch_upper'),
            'source': 'profiles/pmc_latest.json (bm_search_kernel, C3, 2^28-trial launches)',
            'build': full.get('build'), 'trials_per_launch': full.get('raw', {}).get('trials_per_launch')}
+    # provenance: were the counters collected on the library this run loaded?
+    from pybitmessage_amd import _lib
+    md5 = lib_md5(_lib.lib_path())
+    out['benched_lib_md5'] = md5
+    out['stale'] = md5 is None or (full.get('build') or {}).get('lib_md5') != md5
     for k in ('valu_instr_per_trial', 'valu_issue_util', 'valu_instr_per_simd_quad_cycle', 'dual_issue_share',
               'simd_busy_frac', 'wave_issue_stall_share', 'wave_wait_share', 'eff_clock_ghz'):
         if d.get(k) is not None:

@@ -76,6 +76,10 @@ BMPOW_API int bmpow_set_device_count(int ndev);
 /* Copy the active shard -> device map into ids[0..cap); returns the shard count. */
 BMPOW_API int bmpow_get_devices(int *ids, int cap);
 
+/* PCI bus id ("0000:75:00.0") of device ordinal `device` into out[0..len) (NUL-terminated); 0 or < 0.
+ * Lets a multi-rank run show which physical GPU each rank drove (bench.py's per_rank). */
+BMPOW_API int bmpow_device_pci_bus_id(int device, char *out, int len);
+
 /* Per-shard search throughput the step planner weights its slices by (trials per ms, an
  * exponential average over launches of >= 2^24 trials; 0 = no sample yet) into rates[0..cap);
  * returns the shard count.  A shard's share of a multi-shard step is its rate over the mean,
@@ -114,7 +118,9 @@ BMPOW_API int bmpow_trials_len(const uint8_t *ih, size_t ih_len, const uint64_t 
                                uint64_t *trials_out);
 
 /* Bounded single-object search of [start, start + max_trials) (never past 2^64-1), nonce
- * space sharded over the active devices.  Replaces BitmessagePOW
+ * space sharded over the active devices: each window is cut into one interleaved piece per physical
+ * device (shards sharing a device never split a window; bmpow_set_run_split), the pieces sharing the
+ * running minimum through a host-pinned cross-device bound.  Replaces BitmessagePOW
  * (src/bitmsghash/bitmsghash.cpp:127-165) and do_opencl_pow (src/openclpow.py:77-111).
  * Returns BMPOW_FOUND with the exact first hit, BMPOW_NOT_FOUND, or < 0. */
 BMPOW_API int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials,
@@ -353,6 +359,10 @@ typedef struct bmpow_stats {
     /* run()'s single-object kernel: nonces whose trial stopped after the first of its two SHA-512
        compressions, the call's answer having been published below them meanwhile (not in trials) */
     uint64_t cut_trials;
+    /* run()'s single-object path: wall time the calling thread spent waiting for its launches,
+       spinning on the result word (a short call's last window) and sleeping between polls */
+    double one_wait_spin_ms;
+    double one_wait_sleep_ms;
 } bmpow_stats;
 
 BMPOW_API int bmpow_get_stats(bmpow_stats *out);
@@ -372,6 +382,14 @@ BMPOW_API int bmpow_get_thread_info(double *cpu_s, int *policy, int cap);
 /* A/B and test knob: shard `shard`'s stepper sleeps `ms` before each launch (a slow device); 0 turns
  * it off.  Returns 0 or < 0. */
 BMPOW_API int bmpow_set_shard_throttle(int shard, double ms);
+
+/* run()'s pieces (bmpow_search / bmpow_search_len): 0 (default) = one piece per physical device, the
+ * first shard of each; 1 = one piece per shard even where shards share a device -- a test and
+ * rehearsal knob (pieces on one device compete for its SIMDs).  < 0 only queries.  Returns the
+ * previous setting. */
+BMPOW_API int bmpow_set_run_split(int per_shard);
+/* The shards carrying run()'s pieces into shards[0..cap) (may be NULL); returns their count or < 0. */
+BMPOW_API int bmpow_get_run_pieces(int *shards, int cap);
 
 /* Per-shard trial budget of one step (one kernel launch), default 2^29 (~80 ms on one MI355X: the
  * interrupt granularity of a batch); set 0 to restore the default.  At least one chunk (8,192). */

@@ -54,7 +54,8 @@ class BmpowStats(ctypes.Structure):
                 ('probe_trials', ctypes.c_uint64), ('probe_kernel_ms', ctypes.c_double),
                 ('verify_host_build_ms', ctypes.c_double), ('verify_host_run_ms', ctypes.c_double),
                 ('verify_host_verdict_ms', ctypes.c_double),
-                ('cut_trials', ctypes.c_uint64)]
+                ('cut_trials', ctypes.c_uint64),
+                ('one_wait_spin_ms', ctypes.c_double), ('one_wait_sleep_ms', ctypes.c_double)]
 
 
 class BmpowAddress(ctypes.Structure):
@@ -74,6 +75,7 @@ SIGNATURES = [
     ('bmpow_set_devices', ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ('bmpow_set_device_count', ctypes.c_int, [ctypes.c_int]),
     ('bmpow_get_devices', ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ('bmpow_device_pci_bus_id', ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
     ('bmpow_get_shard_rates', ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ('bmpow_shutdown', None, []),
     ('bmpow_last_error', ctypes.c_char_p, []),
@@ -111,6 +113,8 @@ SIGNATURES = [
     ('bmpow_get_shard_stats', ctypes.c_int, [_p64, ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ('bmpow_get_thread_info', ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ('bmpow_set_shard_throttle', ctypes.c_int, [ctypes.c_int, ctypes.c_double]),
+    ('bmpow_set_run_split', ctypes.c_int, [ctypes.c_int]),
+    ('bmpow_get_run_pieces', ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ('bmpow_get_step_trials', _u64, []),
     ('bmpow_set_step_trials', None, [_u64]),
     ('bmpow_pow_values', ctypes.c_int, [ctypes.c_size_t, ctypes.c_char_p, _p64, _p64]),

@@ -71,10 +71,11 @@ int set_err(int code, const std::string& msg) {
 //   "spin": HIP's default wait (busy); "poll": query the event every 50 us.
 enum WaitMode { kWaitSleep, kWaitBlock, kWaitSpin, kWaitPoll };
 WaitMode g_wait = kWaitSleep;
-// run()'s single-object path (search_one): BMPOW_WAIT1 "spin" (default) polls the result word,
-// "block" sleeps in hipEventSynchronize on a blocking-sync event first; BMPOW_ONE=0 sends run()
-// through the engine instead (A/B).
-bool g_one_block = false;
+// run()'s single-object path (search_one): BMPOW_WAIT1 "auto" (default) spins on the result word when
+// the call's answer is due within a few ms and sleeps between polls otherwise, "spin" / "sleep" force
+// one (A/B); BMPOW_ONE=0 sends run() through the engine instead (A/B).
+enum OneWait { kOneAuto, kOneSpin, kOneSleep };
+OneWait g_one_wait = kOneAuto;
 bool g_one_enabled = true;
 
 // One of a shard's two engine launch buffers (the running launch and the one staged behind it).
@@ -359,7 +360,8 @@ int init_locked() {
              : std::strcmp(w, "poll") == 0  ? kWaitPoll
              : std::strcmp(w, "block") == 0 ? kWaitBlock
                                             : kWaitSleep;
-  if (const char* w = std::getenv("BMPOW_WAIT1")) g_one_block = std::strcmp(w, "block") == 0;
+  if (const char* w = std::getenv("BMPOW_WAIT1"))
+    g_one_wait = std::strcmp(w, "spin") == 0 ? kOneSpin : std::strcmp(w, "sleep") == 0 ? kOneSleep : kOneAuto;
   if (const char* w = std::getenv("BMPOW_ONE")) g_one_enabled = std::atoi(w) != 0;
   const auto vis = visible_gfx950();
   if (vis.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
@@ -497,9 +499,10 @@ int batch_init(std::unique_lock<std::mutex>& lk, bmpow_batch* b, size_t n, const
 
 // Write objects into slots of the devices' tables -- the record, best = UINT64_MAX, found = 0 --
 // on each shard's stream, behind whatever is in flight there (bm_slots_init_kernel reading the
-// records from pinned staging).  A launch planned before the slot got its new object and still
-// queued then reads the new record: what it finds are real hits of the new object, and its results
-// are stale (the slot's generation) anyway.
+// records from pinned staging).  Called under the engine's mutex, under which the steppers also plan
+// AND enqueue their launches, so every launch planned for the slot's previous occupant is queued
+// before this init: it hashes the old record, its results are stale by the slot's generation, and the
+// init resets best[] / found[] behind it (bmsched::Engine::stepper).
 int init_slots(bmpow_batch* b, const uint32_t* slots, size_t m) {
   if (m == 0) return 0;
   const size_t rec = m * sizeof(bm_obj), bytes = rec + m * sizeof(uint32_t);
@@ -825,156 +828,291 @@ int scratch_batch(std::unique_lock<std::mutex>& lk, size_t n, const uint8_t* ihs
 }
 
 // ---------------------------------------------------------------------------------------
-// run()'s single-object path on one shard (bm_search1_kernel, bm_one_* in bmpow_layout.h).  A serial
-// run() call -- every call site in the reference (class_singleWorker.py:236,1276, api.py:1304,1350)
-// -- needs the lowest latency per object: the object rides in the kernel arguments (no upload), each
-// window is one launch with the next window queued behind it (it stops at once on the call's hit),
-// and the launch's last wave writes the result into host-mapped memory that this thread polls (no
-// resolve kernel, no copy, no event wait, no stepper thread in between).
+// run()'s single-object path (bm_search1_kernel, bm_one_* in bmpow_layout.h).  A serial run() call --
+// every call site in the reference (class_singleWorker.py:236,1276, api.py:1304,1350) -- needs the
+// lowest latency per object: the object rides in the kernel arguments (no upload), each window is one
+// launch per piece with the next window queued behind it when it may be needed (it stops at once on
+// the call's hit), and each launch's last workgroup writes its result into host-mapped memory that this
+// thread polls (no resolve kernel, no copy, no event, no stepper thread in between).
+//
+// Pieces (round 5).  On several physical devices each window is cut into one interleaved piece per
+// device (columns [g0, g0 + nwg) of the window's gn, as the engine's split windows) and the pieces share
+// the call's running minimum through the cross-device bound (a host-pinned table, one slot per call in
+// the ring, one row per piece; bm_publish / the kernel's relay).  Shards that share a device never split
+// a window: their kernels would compete for the same SIMDs (the engine's split windows over 8 streams
+// of one MI355X ran C1 at 3.11 GH/s with 46 % of the hashed nonces past the answer, round 4), so such a
+// device gets one piece with all its resident workgroups.  bmpow_set_run_split(1) forces one piece per
+// shard (the tests' rehearsal of the multi-device path on one GPU).
 // ---------------------------------------------------------------------------------------
-constexpr int kOneEvents = 8;
 struct OnePath {
   int dev = -1;
   bm_one_call* d_calls = nullptr;
   bm_one_ctr* d_ctr = nullptr;
   bm_one_out* h_out = nullptr;  // host-mapped ring of results
   bm_one_out* d_out = nullptr;  // the device's address of h_out
-  hipEvent_t ev[kOneEvents] = {};
-  uint64_t call = 0, seq = 0;
+  unsigned long long* d_xone = nullptr;  // the cross-device table as this device maps it
+  uint64_t seq = 0;
+  double rate = 0;  // trials per ms, an exponential average over launches of >= 2^24 trials (0: none yet)
+  uint64_t trials = 0;  // since bmpow_reset_stats (bmpow_get_shard_stats)
+  double ms = 0;
 };
-OnePath g_one;
+std::vector<OnePath> g_ones;  // per shard; set up for the shards that carry pieces
+unsigned long long* g_xone = nullptr;  // the cross-device bound of split run() calls (BM_MAX_SHARDS x BM_XSLOTS)
+uint64_t g_one_call = 0;
+bool g_run_split = false;  // bmpow_set_run_split: one piece per shard even where shards share a device
+// The wait (g_one_wait): "auto" spins when the launch waited for is the last one in flight and the
+// call's answer is expected within kOneSpinMs (E over the pieces' measured rate), and otherwise sleeps
+// between polls of the result word.  The reference's PoW threads run at SCHED_IDLE
+// (bitmsghash.cpp:149) and its pool workers at nice 20 (proofofwork.py:72-87): run() happens on the
+// caller's own thread here, so it keeps its priority and instead leaves the CPU alone while the GPU
+// works, except for the last few ms of a short call.
+constexpr double kOneSpinMs = 20.0;
+// a piece's rate before it has a sample: one MI355X's bm_search1_kernel, measured
+constexpr double kOneRateGuess = 6.5e6;
 
 void free_one() {
-  if (g_one.dev < 0) return;
-  (void)hipSetDevice(g_one.dev);
-  for (hipEvent_t& e : g_one.ev) {
-    if (e) (void)hipEventSynchronize(e);
+  for (size_t s = 0; s < g_ones.size(); ++s) {
+    OnePath& op = g_ones[s];
+    if (op.dev < 0) continue;
+    (void)hipSetDevice(op.dev);
+    if (s < g_shards.size() && g_shards[s].stream) (void)hipStreamSynchronize(g_shards[s].stream);
+    if (op.d_calls) (void)hipFree(op.d_calls);
+    if (op.d_ctr) (void)hipFree(op.d_ctr);
+    if (op.h_out) (void)hipHostFree(op.h_out);
   }
-  if (g_one.d_calls) (void)hipFree(g_one.d_calls);
-  if (g_one.d_ctr) (void)hipFree(g_one.d_ctr);
-  if (g_one.h_out) (void)hipHostFree(g_one.h_out);
-  for (hipEvent_t& e : g_one.ev)
-    if (e) (void)hipEventDestroy(e);
-  g_one = OnePath();
+  g_ones.clear();
+  if (g_xone) (void)hipHostFree(g_xone);
+  g_xone = nullptr;
 }
 
-int ensure_one(const Shard& sh) {
-  if (g_one.dev == sh.dev && g_one.d_calls) return 0;
-  free_one();
+int ensure_one(size_t s) {
+  if (g_ones.size() != g_shards.size()) g_ones.resize(g_shards.size());
+  OnePath& op = g_ones[s];
+  const Shard& sh = g_shards[s];
+  if (op.dev == sh.dev && op.d_calls) return 0;
   HIPTRY(hipSetDevice(sh.dev));
-  g_one.dev = sh.dev;
+  if (!g_xone) {
+    HIPTRY(hipHostMalloc(&g_xone, sizeof(unsigned long long) * BM_MAX_SHARDS * BM_XSLOTS,
+                         hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
+    for (size_t i = 0; i < (size_t)BM_MAX_SHARDS * BM_XSLOTS; ++i) g_xone[i] = ~0ULL;
+  }
+  op = OnePath();
+  op.dev = sh.dev;
   bm_one_call init[BM_ONE_CALLS];
   std::memset(init, 0, sizeof init);
   for (bm_one_call& c : init) c.best = ~0ULL;
-  HIPTRY(hipMalloc(&g_one.d_calls, sizeof init));
-  HIPTRY(hipMemcpy(g_one.d_calls, init, sizeof init, hipMemcpyHostToDevice));
-  HIPTRY(hipMalloc(&g_one.d_ctr, BM_ONE_RING * sizeof(bm_one_ctr)));
-  HIPTRY(hipMemset(g_one.d_ctr, 0, BM_ONE_RING * sizeof(bm_one_ctr)));
-  HIPTRY(hipHostMalloc(&g_one.h_out, BM_ONE_RING * sizeof(bm_one_out), hipHostMallocMapped | hipHostMallocCoherent));
-  std::memset(g_one.h_out, 0, BM_ONE_RING * sizeof(bm_one_out));
+  HIPTRY(hipMalloc(&op.d_calls, sizeof init));
+  HIPTRY(hipMemcpy(op.d_calls, init, sizeof init, hipMemcpyHostToDevice));
+  HIPTRY(hipMalloc(&op.d_ctr, BM_ONE_RING * sizeof(bm_one_ctr)));
+  HIPTRY(hipMemset(op.d_ctr, 0, BM_ONE_RING * sizeof(bm_one_ctr)));
+  HIPTRY(hipHostMalloc(&op.h_out, BM_ONE_RING * sizeof(bm_one_out), hipHostMallocMapped | hipHostMallocCoherent));
+  std::memset(op.h_out, 0, BM_ONE_RING * sizeof(bm_one_out));
   void* dp = nullptr;
-  HIPTRY(hipHostGetDevicePointer(&dp, g_one.h_out, 0));
-  g_one.d_out = (bm_one_out*)dp;
-  for (hipEvent_t& e : g_one.ev)
-    HIPTRY(hipEventCreateWithFlags(&e, hipEventDisableTiming | (g_one_block ? hipEventBlockingSync : 0)));
+  HIPTRY(hipHostGetDevicePointer(&dp, op.h_out, 0));
+  op.d_out = (bm_one_out*)dp;
+  HIPTRY(hipHostGetDevicePointer(&dp, g_xone, 0));
+  op.d_xone = (unsigned long long*)dp;
   return 0;
 }
 
-// Wait for launch `seq`'s result word.  The event recorded behind the launch catches a launch that
-// ended without writing it (a fault) instead of spinning forever.
-int wait_one(uint64_t seq) {
-  bm_one_out* o = &g_one.h_out[seq % BM_ONE_RING];
-  hipEvent_t ev = g_one.ev[seq % kOneEvents];
-  if (g_one_block) HIPTRY(hipEventSynchronize(ev));
-  for (uint32_t spin = 1;; ++spin) {
-    if (__atomic_load_n(&o->seq, __ATOMIC_ACQUIRE) == seq) return 0;
-    if ((spin & 1023) == 0) {
-      const hipError_t e = hipEventQuery(ev);
+// The shards that carry a run()'s pieces: the first shard of every device (or every shard, forced).
+std::vector<size_t> one_pieces() {
+  std::vector<size_t> p;
+  for (size_t s = 0; s < g_shards.size(); ++s) {
+    bool dup = false;
+    for (size_t q : p) dup = dup || g_shards[q].dev == g_shards[s].dev;
+    if (!dup || g_run_split) p.push_back(s);
+  }
+  return p;
+}
+
+// Wait for launch `seq`'s result word.  spin: poll it with a pause (the answer is due within a few
+// ms); else sleep between polls for 1/64 of the time waited so far (20 us .. 250 us) -- a few
+// thousand polls per second, each a load of host memory.  The stream is queried every few polls, so
+// a launch that ended without writing its result (a fault) is caught instead of waited for forever.
+int wait_one(const Shard& sh, OnePath& op, uint64_t seq, bool spin) {
+  bm_one_out* o = &op.h_out[seq % BM_ONE_RING];
+  const double t0 = now_ms();
+  for (uint32_t k = 1;; ++k) {
+    if (__atomic_load_n(&o->seq, __ATOMIC_ACQUIRE) == seq) break;
+    if (k % (spin ? 1024u : 8u) == 0) {
+      const hipError_t e = hipStreamQuery(sh.stream);
       if (e == hipSuccess) {
-        if (__atomic_load_n(&o->seq, __ATOMIC_ACQUIRE) == seq) return 0;
+        if (__atomic_load_n(&o->seq, __ATOMIC_ACQUIRE) == seq) break;
         return set_err(BMPOW_E_HIP, "single-object launch completed without its result");
       }
       if (e != hipErrorNotReady) return set_err(BMPOW_E_HIP, std::string("single-object launch: ") + hipGetErrorString(e));
     }
-    __builtin_ia32_pause();
+    if (spin) {
+      __builtin_ia32_pause();
+    } else {
+      const double waited_us = (now_ms() - t0) * 1e3;
+      std::this_thread::sleep_for(std::chrono::microseconds((int64_t)std::min(250.0, std::max(20.0, waited_us / 64))));
+    }
   }
+  const double ms = now_ms() - t0;
+  (spin ? g_stats.one_wait_spin_ms : g_stats.one_wait_sleep_ms) += ms;
+  return 0;
 }
 
 int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials, uint64_t* nonce_out,
                uint64_t* trial_out) {
-  Shard& sh = g_shards[0];
-  int rc = ensure_one(sh);
-  if (rc < 0) return rc;
-  HIPTRY(hipSetDevice(sh.dev));
+  const std::vector<size_t> pieces = one_pieces();
+  const size_t P = pieces.size();
+  for (size_t s : pieces) {
+    const int rc = ensure_one(s);
+    if (rc < 0) return rc;
+  }
   const uint64_t end = (max_trials - 1 > kU64Max - start) ? kU64Max : start + max_trials - 1;  // last nonce
+  const uint64_t call = ++g_one_call;  // every call launches on every piece (it resets call + 2's state)
+  const uint32_t xslot = (uint32_t)(call % BM_ONE_CALLS);
+  if (P > 1) {
+    // the call's slot of every row starts at "no hit": launches still in flight belong to the previous
+    // call (each call waits for its first window on every piece), which uses another slot
+    for (size_t r = 0; r < P; ++r) __atomic_store_n(&g_xone[r * BM_XSLOTS + xslot], ~0ULL, __ATOMIC_RELAXED);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  }
+  // Columns per piece: the device's resident workgroups over the pieces sharing it (at most the
+  // hardware queues' worth run at once), less the relay's workgroup of a split call.
+  uint32_t hwq = 4;
+  if (const char* e = std::getenv("GPU_MAX_HW_QUEUES"))
+    if (std::atoi(e) > 0) hwq = (uint32_t)std::atoi(e);
+  std::vector<uint32_t> cap(P);
+  double rate = 0;
+  bool shared = false;  // pieces share a device (bmpow_set_run_split)
+  for (size_t p = 0; p < P; ++p) {
+    const Shard& sh = g_shards[pieces[p]];
+    uint32_t same = 0;
+    for (size_t q : pieces) same += g_shards[q].dev == sh.dev;
+    shared = shared || same > 1;
+    uint32_t c = sh.resident / std::min(same, hwq);
+    if (P > 1 && c > 1) --c;
+    cap[p] = std::max<uint32_t>(1, std::min<uint32_t>(c, BM_ONE_MAX_WG));
+    const OnePath& op = g_ones[pieces[p]];
+    rate += (op.rate > 0 ? op.rate : kOneRateGuess) / std::min(same, hwq);
+  }
+  // A window: one step per piece (a piece hashes ~1/P of it; bm_one_ctr.acc's trial field).  Pieces
+  // that share a device do not all run at once (its hardware queues run 4 kernels; the rest start as
+  // those finish), so a piece may sweep its whole share of a window before the piece holding the answer
+  // starts: there a window is 2E (bmsched::expect_cap), as the engine's split windows.
+  uint64_t step = std::min<uint64_t>(g_step_trials.load(), BM_ONE_MAX_WINDOW) * P;
+  if (shared) step = std::min(step, bmsched::expect_cap(target, P, BM_CHUNK));
+  const uint64_t bpw = bmsched::kBlocksPerWorker;
+  uint64_t next = start;
+  bool top = false;
+  // windows in flight, oldest first: their nonces and each piece's sequence number
+  struct Fly {
+    uint64_t n;
+    uint64_t seq[BM_MAX_SHARDS];
+  };
+  Fly fly[2];
+  int nfly = 0;
+  // The next window is queued behind the running one only while the windows in flight may well hold
+  // no hit (fewer than kAheadE x E nonces, E = 2^64 / (target + 1): P(no hit) > e^-8): a C1 object
+  // (E ~ 1.3e7 against a 2^29 window) then costs one launch per piece, and no idle lookahead launch sits
+  // in the next call's way; a hard object (C4) or a sweep (C3) keeps two windows in flight.
+  constexpr double kAheadE = 8.0;
+  const double expect = 18446744073709551616.0 / ((double)target + 1.0);
+  auto want_next = [&]() {
+    double n = 0;
+    for (int i = 0; i < nfly; ++i) n += (double)fly[i].n;
+    return !top && nfly < 2 && (nfly == 0 || n < kAheadE * expect);
+  };
+  // spin only for a call whose answer is due within kOneSpinMs, and only while no window is queued
+  // behind the one waited for (then a late wake-up would cost the device nothing)
+  const bool short_call = expect / rate < kOneSpinMs;
   bm_one_args a;
   std::memset(&a, 0, sizeof a);
   for (int i = 0; i < 8; ++i) a.w[i] = bmsched::load_be64(ih + 8 * i);
   a.target = target;
-  const uint64_t call = ++g_one.call;  // every call launches at least once (it resets call + 2's state)
-  a.call = g_one.d_calls + call % BM_ONE_CALLS;
-  a.reset = g_one.d_calls + (call + 2) % BM_ONE_CALLS;
-  const uint64_t step = std::min<uint64_t>(g_step_trials.load(), BM_ONE_MAX_WINDOW);  // bm_one_ctr.acc's field
-  const uint64_t bpw = bmsched::kBlocksPerWorker;
-  uint64_t next = start;
-  bool top = false;
-  uint64_t fly[4], fly_n[4];  // sequence numbers in flight, oldest first, and their windows' nonces
-  int nfly = 0;
-  // The next window is queued behind the running one only while the windows in flight may well hold
-  // no hit (fewer than kAheadE x E nonces, E = 2^64 / (target + 1): P(no hit) > e^-8): a C1 object
-  // (E ~ 1.3e7 against a 2^29 window) then costs one launch, and no idle lookahead launch sits in the
-  // next call's way; a hard object (C4, E ~ 1.5e9) or a sweep (C3) keeps two windows in flight.
-  constexpr double kAheadE = 8.0;
-  const double expect = 18446744073709551616.0 / ((double)target + 1.0);
-  auto in_flight = [&]() {
-    double n = 0;
-    for (int i = 0; i < nfly; ++i) n += (double)fly_n[i];
-    return n;
-  };
-  auto want_next = [&]() { return !top && nfly < 2 && (nfly == 0 || in_flight() < kAheadE * expect); };
+  a.xslot = xslot;
+  a.xrows = (uint32_t)P;
+  uint32_t nwg[BM_MAX_SHARDS];
   auto launch = [&]() -> int {
     const uint64_t room = end - next;  // nonces after next, up to end
     const uint64_t count = room >= step ? step : room + 1;
     const uint64_t nblk = count / BM_BLOCK + (count % BM_BLOCK ? 1 : 0);
+    const uint64_t per = (nblk + P - 1) / P;  // blocks of a piece
+    uint32_t gn = 0;
+    for (size_t p = 0; p < P; ++p) {
+      nwg[p] = (uint32_t)std::min<uint64_t>(cap[p], std::max<uint64_t>(1, (per + bpw - 1) / bpw));
+      gn += nwg[p];
+    }
+    Fly& f = fly[nfly];
+    f.n = count;
     a.start = next;
     a.count = count;
-    a.nwg = (uint32_t)std::min<uint64_t>(std::min<uint64_t>(g_resident, BM_ONE_MAX_WG),
-                                         std::max<uint64_t>(1, (nblk + bpw - 1) / bpw));
-    a.seq = ++g_one.seq;
-    const uint32_t r = (uint32_t)(a.seq % BM_ONE_RING);
-    a.ctr = g_one.d_ctr + r;
-    a.out = g_one.d_out + r;
-    HIPTRY(bm_launch_search1(sh.stream, a));
-    HIPTRY(hipEventRecord(g_one.ev[a.seq % kOneEvents], sh.stream));
-    fly[nfly] = a.seq;
-    fly_n[nfly++] = count;
+    a.gn = gn;
+    uint32_t g0 = 0;
+    for (size_t p = 0; p < P; ++p) {
+      const Shard& sh = g_shards[pieces[p]];
+      OnePath& op = g_ones[pieces[p]];
+      a.call = op.d_calls + call % BM_ONE_CALLS;
+      a.reset = op.d_calls + (call + 2) % BM_ONE_CALLS;
+      a.nwg = nwg[p];
+      a.g0 = g0;
+      g0 += nwg[p];
+      a.xb = P > 1 ? op.d_xone : nullptr;
+      a.xrow = (uint32_t)p;
+      a.seq = ++op.seq;
+      const uint32_t r = (uint32_t)(a.seq % BM_ONE_RING);
+      a.ctr = op.d_ctr + r;
+      a.out = op.d_out + r;
+      f.seq[p] = a.seq;
+      if (P > 1) HIPTRY(hipSetDevice(sh.dev));
+      HIPTRY(bm_launch_search1(sh.stream, a));
+    }
+    ++nfly;
     if (room < step) top = true;
     else next += count;
     return 0;
   };
-  rc = launch();
+  if (P == 1) HIPTRY(hipSetDevice(g_shards[pieces[0]].dev));
+  int rc = launch();
   while (rc == 0 && want_next()) rc = launch();  // the next window, queued behind
   while (rc == 0) {
-    const uint64_t seq = fly[0];
-    rc = wait_one(seq);
+    // the oldest window: every piece's launch
+    bool found = false;
+    uint64_t best = 0, best_trial = 0;
+    double span = 0;
+    for (size_t p = 0; p < P && rc == 0; ++p) {
+      const Shard& sh = g_shards[pieces[p]];
+      OnePath& op = g_ones[pieces[p]];
+      const uint64_t seq = fly[0].seq[p];
+      const bool spin = g_one_wait == kOneSpin || (g_one_wait == kOneAuto && short_call && nfly == 1);
+      rc = wait_one(sh, op, seq, spin);
+      if (rc < 0) break;
+      const bm_one_out& o = op.h_out[seq % BM_ONE_RING];
+      const double ms = (double)(o.t1 - o.t0) * 1e-5;  // s_memrealtime: 100 MHz
+      g_stats.launches++;
+      g_stats.trials += o.trials;
+      g_stats.cut_trials += o.cut;
+      g_stats.kernel_ms += ms;
+      span = std::max(span, ms);
+      op.trials += o.trials;
+      op.ms += ms;
+      if (o.trials >= bmsched::kRateMinTrials && ms > 0)
+        op.rate = op.rate > 0 ? (1 - bmsched::kRateAlpha) * op.rate + bmsched::kRateAlpha * (double)o.trials / ms
+                              : (double)o.trials / ms;
+      // a piece's result is its device's running minimum: its own hit, or one the relay folded in (a
+      // real hit of the object too); found is its own.  The least found over the pieces is the answer:
+      // every piece hashed all of its blocks that start at or below any hit it saw, so the block holding
+      // the least hit of the window was hashed by its piece, which then holds that hit
+      if (o.found && (!found || o.nonce < best)) {
+        found = true;
+        best = o.nonce;
+        best_trial = o.trial;
+      }
+    }
     if (rc < 0) break;
-    const bm_one_out& o = g_one.h_out[seq % BM_ONE_RING];
-    g_stats.launches++;
     g_stats.steps++;
-    g_stats.trials += o.trials;
-    g_stats.cut_trials += o.cut;
-    const double ms = (double)(o.t1 - o.t0) * 1e-5;  // s_memrealtime: 100 MHz
-    g_stats.kernel_ms += ms;
-    g_stats.max_shard_kernel_ms += ms;
-    if (o.found) {  // the lowest hit: every earlier window of the call ended without one
-      *nonce_out = o.nonce;
-      *trial_out = o.trial;
+    g_stats.max_shard_kernel_ms += span;
+    if (found) {  // the lowest hit: every earlier window of the call ended without one
+      *nonce_out = best;
+      *trial_out = best_trial;
       return BMPOW_FOUND;  // a window still queued stops at its first block (the call's best)
     }
-    for (int i = 1; i < nfly; ++i) {
-      fly[i - 1] = fly[i];
-      fly_n[i - 1] = fly_n[i];
-    }
+    fly[0] = fly[1];
     --nfly;
     if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
     while (rc == 0 && want_next()) rc = launch();
@@ -1562,6 +1700,13 @@ int bmpow_get_devices(int* ids, int cap) {
   return (int)g_shards.size();
 }
 
+int bmpow_device_pci_bus_id(int device, char* out, int len) {
+  if (!out || len < 13) return set_err(BMPOW_E_ARG, "buffer too small");
+  const hipError_t e = hipDeviceGetPCIBusId(out, len, device);
+  if (e != hipSuccess) return set_err(BMPOW_E_ARG, std::string("hipDeviceGetPCIBusId: ") + hipGetErrorString(e));
+  return 0;
+}
+
 int bmpow_get_shard_rates(double* rates, int cap) {
   std::lock_guard<std::mutex> lk(g_mu);
   if (!rates && cap > 0) return set_err(BMPOW_E_ARG, "null pointer");
@@ -1655,7 +1800,9 @@ int bmpow_search_len(const uint8_t* ih, size_t ih_len, uint64_t target, uint64_t
   if (ih_len > BMPOW_MAX_IH_LEN) return set_err(BMPOW_E_ARG, "initialHash longer than BMPOW_MAX_IH_LEN");
   if (max_trials == 0) return BMPOW_NOT_FOUND;
   if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
-  if (g_shards.size() == 1 && ih_len == 64 && g_one_enabled) return search_one(ih, target, start, max_trials, nonce_out, trial_out);
+  // every 64-byte object takes the single-object path, on any number of devices (round 5; before, only
+  // one shard did and several took the engine's split windows)
+  if (ih_len == 64 && g_one_enabled) return search_one(ih, target, start, max_trials, nonce_out, trial_out);
   const uint8_t zero = 0;
   const uint64_t off[2] = {0, ih_len};
   std::unique_lock<std::mutex> lk(g_engine->mu);
@@ -2228,6 +2375,10 @@ int bmpow_get_stats(bmpow_stats* out) {
 void bmpow_reset_stats(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   g_stats = bmpow_stats{};
+  for (OnePath& op : g_ones) {
+    op.trials = 0;
+    op.ms = 0;
+  }
   if (g_engine) {
     std::lock_guard<std::mutex> el(g_engine->mu);
     bmsched::EngineStats& es = g_engine->stats;
@@ -2244,10 +2395,34 @@ int bmpow_get_shard_stats(uint64_t* trials, double* kernel_ms, int cap) {
   std::lock_guard<std::mutex> el(g_engine->mu);
   const bmsched::EngineStats& es = g_engine->stats;
   for (int i = 0; i < (int)es.shard_ms.size() && i < cap; ++i) {
-    if (trials) trials[i] = es.shard_trials[i];
-    if (kernel_ms) kernel_ms[i] = es.shard_ms[i];
+    // the engine's launches and run()'s single-object pieces on the shard
+    const bool one = i < (int)g_ones.size();
+    if (trials) trials[i] = es.shard_trials[i] + (one ? g_ones[i].trials : 0);
+    if (kernel_ms) kernel_ms[i] = es.shard_ms[i] + (one ? g_ones[i].ms : 0);
   }
   return (int)g_shards.size();
+}
+
+int bmpow_set_run_split(int per_shard) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int prev = g_run_split ? 1 : 0;
+  if (per_shard < 0) return prev;
+  if ((per_shard != 0) != g_run_split) {
+    // a shard that carries no piece misses the ring resets of the calls it sits out: start afresh
+    free_one();
+    g_run_split = per_shard != 0;
+  }
+  return prev;
+}
+
+int bmpow_get_run_pieces(int* shards, int cap) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  const int rc = init_locked();
+  if (rc < 0) return rc;
+  const std::vector<size_t> p = one_pieces();
+  for (int i = 0; i < (int)p.size() && i < cap; ++i)
+    if (shards) shards[i] = (int)p[i];
+  return (int)p.size();
 }
 
 int bmpow_get_thread_info(double* cpu_s, int* policy, int cap) {

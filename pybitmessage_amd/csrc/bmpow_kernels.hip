@@ -280,51 +280,25 @@ __device__ __noinline__ uint64_t trial_one(uint64_t w0, uint64_t w1, uint64_t w2
   return trial_of(ihw, nonce);
 }
 
-// The single-object kernel of run() (bm_one_args, bmpow_layout.h): one window, the object in the
-// arguments; the launch's last wave to leave its sweep writes the result into host-mapped memory --
-// the minimum, its trial value from the hit log (re-hashed only when the log overflowed), the trials
-// hashed and the launch's start and end on the 100 MHz realtime clock -- and then its sequence
-// number, which the host polls.  (The argument's fields are read into locals: taking the address of
-// a by-value kernel argument copies it to scratch.)
-__global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search1_kernel(const bm_one_args a) {
-  bm_one_ctr* const ctr = a.ctr;
-  bm_one_call* const call = a.call;
-  uint64_t w[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) w[i] = a.w[i];
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
-    // the call two ahead starts from "no hit" (no launch in flight uses it)
-    bm_one_call* const r = a.reset;
-    r->best = ~0ULL;
-    r->found = 0;
-    r->nhits = 0;
-    __hip_atomic_store(&ctr->t0, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  }
-  bm_item it;
-  it.start = a.start;
-  it.count = a.count;
-  it.obj = 0;
-  it.chunk_base = 0;
-  it.g0 = 0;
-  it.gn = a.nwg;
-  it.nwg = a.nwg;
-  it.xslot = BM_NO_XSLOT;
-  it.pad = 0;
-  const bm_swept r = sweep<false, true>(it, 0, w, a.target, &call->best, &call->found, &ctr->queue, nullptr, 0, call);
-  if ((threadIdx.x & 63) != 0) return;
-  bm_fold tot;
-  if (!bm_fold_leave(r.done, r.cut, r.hit, tot)) return;
-  // one device atomic per workgroup (bm_one_ctr.acc: trials << 31 | cut << 12 | workgroups); a release
-  // only from a workgroup whose waves published hits, so the last workgroup's acquire sees them all
-  const uint64_t add = ((uint64_t)tot.done << 31) | ((uint64_t)tot.cut << 12) | 1u;
-  uint64_t old;
-  if (tot.hits) old = __hip_atomic_fetch_add(&ctr->acc, add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-  else old = __hip_atomic_fetch_add(&ctr->acc, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if ((old & 0xfffu) != a.nwg - 1) return;
+// The single-object kernel of run() (bm_one_args, bmpow_layout.h): one window (or, with kX, one
+// device's piece of it), the object in the arguments; the launch's last workgroup to finish writes the
+// result into host-mapped memory -- the minimum, its trial value from the hit log (re-hashed only when
+// the log overflowed), the trials hashed and the launch's start and end on the 100 MHz realtime clock
+// -- and then its sequence number, which the host polls.  (The argument's fields are read into locals:
+// taking the address of a by-value kernel argument copies it to scratch.)
+//
+// kX (a run() split over several physical devices): workgroup 0 is the relay.  One lane polls this
+// piece's row of the cross-device table (a system-scope load every few microseconds) and folds what the
+// other devices' pieces published into this device's running minimum, which every column reads once
+// per block; it leaves once every column workgroup has counted itself in ctr->acc, adds itself, and so
+// is the launch's last workgroup -- it writes the result.  Columns publish their hits into every row
+// (bm_publish).  Every value in the table is a real hit of the object, so it only stops columns above
+// an answer.  kX = false is the one-device kernel, with none of this in its code.
+template <bool kX>
+__device__ __forceinline__ void one_result(const bm_one_args& a, bm_one_ctr* ctr, bm_one_call* call, const uint64_t (&w)[8],
+                                           uint64_t acc) {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // the last workgroup's last wave (lane 0): every workgroup's counts and hits are in
-  const uint64_t acc = old + add;
   const uint64_t best = __hip_atomic_load(&call->best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t found = __hip_atomic_load(&call->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t nh = __hip_atomic_load(&call->nhits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -335,7 +309,8 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search1_kernel(c
       trial = call->hit_trial[k];
       have = true;
     }
-  if (found && !have) trial = trial_one(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], best);  // log overflowed
+  // the log overflowed, or (kX) the minimum is another device's hit folded in by the relay
+  if (found && !have) trial = trial_one(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], best);
   bm_one_out* const o = a.out;
   const uint64_t t1 = (uint64_t)__builtin_amdgcn_s_memrealtime();
   uint64_t t0 = __hip_atomic_load(&ctr->t0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -354,6 +329,69 @@ __global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search1_kernel(c
   __hip_atomic_store(&o->seq, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+template <bool kX>
+__global__ __launch_bounds__(BM_BLOCK, BM_SEARCH_WAVES) void bm_search1_kernel(const bm_one_args a) {
+  bm_one_ctr* const ctr = a.ctr;
+  bm_one_call* const call = a.call;
+  uint64_t w[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) w[i] = a.w[i];
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    // the call two ahead starts from "no hit" (no launch in flight uses it)
+    bm_one_call* const r = a.reset;
+    r->best = ~0ULL;
+    r->found = 0;
+    r->nhits = 0;
+    __hip_atomic_store(&ctr->t0, (unsigned long long)__builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if constexpr (kX) {
+    if (blockIdx.x == 0) {
+      if (threadIdx.x != 0) return;
+      unsigned long long* const slot = a.xb + (size_t)a.xrow * BM_XSLOTS + a.xslot;
+      uint64_t seen = ~0ULL;
+      // bounded (2^26 polls, over a minute) so a lost column cannot keep the relay forever; the last
+      // column then writes the result instead
+      for (uint32_t spin = 0; spin < (1u << 26); ++spin) {
+        const uint64_t v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (v < seen) {
+          atomicMin(&call->best, (unsigned long long)v);
+          seen = v;
+        }
+        if ((__hip_atomic_load(&ctr->acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 0xfffu) >= a.nwg) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      const uint64_t old = __hip_atomic_fetch_add(&ctr->acc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((old & 0xfffu) == a.nwg) one_result<kX>(a, ctr, call, w, old + 1);
+      return;
+    }
+  }
+  bm_item it;
+  it.start = a.start;
+  it.count = a.count;
+  it.obj = 0;
+  it.chunk_base = 0;
+  it.g0 = kX ? a.g0 : 0;
+  it.gn = kX ? a.gn : a.nwg;
+  it.nwg = a.nwg;
+  it.xslot = kX ? a.xslot : BM_NO_XSLOT;
+  it.pad = 0;
+  const bm_swept r = sweep<kX, true>(it, 0, w, a.target, &call->best, &call->found, &ctr->queue, kX ? a.xb : nullptr,
+                                     kX ? a.xrows : 0, call);
+  if ((threadIdx.x & 63) != 0) return;
+  bm_fold tot;
+  if (!bm_fold_leave(r.done, r.cut, r.hit, tot)) return;
+  // one device atomic per workgroup (bm_one_ctr.acc: trials << 31 | cut << 12 | workgroups); a release
+  // only from a workgroup whose waves published hits, so the last workgroup's acquire sees them all
+  const uint64_t add = ((uint64_t)tot.done << 31) | ((uint64_t)tot.cut << 12) | 1u;
+  uint64_t old;
+  if (tot.hits) old = __hip_atomic_fetch_add(&ctr->acc, add, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  else old = __hip_atomic_fetch_add(&ctr->acc, add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the launch's workgroups: the columns, and with kX the relay
+  if ((old & 0xfffu) != a.nwg - (kX ? 0u : 1u)) return;
+  one_result<kX>(a, ctr, call, w, old + add);
+}
+
 // ---------------------------------------------------------------------------------------
 // Launch wrappers (C++ linkage, used by bmpow_host.hip).
 // ---------------------------------------------------------------------------------------
@@ -370,7 +408,10 @@ hipError_t bm_launch_search(hipStream_t st, uint32_t nwg, const bm_obj* objs, co
 }
 
 hipError_t bm_launch_search1(hipStream_t st, const bm_one_args& a) {
-  hipLaunchKernelGGL(bm_search1_kernel, dim3(a.nwg), dim3(BM_BLOCK), 0, st, a);
+  if (a.xb)
+    hipLaunchKernelGGL(bm_search1_kernel<true>, dim3(a.nwg + 1), dim3(BM_BLOCK), 0, st, a);
+  else
+    hipLaunchKernelGGL(bm_search1_kernel<false>, dim3(a.nwg), dim3(BM_BLOCK), 0, st, a);
   return hipGetLastError();
 }
 

@@ -90,13 +90,15 @@ struct bm_one_call {
   uint32_t found, nhits;
   unsigned long long hit_nonce[BM_ONE_LOG], hit_trial[BM_ONE_LOG];
 };
-// Per launch (a ring of BM_ONE_RING; reset by the launch's last wave once it has used them).
+// Per launch (a ring of BM_ONE_RING per piece; reset by the launch's last wave once it has used them).
 #define BM_ONE_RING 256
 // acc packs, per launch, the sums of every workgroup's one atomic as it finishes: trials hashed
-// (bits 31..63; a window is at most 2^32 nonces, bmpow_host.hip search_one), lanes whose block skipped
-// its second compression (bits 12..30; at most one block per wave), workgroups done (bits 0..11).
+// (bits 31..63; a piece hashes at most ~2^32 nonces of a window, bmpow_host.hip search_one), lanes
+// whose block skipped its second compression (bits 12..30: at most one block per wave, so at most
+// 2,047 x 256 = 524,032 < 2^19 with BM_ONE_MAX_WG column workgroups), workgroups done (bits 0..11,
+// the relay included).
 #define BM_ONE_MAX_WINDOW (1ULL << 32)
-#define BM_ONE_MAX_WG 4095u
+#define BM_ONE_MAX_WG 2047u
 struct bm_one_ctr {
   unsigned long long queue;  // the block queue
   unsigned long long acc;    // trials << 31 | cut << 12 | workgroups done
@@ -110,7 +112,11 @@ struct bm_one_out {
   uint32_t cut;  // lanes that hashed only the first compression of their trial (bm_one_ctr.acc)
   uint64_t seq;
 };
-// The kernel's arguments (by value).
+// The kernel's arguments (by value).  A run() on several physical devices cuts each window into P
+// interleaved pieces, one per device (piece p = columns [g0, g0 + nwg) of the window's gn, as a split
+// bm_item); the pieces share the call's running minimum through the cross-device bound: a hit is
+// stored into slot xslot of every row of the host-pinned table xb (bm_publish), and each launch's
+// workgroup 0 relays its own row into the device's running minimum (the grid is then nwg + 1).
 struct bm_one_args {
   uint64_t w[8];  // the initialHash as big-endian words (W1..W8 of block 1)
   uint64_t target, start, count;
@@ -119,7 +125,12 @@ struct bm_one_args {
   bm_one_ctr* ctr;
   bm_one_out* out;     // the device's address of the host-mapped result
   uint64_t seq;
-  uint32_t nwg, pad;
+  uint32_t nwg;        // column workgroups of this piece
+  uint32_t g0, gn;     // split run: this piece's first column and the window's columns (else 0, nwg)
+  uint32_t xslot, xrow, xrows;  // split run: the call's slot, this piece's row, the rows (pieces)
+  // split run: the cross-device bound table as this device maps it, else null (last, so the one-device
+  // kernel reads its fields at the offsets it always did: its code is unchanged)
+  unsigned long long* xb;
 };
 
 struct bm_result {

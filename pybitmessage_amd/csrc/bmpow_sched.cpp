@@ -419,13 +419,38 @@ void split_kinds(const std::vector<bm_obj>& objs, bool any_var, StepPlan& p) {
 // ---------------------------------------------------------------------------------------
 // per-device stepping: claims from the frontier
 // ---------------------------------------------------------------------------------------
-int XPool::alloc(uint32_t obj) {
-  for (uint32_t x = 0; x < BM_XSLOTS; ++x)
-    if (owner[x] == 0 && ref[x] == 0) {
-      owner[x] = obj + 1;
-      return (int)x;
+bool XPool::needed(uint32_t x, const BatchState* b) const {
+  if (!owner[x]) return false;
+  if (ref[x]) return true;  // a launch in flight may still publish there
+  const uint32_t o = owner[x] - 1;
+  // its object still holds it, is searching and has items in flight (which may not carry the slot
+  // yet: they were planned before it was allocated)
+  return b && o < b->n && b->xs[o] == x + 1 && b->done[o] == BMPOW_PENDING && b->nfly[o] > 0;
+}
+
+int XPool::alloc(uint32_t obj, BatchState* b) {
+  int got = -1;
+  for (uint32_t x = 0; x < BM_XSLOTS && got < 0; ++x)
+    if (owner[x] == 0 && ref[x] == 0) got = (int)x;
+  if (got < 0) {
+    // reclaim slots whose owner no longer needs them: released outside release_xslots (the object
+    // restarted by init / reset / add, or settled while items planned before the slot were in flight)
+    for (uint32_t x = 0; x < BM_XSLOTS; ++x) {
+      if (!owner[x] || needed(x, b)) continue;
+      const uint32_t o = owner[x] - 1;
+      if (b && o < b->n && b->xs[o] == x + 1) b->xs[o] = 0;
+      owner[x] = 0;
+      if (got < 0) got = (int)x;
     }
-  return -1;
+  }
+  if (got >= 0) owner[got] = obj + 1;
+  return got;
+}
+
+size_t XPool::owned() const {
+  size_t n = 0;
+  for (uint32_t x = 0; x < BM_XSLOTS; ++x) n += owner[x] != 0;
+  return n;
 }
 
 bool claimable(const BatchState& b, size_t o) {
@@ -578,7 +603,7 @@ bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L) {
     else if (b.holder[o] != (int16_t)c.s) b.holder[o] = kShared;
     b.nfly[o]++;
     if (c.xp && !b.xs[o] && (cl.P > 1 || b.holder[o] == kShared)) {
-      const int x = c.xp->alloc(o);
+      const int x = c.xp->alloc(o, &b);
       if (x >= 0) {
         b.xs[o] = (uint8_t)(x + 1);
         if (c.xreset) c.xreset((uint32_t)x);
@@ -632,6 +657,17 @@ void release_xslots(BatchState& b, const Launch& L, XPool* xp) {
   }
 }
 
+// Give an object's cross-shard slot back once nothing needs it: no in-flight item carries it and the
+// object is finished or has nothing in flight (a slot whose last carrying item completed
+// while older items of its object were still in flight kept its owner, and nothing freed it later).
+void free_idle_xslot(BatchState& b, uint32_t o, XPool* xp) {
+  if (!xp || o >= b.n || !b.xs[o]) return;
+  const uint32_t x = b.xs[o] - 1u;
+  if (xp->ref[x] || (b.done[o] == BMPOW_PENDING && b.nfly[o] > 0)) return;
+  if (xp->owner[x] == o + 1) xp->owner[x] = 0;
+  b.xs[o] = 0;
+}
+
 // The item's piece is no longer in flight.
 const Claim* unfly(BatchState& b, const Launch& L, const bm_item& it) {
   const Claim& cl = L.claims[it.pad];
@@ -668,12 +704,15 @@ size_t apply_launch(BatchState& b, const Launch& L, XPool* xp, const std::functi
   size_t fin = 0;
   for (uint32_t o : touched) fin += settle(b, o) ? 1 : 0;
   release_xslots(b, L, xp);
+  for (uint32_t o : touched) free_idle_xslot(b, o, xp);
   return fin;
 }
 
 void drop_launch(BatchState& b, const Launch& L, XPool* xp) {
   for (const bm_item& it : L.plan.items[0]) unfly(b, L, it);
   release_xslots(b, L, xp);
+  for (const Claim& cl : L.claims)
+    if (cl.obj < b.n && b.gen[cl.obj] == cl.gen) free_idle_xslot(b, cl.obj, xp);
   b.broken = true;
 }
 
@@ -1270,6 +1309,17 @@ void Engine::stepper(size_t s) {
     // 1. while fewer than two launches are in flight, plan the next one (it queues behind the
     //    running one on the shard's stream)
     if (e.q.size() < 2 && can_plan()) {
+      if (e.throttle_ms > 0 && !e.throttled) {
+        // A/B knob: a slow device -- the delay comes before the plan, never between the plan and the
+        // enqueue (below)
+        const double thr = e.throttle_ms;
+        lk.unlock();
+        std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(thr * 1000)));
+        lk.lock();
+        e.throttled = true;
+        continue;  // the state changed meanwhile: check again
+      }
+      e.throttled = false;
       Launch& L = e.buf[e.next];
       PlanCtx c;
       c.s = s;
@@ -1288,13 +1338,18 @@ void Engine::stepper(size_t s) {
         stats.planned += L.planned;
         ++inflight_;
         e.q.push_back(&L);
-        const double thr = e.throttle_ms;
-        lk.unlock();
-        if (thr > 0) std::this_thread::sleep_for(std::chrono::microseconds((int64_t)(thr * 1000)));
+        // Enqueued under the mutex, in one piece with the plan: a slot's reuse
+        // (take_done + add, or a scratch re-init) writes the new object on every shard's stream under
+        // this mutex too (init_slots), so a launch is queued either before that slot init -- it then
+        // hashes the old record, its results are stale by the slot's generation, and the init resets
+        // best[] / found[] behind it -- or after it, planned from the new generation.  Enqueued after the
+        // unlock, a launch planned for the old occupant could run after the init and leave a hit of the
+        // new object from the old window in best[], which the new object's first window then reported as
+        // found: nonces between its frontier and that hit were never hashed.  An enqueue is a handful of
+        // asynchronous HIP calls (~20 us), once per launch of ~80 ms.
         std::string err;
         L.t_launch = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
         const int rc = ops_.launch(L, err);
-        lk.lock();
         if (rc < 0) {
           e.q.pop_back();
           e.next ^= 1;  // its buffer is free again
@@ -1354,8 +1409,20 @@ void Engine::attach(std::unique_lock<std::mutex>& lk, BatchState* b) {
   if (b_ != b) {
     drain(lk);
     b_ = b;
+    xp_ = XPool();  // nothing in flight: no slot is carried, and the owners were the old batch's objects
   }
   clear_error();
+}
+
+size_t Engine::xslots_owned(bool gc) {
+  if (gc)
+    for (uint32_t x = 0; x < BM_XSLOTS; ++x)
+      if (xp_.owner[x] && !xp_.needed(x, b_)) {
+        const uint32_t o = xp_.owner[x] - 1;
+        if (b_ && o < b_->n && b_->xs[o] == x + 1) b_->xs[o] = 0;
+        xp_.owner[x] = 0;
+      }
+  return xp_.owned();
 }
 
 void Engine::detach(std::unique_lock<std::mutex>& lk) {

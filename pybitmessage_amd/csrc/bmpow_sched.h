@@ -233,7 +233,11 @@ struct Launch {
 struct XPool {
   uint32_t ref[BM_XSLOTS] = {};    // in-flight items carrying the slot
   uint32_t owner[BM_XSLOTS] = {};  // object + 1, 0 = unowned
-  int alloc(uint32_t obj);         // -1 when every slot is taken (the items then go without one)
+  // -1 when every slot is needed (the items then go without one); with b, a slot whose owner no
+  // longer needs it (needed) is reclaimed first
+  int alloc(uint32_t obj, BatchState* b = nullptr);
+  bool needed(uint32_t x, const BatchState* b) const;
+  size_t owned() const;
 };
 
 // What plan_launch needs to know about the shard it plans for.
@@ -294,7 +298,9 @@ class Engine {
  public:
   Engine(EngineOps ops, size_t S, uint32_t resident, uint64_t step_trials);
   ~Engine();  // drains and joins the steppers
-  std::mutex mu;  // the attached batch's state and everything below; never held across a device call
+  // the attached batch's state and everything below; held across a launch's enqueue (plan and enqueue
+  // are one step, so a slot's reuse cannot fall between them), never across a wait for the device
+  std::mutex mu;
   // Make b the batch the steppers work on; a different attached batch is drained first.  lk holds mu.
   void attach(std::unique_lock<std::mutex>& lk, BatchState* b);
   // No new claims; wait until no launch is in flight (results applied); the batch stays attached.
@@ -313,6 +319,9 @@ class Engine {
   void set_throttle(size_t s, double ms);  // A/B knob: a shard sleeps this long before each launch
   size_t shards() const { return S_; }
   size_t in_flight() const { return inflight_; }
+  // Cross-shard bound slots with an owner (under mu); gc: first give back those no object needs.  After
+  // a drain with every object settled, 0 (sched_sim checks it).
+  size_t xslots_owned(bool gc = false);
   ShardRates rates;  // under mu
   EngineStats stats; // under mu
   int error() const { return error_; }
@@ -327,6 +336,7 @@ class Engine {
     Launch buf[2];
     int next = 0;
     double throttle_ms = 0;
+    bool throttled = false;  // the throttle's delay before this shard's next plan has been served
     int policy = -2;       // the stepper's scheduling policy
     clockid_t cpu_clock{}; // its CPU-time clock
     bool have_clock = false;

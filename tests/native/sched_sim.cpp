@@ -846,6 +846,101 @@ static void scenario_session() {
   fprintf(stderr, "session: %zu objects through %zu slots while the steppers ran\n", all.size(), b.n);
 }
 
+// ---- scenario 7b: slot reuse while a shard is throttled ----
+// Producers and a consumer churn a session's slots over 4 shards while shard 1 sleeps 2 ms before each
+// of its plans.  Round 4 slept between the plan and the enqueue: a slot could be released and re-filled
+// (its init queued on every stream) in between, the stale launch then ran after the init, hashed the
+// NEW object over the OLD window and left a real but high hit in best[], which the new object's first
+// window reported -- nonces between its frontier and that hit were never hashed.  Every answer must be
+// exact, and once the session has drained no cross-shard slot may still be owned (round 4 leaked slots
+// whose last carrying item completed while older items of the object were in flight).
+static void scenario_session_churn() {
+  std::mutex gmu;
+  const size_t S = 4;
+  SimLib lib(S, 24, 1 << 12);
+  lib.eng().set_throttle(1, 2.0);
+  BatchState b;
+  init(b, 0, nullptr, nullptr, nullptr);
+  b.cap = 1 << 20;
+  std::vector<Obj> all;
+  std::vector<int> slot_owner;
+  std::vector<std::array<uint64_t, 3>> results;
+  std::atomic<int> producers_left{3};
+  auto producer = [&](int id) {
+    std::mt19937_64 rng(300 + id);
+    for (int burst = 0; burst < 30; ++burst) {
+      const size_t m = 1 + rng() % 6;
+      std::vector<Obj> objs = random_objs(rng, m, 1);
+      // easy and hard objects mixed: hard ones run their frontiers far up, so a stale launch of their
+      // slot hashes a window well above a new easy object's first window
+      for (Obj& o : objs) o.target = kU64Max / (rng() % 3 ? 200 + rng() % 3000 : 20000 + rng() % 60000);
+      std::vector<uint8_t> ihs;
+      std::vector<uint64_t> tg, st;
+      pack_list(objs, ihs, tg, st);
+      {
+        std::lock_guard<std::mutex> g(gmu);
+        std::unique_lock<std::mutex> lk(lib.eng().mu);
+        std::vector<uint32_t> slots;
+        add(b, m, ihs.data(), tg.data(), nullptr, slots);
+        lib.init_slots(b, slots);
+        lib.eng().notify();
+        for (size_t i = 0; i < m; ++i) {
+          if (slot_owner.size() <= slots[i]) slot_owner.resize(slots[i] + 1, -1);
+          slot_owner[slots[i]] = (int)all.size();
+          all.push_back(objs[i]);
+          results.push_back({0, 0, 0});
+        }
+      }
+      std::this_thread::sleep_for(std::chrono::microseconds(100 + rng() % 2000));
+    }
+    producers_left--;
+  };
+  auto runner = [&]() {
+    uint32_t slot[64];
+    uint64_t nonce[64], trial[64];
+    uint8_t done[64];
+    for (;;) {
+      std::unique_lock<std::mutex> g(gmu);
+      std::unique_lock<std::mutex> lk(lib.eng().mu);
+      lib.eng().attach(lk, &b);
+      std::string err;
+      const int rc = lib.eng().run(lk, S << 12, true,
+                                   [&] { return b.finished_head < b.finished.size() || b.pending == 0; }, err);
+      CHECK(rc == 0, "churn run %d %s", rc, err.c_str());
+      // pop (and so free for reuse) at once, while the other shards' launches are in flight
+      const size_t k = take_done(b, 64, slot, nonce, trial, done);
+      for (size_t j = 0; j < k; ++j) {
+        const int a = slot_owner[slot[j]];
+        if (a < 0) continue;
+        results[a] = {done[j], nonce[j], trial[j]};
+        slot_owner[slot[j]] = -1;
+      }
+      const bool idle = b.pending == 0;
+      if (producers_left.load() == 0 && idle && b.finished_head == b.finished.size()) break;
+      lk.unlock();
+      g.unlock();
+      if (idle) std::this_thread::sleep_for(std::chrono::microseconds(200));
+    }
+  };
+  std::vector<std::thread> th;
+  for (int i = 0; i < 3; ++i) th.emplace_back(producer, i);
+  th.emplace_back(runner);
+  for (auto& t : th) t.join();
+  size_t owned = 0;
+  {
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().drain(lk);
+    owned = lib.eng().xslots_owned();
+    lib.eng().detach(lk);
+  }
+  for (size_t i = 0; i < all.size(); ++i)
+    expect_exact(all[i], (int)results[i][0], results[i][1], results[i][2], "churn", i);
+  CHECK(owned == 0, "%zu cross-shard slots still owned after the session drained", owned);
+  CHECK(b.n < all.size(), "slots were not reused (%zu slots for %zu objects)", b.n, all.size());
+  fprintf(stderr, "session_churn: %zu objects through %zu slots, shard 1 throttled; %zu slots owned at the end\n",
+          all.size(), b.n, owned);
+}
+
 // ---- scenario 8: rate averages, fair shares, the steppers' scheduling class ----
 static void scenario_rates_policy() {
   ShardRates r;
@@ -1277,6 +1372,7 @@ int main(int argc, char** argv) {
   timed("top_of_space", scenario_top_of_space);
   timed("bounded", scenario_bounded);
   timed("session", scenario_session);
+  timed("session_churn", scenario_session_churn);
   timed("rates_policy", scenario_rates_policy);
   timed("min_trial", scenario_min_trial);
   timed("verify", scenario_verify);

@@ -139,6 +139,7 @@ def test_single_rank_line_carries_the_round4_fields(monkeypatch):
     assert 'frac_vs_mix_ceiling' not in line['roofline'] and 'frac_vs_baseline_md_peak' not in line['roofline']
     monkeypatch.setenv('BMPOW_ONE', '1')
     assert bench.single_object_path(args)
-    assert not bench.single_object_path(types.SimpleNamespace(devices=1, shards_per_device=8))
+    # round 5: run() takes the single-object path on any number of shards (pieces per device)
+    assert bench.single_object_path(types.SimpleNamespace(devices=1, shards_per_device=8))
     monkeypatch.setenv('BMPOW_ONE', '0')
     assert not bench.single_object_path(args)

@@ -129,41 +129,44 @@ def test_c5_default_difficulty_slice(gpulib, shards, coracle):
 ROW = 1024 * 256
 
 
-@pytest.mark.parametrize('nshards', [1, 4, 8])
-def test_c1_sweep_stops_within_rows_of_the_hit(gpulib, shards, golden, nshards):
-    """One C1 object (1 KB msg at defaults, golden nonce 10,909,138) on one shard, and nonce-split
-    over 4 and 8 shards (streams on this device, the slicing of 4 / 8 GPUs).
+@pytest.mark.parametrize('nshards,split', [(1, False), (8, False), (4, True), (8, True)])
+def test_c1_sweep_stops_within_rows_of_the_hit(gpulib, shards, golden, nshards, split):
+    """One C1 object (1 KB msg at defaults, golden nonce 10,909,138) through run() on one shard, on 8
+    shards of this device, and split into 4 and 8 forced pieces (bmpow_set_run_split).
 
-    One shard: the workgroups take the window's blocks in order from the item's queue, so the trials
-    hashed past the answer stay within a few block rows (the static column layout of early round 3
-    hashed 29 M on one shard for the 10.9 M useful, profiles/r03/c1_columns_static.jsonl: the SIMD arbiter
-    favours older waves, so the columns drifted apart).
+    One piece: the workgroups take the window's blocks in order from its queue, so the trials hashed
+    past the answer stay within a few block rows (the static column layout of early round 3 hashed
+    29 M on one shard for the 10.9 M useful, profiles/r03/c1_columns_static.jsonl: the SIMD arbiter
+    favours older waves, so the columns drifted apart).  Shards sharing a device do not split run()
+    (round 5), so 8 shards of this device behave as one.
 
-    Several shards on ONE device: a split window's pieces (one per shard, claimed by each shard's
-    stepper on its own, bmsched::plan_launch) sweep interleaved columns of the same rows and stop at
-    the first hit of any through the cross-shard bound, but their kernels share this
-    device's SIMDs, where the earlier-launched kernel's (older) waves get the issue first, and 8
-    streams share the 4 hardware queues (GPU_MAX_HW_QUEUES); so one shard runs ahead of another and
-    the waste is bounded by the split window's cap (2E, bmsched::expect_cap), not by rows.  On
-    separate GPUs no shard competes with another for issue."""
+    Forced pieces on ONE device: each piece sweeps its interleaved columns of the same rows and stops at
+    the first hit of any through the cross-device bound, but the pieces' kernels share this device:
+    4 hardware queues (GPU_MAX_HW_QUEUES) run 4 pieces at once and the others start as those finish,
+    so a piece may run through its whole share of a window before the piece holding the answer starts.
+    Where pieces share a device, a window is therefore 2E (bmsched::expect_cap) rather than a step per
+    piece, and that bounds the waste.  On separate GPUs every piece runs from the start."""
     shards([0] * nshards)
+    prev = gpulib.bmpow_set_run_split(1 if split else 0)
     k = [k for k in golden('first_nonce_kats.json')['kats'] if k['nonce'] == 10909138][0]
     ih = bytes.fromhex(k['ih'])
     e = 2 ** 64 / (k['target'] + 1)
     past = []
-    for _ in range(5):
-        gpulib.bmpow_reset_stats()
-        assert proofofwork.run(k['target'], ih) == [k['trial'], k['nonce']]
-        st = _lib.BmpowStats()
-        gpulib.bmpow_get_stats(ctypes.byref(st))
-        assert st.trials >= k['nonce'] - 1
-        past.append(st.trials - k['nonce'])
-        if nshards > 1:
-            # one split window of 2E (bmsched::expect_cap) in nshards pieces; the pieces of the next
-            # window each shard already queued behind its first stop at their first block (the
-            # relay folds the hit into every shard's best[])
-            assert st.trials <= 2 * e + 2 * nshards * ROW, (st.trials, st.launches)
-    if nshards == 1:
+    try:
+        for _ in range(5):
+            gpulib.bmpow_reset_stats()
+            assert proofofwork.run(k['target'], ih) == [k['trial'], k['nonce']]
+            st = _lib.BmpowStats()
+            gpulib.bmpow_get_stats(ctypes.byref(st))
+            assert st.trials >= k['nonce'] - 1
+            past.append(st.trials - k['nonce'])
+            if split:
+                # one window of 2E in nshards pieces; the pieces of the next window queued behind stop
+                # at their first blocks (the relay folds the hit into every piece's minimum)
+                assert st.trials <= 2 * e + 2 * nshards * ROW, (st.trials, st.launches)
+    finally:
+        gpulib.bmpow_set_run_split(prev)
+    if not split:
         # typically within a row or two; a rare call runs on while the workgroup holding the answer's
         # block is held back (the slowest of 300 calls: 1 - 8 M past, profiles/r04/), so the median
         # carries the bound and every call stays under one window's worth of rows

@@ -68,7 +68,8 @@ def test_throttled_shard_does_not_gate_the_others(gpulib, shards, coracle):
 
 def test_steppers_idle_priority_and_cpu(gpulib, shards):
     """Every stepper thread runs at SCHED_IDLE and, while a C2-like batch keeps the GPU busy for a
-    few seconds, uses a small share of one CPU (it sleeps in a blocking-sync event wait)."""
+    few seconds, uses a small share of one CPU (it sleeps between queries of its launch's event,
+    bmpow_host.hip engine_wait)."""
     shards([0, 0])
     objs, _ = bench.make_objects('c2', 0, 96)
     cpu0 = (ctypes.c_double * 2)()
@@ -173,3 +174,127 @@ def test_no_empty_launch_stream_behind_a_slow_shard(gpulib, shards, coracle):
     for (t, ih), r in zip(objs, res):
         assert tuple(r) == coracle.search(ih, t), t
     assert st.launches < 200, st.launches
+
+
+@pytest.fixture
+def run_split(gpulib):
+    """bmpow_set_run_split for the test body, restored after."""
+    prev = gpulib.bmpow_set_run_split(-1)
+    yield lambda on: gpulib.bmpow_set_run_split(1 if on else 0)
+    gpulib.bmpow_set_run_split(prev)
+
+
+def run_pieces(lib):
+    ids = (ctypes.c_int * 64)()
+    n = lib.bmpow_get_run_pieces(ids, 64)
+    return list(ids[:n])
+
+
+def test_run_split_over_pieces_exact(gpulib, shards, run_split, golden, coracle):
+    """run() split into 2, 3 and 8 interleaved pieces (bmpow_set_run_split: one piece per shard, here
+    shards as streams of this device -- the multi-device path of round 5 rehearsed on one GPU: every
+    piece a bm_search1_kernel<true> launch with its relay, the cross-device bound in host-pinned
+    memory).  The golden C1 object (10,909,138), the test_openclpow vector (224,121,278), random
+    objects against the C oracle, and bounded calls whose answer is the last nonce of the range or
+    one past it."""
+    kats = golden('first_nonce_kats.json')['kats']
+    c1 = [k for k in kats if k['nonce'] == 10909138][0]
+    ocl = [k for k in kats if k['nonce'] == 224121278][0]
+    rng = random.Random(77)
+    n, t = ctypes.c_uint64(), ctypes.c_uint64()
+    run_split(True)
+    for layout in ([0, 0], [0, 0, 0], [0] * 8):
+        shards(layout)
+        assert run_pieces(gpulib) == list(range(len(layout)))
+        for k in (c1, ocl):
+            assert proofofwork.run(k['target'], bytes.fromhex(k['ih'])) == [k['trial'], k['nonce']], (layout, k['note'])
+        for k in kats[:12]:
+            assert proofofwork.run(k['target'], bytes.fromhex(k['ih'])) == [k['trial'], k['nonce']], layout
+        for _ in range(6):
+            x = rng.randbytes(64)
+            tg = U64 // rng.choice([10, 3000, 200000, 5000000])
+            assert proofofwork.run(tg, x) == list(coracle.search(x, tg)), layout
+        # bounded calls: the answer is the last nonce of the range, then one past it
+        ih = hashlib.sha512(b'split-edge %d' % len(layout)).digest()
+        want_t, want_n = coracle.search(ih, U64 // 40000)
+        assert gpulib.bmpow_search(ih, U64 // 40000, 1, want_n, ctypes.byref(n), ctypes.byref(t)) == _lib.FOUND
+        assert (t.value, n.value) == (want_t, want_n)
+        assert gpulib.bmpow_search(ih, U64 // 40000, 1, want_n - 1, ctypes.byref(n), ctypes.byref(t)) == _lib.NOT_FOUND
+        assert gpulib.bmpow_search(ih, U64 // 40000, want_n, 5, ctypes.byref(n), ctypes.byref(t)) == _lib.FOUND
+        assert (t.value, n.value) == (want_t, want_n)
+        # every nonce a hit: the pieces' hit logs overflow and the trial is re-hashed on the device
+        assert gpulib.bmpow_search(ih, U64, 1, 1 << 20, ctypes.byref(n), ctypes.byref(t)) == _lib.FOUND
+        assert (n.value, t.value) == (1, coracle.trial(1, ih))
+
+
+def test_run_split_small_windows_and_sweep(gpulib, shards, run_split, coracle):
+    """Split run() with 2^20-trial windows per piece (several windows per call, the next queued behind
+    the running one on every piece) over 3 pieces: answers against the C oracle; and a no-hit sweep
+    (target 0) of 2^28 nonces that hashes exactly 2^28 trials in all (no block lost or hashed twice
+    over the pieces' interleaved columns)."""
+    shards([0, 0, 0])
+    run_split(True)
+    gpulib.bmpow_set_step_trials(1 << 20)
+    rng = random.Random(5)
+    for i in range(12):
+        x = rng.randbytes(64)
+        tg = U64 // rng.choice([1 << 18, 1 << 20, 1 << 21])
+        assert proofofwork.run(tg, x) == list(coracle.search(x, tg)), i
+    gpulib.bmpow_reset_stats()
+    n, t = ctypes.c_uint64(), ctypes.c_uint64()
+    ih = hashlib.sha512(b'split sweep').digest()
+    assert gpulib.bmpow_search(ih, 0, 1, 1 << 28, ctypes.byref(n), ctypes.byref(t)) == _lib.NOT_FOUND
+    st = _lib.BmpowStats()
+    gpulib.bmpow_get_stats(ctypes.byref(st))
+    assert st.trials == 1 << 28, st.trials
+    tr, _ = shard_stats(gpulib, 3)
+    assert sum(tr) == 1 << 28 and min(tr) > 0, tr
+
+
+def test_shards_sharing_a_device_do_not_split_run(gpulib, shards, golden):
+    """Without the forced split, shards that share a device give run() ONE piece (their kernels would
+    compete for the same SIMDs): 8 shards of this device run the golden C1 object as one shard does --
+    one launch, within a few block rows of the answer."""
+    shards([0] * 8)
+    assert run_pieces(gpulib) == [0]
+    k = [k for k in golden('first_nonce_kats.json')['kats'] if k['nonce'] == 10909138][0]
+    past = []
+    for _ in range(5):
+        gpulib.bmpow_reset_stats()
+        assert proofofwork.run(k['target'], bytes.fromhex(k['ih'])) == [k['trial'], k['nonce']]
+        st = _lib.BmpowStats()
+        gpulib.bmpow_get_stats(ctypes.byref(st))
+        assert st.launches == 1
+        past.append(st.trials - k['nonce'])
+    assert sorted(past)[2] <= 4 * 1024 * 256, past
+
+
+def test_long_run_leaves_the_cpu_alone(gpulib, shards):
+    """A run() call of over a second sleeps while the GPU works (the reference's PoW threads run at
+    SCHED_IDLE, bitmsghash.cpp:149, its pool workers at nice 20, proofofwork.py:72-87; round 4's
+    single-object path busy-polled a core for the whole call): process CPU under 0.1 s per second,
+    for a no-hit sweep of 2^33 nonces and for a series of objects of E = 2^30 (~165 ms each)."""
+    import resource
+    shards([0])
+    n, t = ctypes.c_uint64(), ctypes.c_uint64()
+    ih = hashlib.sha512(b'cpu sweep').digest()
+
+    def cpu():
+        ru = resource.getrusage(resource.RUSAGE_SELF)
+        return ru.ru_utime + ru.ru_stime
+    assert gpulib.bmpow_search(ih, 0, 1, 1 << 26, ctypes.byref(n), ctypes.byref(t)) == _lib.NOT_FOUND  # warm
+    gpulib.bmpow_reset_stats()
+    c0, w0 = cpu(), time.perf_counter()
+    assert gpulib.bmpow_search(ih, 0, 1, 1 << 33, ctypes.byref(n), ctypes.byref(t)) == _lib.NOT_FOUND
+    wall, used = time.perf_counter() - w0, cpu() - c0
+    st = _lib.BmpowStats()
+    gpulib.bmpow_get_stats(ctypes.byref(st))
+    assert wall > 1.0 and used / wall < 0.1, (wall, used)
+    assert st.one_wait_sleep_ms > 0.9 * wall * 1e3 and st.one_wait_spin_ms == 0, (st.one_wait_sleep_ms, st.one_wait_spin_ms)
+    rng = random.Random(8)
+    objs = [(U64 >> 30, rng.randbytes(64)) for _ in range(10)]
+    c0, w0 = cpu(), time.perf_counter()
+    for tg, x in objs:
+        proofofwork.run(tg, x)  # re-checked with hashlib inside
+    wall, used = time.perf_counter() - w0, cpu() - c0
+    assert wall > 1.0 and used / wall < 0.1, (wall, used)

@@ -43,9 +43,10 @@ def test_header_declares_the_boundary():
               'bmpow_service_submit', 'bmpow_service_poll', 'bmpow_service_cancel', 'bmpow_service_outstanding',
               'bmpow_service_stop', 'bmpow_service_destroy', 'bmpow_set_device_count', 'bmpow_trials_len',
               'bmpow_search_len', 'bmpow_min_trial_var', 'bmpow_batch_add_var', 'bmpow_service_submit_var',
-              'bmpow_get_shard_rates', 'bmpow_get_shard_stats', 'bmpow_get_thread_info', 'bmpow_set_shard_throttle']:
+              'bmpow_get_shard_rates', 'bmpow_get_shard_stats', 'bmpow_get_thread_info', 'bmpow_set_shard_throttle',
+              'bmpow_set_run_split', 'bmpow_get_run_pieces', 'bmpow_device_pci_bus_id']:
         assert s in syms
-    assert len(syms) == 57
+    assert len(syms) == 60
 
 
 def test_library_exports_every_declared_symbol(rawlib):

@@ -25,7 +25,11 @@
 #   c1-dist:V        C1 through run(), 300 calls with the variant's library (default | variants/<name>):
 #                    the per-call distribution of wall time and trials past the answer
 #   c1-engine        C1 through the engine (BMPOW_ONE=0), 300 calls
-#   c1-shards:K      C1 with K shards on device 0 (the engine's split windows), 300 calls
+#   c1-shards:K      C1 with K shards on device 0 (run(): one piece, the device's), 300 calls
+#   c1-split:K       C1 with K shards on device 0, run() forced into K pieces (bmpow_set_run_split), 100 calls
+#   c3-split:K       C3 (2^34) with K forced pieces on device 0
+#   c4-serial        8 C4 objects one after another through proofofwork.run (host CPU of a long serial call)
+#   c1c3-ab:V1,V2    tools/cmp_c1.sh over the variants (C1 40 calls + C3 2^35 each), same box
 #   c2-wait:MODE     bench-quick with BMPOW_WAIT=MODE (sleep | block | spin | poll): the steppers' CPU
 #   devices:N:K[:T]  C3 and C4 via --devices N --shards-per-device K (throttle shard 0 by T ms)
 #   rehearse-n2 | rehearse-n8   the driver's N-rank bench command with every rank on GPU 0
@@ -53,6 +57,16 @@ for step in "$@"; do
     c1-shards:*) k=${step#c1-shards:}
       timeout -k 10 200 python3 bench.py --config c1 --steps 300 --warmup 5 --no-cpu-baseline --devices 1 \
         --shards-per-device "$k" > "$OUT/c1_shards_$k.json" 2> "$OUT/c1_shards_$k.err" ;;
+    c1-split:*) k=${step#c1-split:}
+      timeout -k 10 200 python3 bench.py --config c1 --steps 100 --warmup 5 --no-cpu-baseline --devices 1 \
+        --shards-per-device "$k" --run-split > "$OUT/c1_split_$k.json" 2> "$OUT/c1_split_$k.err" ;;
+    c3-split:*) k=${step#c3-split:}
+      timeout -k 10 200 python3 bench.py --config c3 --c3-log2 34 --steps 1 --warmup 0 --no-cpu-baseline --devices 1 \
+        --shards-per-device "$k" --run-split > "$OUT/c3_split_$k.json" 2> "$OUT/c3_split_$k.err" ;;
+    c4-serial) timeout -k 10 300 python3 bench.py --config c4 --serial --objects 8 --steps 1 --warmup 1 --no-cpu-baseline \
+        > "$OUT/c4_serial.json" 2> "$OUT/c4_serial.err" ;;
+    c1c3-ab:*) timeout -k 10 900 bash tools/cmp_c1.sh "$OUT/c1c3_ab" $(echo "${step#c1c3-ab:}" | tr ',' ' ') \
+        > "$OUT/c1c3_ab.txt" 2> "$OUT/c1c3_ab.err" ;;
     c2-wait:*) m=${step#c2-wait:}
       BMPOW_WAIT=$m timeout -k 10 300 python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/c2_wait_$m.json" 2> "$OUT/c2_wait_$m.err" ;;
     devices:*) IFS=: read -r _ n k t <<< "$step"; t=${t:-0}; tag="n${n}_k${k}_t${t}"
