@@ -76,6 +76,12 @@ WaitMode g_wait = kWaitSleep;
 // one (A/B); BMPOW_ONE=0 sends run() through the engine instead (A/B).
 enum OneWait { kOneAuto, kOneSpin, kOneSleep };
 OneWait g_one_wait = kOneAuto;
+// The wait's fault check: an event recorded behind each launch, queried every g_one_query sleeping
+// polls (BMPOW_ONE_QUERY=N, 0: never).  BMPOW_ONE_EVENT=0 queries the stream instead (A/B):
+// hipStreamQuery cost the process 0.13 - 1.0 CPU-s per s during a 2^33 sweep, an event query 0.012
+// (tools/diag/one_cpu.py, profiles/r05/one_cpu.jsonl).
+int g_one_query = 8;
+bool g_one_event = true;
 bool g_one_enabled = true;
 
 // One of a shard's two engine launch buffers (the running launch and the one staged behind it).
@@ -362,6 +368,8 @@ int init_locked() {
                                             : kWaitSleep;
   if (const char* w = std::getenv("BMPOW_WAIT1"))
     g_one_wait = std::strcmp(w, "spin") == 0 ? kOneSpin : std::strcmp(w, "sleep") == 0 ? kOneSleep : kOneAuto;
+  if (const char* w = std::getenv("BMPOW_ONE_QUERY")) g_one_query = std::max(0, std::atoi(w));
+  if (const char* w = std::getenv("BMPOW_ONE_EVENT")) g_one_event = std::atoi(w) != 0;
   if (const char* w = std::getenv("BMPOW_ONE")) g_one_enabled = std::atoi(w) != 0;
   const auto vis = visible_gfx950();
   if (vis.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
@@ -851,6 +859,7 @@ struct OnePath {
   bm_one_out* h_out = nullptr;  // host-mapped ring of results
   bm_one_out* d_out = nullptr;  // the device's address of h_out
   unsigned long long* d_xone = nullptr;  // the cross-device table as this device maps it
+  hipEvent_t ev[8] = {};  // BMPOW_ONE_EVENT: recorded behind launch seq in ev[seq % 8]
   uint64_t seq = 0;
   double rate = 0;  // trials per ms, an exponential average over launches of >= 2^24 trials (0: none yet)
   uint64_t trials = 0;  // since bmpow_reset_stats (bmpow_get_shard_stats)
@@ -860,9 +869,8 @@ std::vector<OnePath> g_ones;  // per shard; set up for the shards that carry pie
 unsigned long long* g_xone = nullptr;  // the cross-device bound of split run() calls (BM_MAX_SHARDS x BM_XSLOTS)
 uint64_t g_one_call = 0;
 bool g_run_split = false;  // bmpow_set_run_split: one piece per shard even where shards share a device
-// The wait (g_one_wait): "auto" spins when the launch waited for is the last one in flight and the
-// call's answer is expected within kOneSpinMs (E over the pieces' measured rate), and otherwise sleeps
-// between polls of the result word.  The reference's PoW threads run at SCHED_IDLE
+// The wait (g_one_wait): "auto" spins when the call's answer is expected within kOneSpinMs (E over
+// the pieces' measured rate), and otherwise sleeps between polls of the result word.  The reference's PoW threads run at SCHED_IDLE
 // (bitmsghash.cpp:149) and its pool workers at nice 20 (proofofwork.py:72-87): run() happens on the
 // caller's own thread here, so it keeps its priority and instead leaves the CPU alone while the GPU
 // works, except for the last few ms of a short call.
@@ -879,6 +887,8 @@ void free_one() {
     if (op.d_calls) (void)hipFree(op.d_calls);
     if (op.d_ctr) (void)hipFree(op.d_ctr);
     if (op.h_out) (void)hipHostFree(op.h_out);
+    for (hipEvent_t e : op.ev)
+      if (e) (void)hipEventDestroy(e);
   }
   g_ones.clear();
   if (g_xone) (void)hipHostFree(g_xone);
@@ -912,6 +922,8 @@ int ensure_one(size_t s) {
   op.d_out = (bm_one_out*)dp;
   HIPTRY(hipHostGetDevicePointer(&dp, g_xone, 0));
   op.d_xone = (unsigned long long*)dp;
+  if (g_one_event)
+    for (hipEvent_t& e : op.ev) HIPTRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   return 0;
 }
 
@@ -928,15 +940,16 @@ std::vector<size_t> one_pieces() {
 
 // Wait for launch `seq`'s result word.  spin: poll it with a pause (the answer is due within a few
 // ms); else sleep between polls for 1/64 of the time waited so far (20 us .. 250 us) -- a few
-// thousand polls per second, each a load of host memory.  The stream is queried every few polls, so
-// a launch that ended without writing its result (a fault) is caught instead of waited for forever.
+// thousand polls per second, each a load of host memory.  The launch's event is queried every few
+// polls, so a launch that ended without writing its result (a fault) is caught instead of waited for
+// forever.
 int wait_one(const Shard& sh, OnePath& op, uint64_t seq, bool spin) {
   bm_one_out* o = &op.h_out[seq % BM_ONE_RING];
   const double t0 = now_ms();
   for (uint32_t k = 1;; ++k) {
     if (__atomic_load_n(&o->seq, __ATOMIC_ACQUIRE) == seq) break;
-    if (k % (spin ? 1024u : 8u) == 0) {
-      const hipError_t e = hipStreamQuery(sh.stream);
+    if (spin ? k % 1024u == 0 : (g_one_query > 0 && k % (uint32_t)g_one_query == 0)) {
+      const hipError_t e = g_one_event ? hipEventQuery(op.ev[seq % 8]) : hipStreamQuery(sh.stream);
       if (e == hipSuccess) {
         if (__atomic_load_n(&o->seq, __ATOMIC_ACQUIRE) == seq) break;
         return set_err(BMPOW_E_HIP, "single-object launch completed without its result");
@@ -1018,8 +1031,8 @@ int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
     for (int i = 0; i < nfly; ++i) n += (double)fly[i].n;
     return !top && nfly < 2 && (nfly == 0 || n < kAheadE * expect);
   };
-  // spin only for a call whose answer is due within kOneSpinMs, and only while no window is queued
-  // behind the one waited for (then a late wake-up would cost the device nothing)
+  // spin only for a call whose answer is due within kOneSpinMs (at most that much CPU per call); a
+  // longer call sleeps between polls, so a wake-up may come up to 250 us late -- 0.2 % of a 120 ms call
   const bool short_call = expect / rate < kOneSpinMs;
   bm_one_args a;
   std::memset(&a, 0, sizeof a);
@@ -1061,6 +1074,7 @@ int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
       f.seq[p] = a.seq;
       if (P > 1) HIPTRY(hipSetDevice(sh.dev));
       HIPTRY(bm_launch_search1(sh.stream, a));
+      if (g_one_event) HIPTRY(hipEventRecord(op.ev[a.seq % 8], sh.stream));
     }
     ++nfly;
     if (room < step) top = true;
@@ -1079,7 +1093,7 @@ int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
       const Shard& sh = g_shards[pieces[p]];
       OnePath& op = g_ones[pieces[p]];
       const uint64_t seq = fly[0].seq[p];
-      const bool spin = g_one_wait == kOneSpin || (g_one_wait == kOneAuto && short_call && nfly == 1);
+      const bool spin = g_one_wait == kOneSpin || (g_one_wait == kOneAuto && short_call);
       rc = wait_one(sh, op, seq, spin);
       if (rc < 0) break;
       const bm_one_out& o = op.h_out[seq % BM_ONE_RING];

@@ -28,7 +28,8 @@ def _worker(rank, world, port, outdir):
     d = bench.Dist()
     objs, _ = bench.make_objects('c2', d.rank, 8)
     stats = types.SimpleNamespace(trials=1000 * (rank + 1), kernel_ms=10.0 * (rank + 1), launches=2)
-    r = {'desc': 'test', 'objects': 8, 'useful': 900.0 * (rank + 1), 'elapsed': 1.0 + rank, 'stats': stats}
+    r = {'desc': 'test', 'objects': 8, 'useful': 900.0 * (rank + 1), 'elapsed': 1.0 + rank, 'stats': stats,
+         'pci_bus_id': '0000:%02x:00.0' % (0x10 * (rank + 1))}
     args = types.SimpleNamespace(steps=1, warmup=0)
     d.barrier()
     line = bench.summarize(args, d, r, 'test-lib')
@@ -92,6 +93,13 @@ def test_two_rank_aggregation(tmp_path):
     assert line['objects_per_s'] == round(16 / 2.0, 3)
     assert line['performed_ghs'] == round(3000 / 2.0 / 1e9, 4)
     assert r1['line']['value'] == line['value']  # every rank sees the same reduction
+    # per_rank: which physical GPU each rank drove and its work, in rank order, on every rank
+    pr = line['per_rank']
+    assert [p['rank'] for p in pr] == [0, 1] and r1['line']['per_rank'] == pr
+    assert [p['device_pci_bus_id'] for p in pr] == ['0000:10:00.0', '0000:20:00.0']
+    assert [p['trials'] for p in pr] == [1000, 2000] and [p['kernel_ms'] for p in pr] == [10.0, 20.0]
+    assert [p['elapsed_s'] for p in pr] == [1.0, 2.0]
+    assert set(pr[0]) == {'rank', 'local_rank', 'device_pci_bus_id', 'trials', 'kernel_ms', 'elapsed_s'}
     # the committed PMC traffic (per 2^28-trial launch) scaled to this rank's trials per launch
     pmc = json.load(open(os.path.join(bench.ROOT, 'profiles', 'pmc_latest.json')))
     want = pmc['derived']['hbm_bytes_per_launch_upper'] * (1000 / 2) / pmc['raw']['trials_per_launch']

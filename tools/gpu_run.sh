@@ -14,6 +14,7 @@
 #   c5-full | c5-full-service   C5: 100,000 objects at default difficulty as one batch / through PowService
 #                    (~6 min each; a seeded 1,000 of the answers proven minimal)
 #   rocprof-bench    rocprofv3 --kernel-trace --stats over the default bench (3 steps)
+#   c1-split-trace:K the same with K forced pieces (the multi-device call's host timeline, rehearsed)
 #   pmc              tools/profile_pmc.sh OUT/pmc (C3 2^33, one counter group per pass)
 #   pmc:V            the same with the variant build variants/<name> (OUT/pmc_<name>)
 #   shard-latency    tools/shard_latency.py
@@ -28,6 +29,7 @@
 #   c1-shards:K      C1 with K shards on device 0 (run(): one piece, the device's), 300 calls
 #   c1-split:K       C1 with K shards on device 0, run() forced into K pieces (bmpow_set_run_split), 100 calls
 #   c3-split:K       C3 (2^34) with K forced pieces on device 0
+#   one-cpu          tools/diag/one_cpu.py: run()'s host CPU per wait configuration and per thread
 #   c4-serial        8 C4 objects one after another through proofofwork.run (host CPU of a long serial call)
 #   c1c3-ab:V1,V2    tools/cmp_c1.sh over the variants (C1 40 calls + C3 2^35 each), same box
 #   c2-wait:MODE     bench-quick with BMPOW_WAIT=MODE (sleep | block | spin | poll): the steppers' CPU
@@ -63,6 +65,7 @@ for step in "$@"; do
     c3-split:*) k=${step#c3-split:}
       timeout -k 10 200 python3 bench.py --config c3 --c3-log2 34 --steps 1 --warmup 0 --no-cpu-baseline --devices 1 \
         --shards-per-device "$k" --run-split > "$OUT/c3_split_$k.json" 2> "$OUT/c3_split_$k.err" ;;
+    one-cpu) timeout -k 10 300 python3 tools/diag/one_cpu.py 33 > "$OUT/one_cpu.jsonl" 2> "$OUT/one_cpu.err" ;;
     c4-serial) timeout -k 10 300 python3 bench.py --config c4 --serial --objects 8 --steps 1 --warmup 1 --no-cpu-baseline \
         > "$OUT/c4_serial.json" 2> "$OUT/c4_serial.err" ;;
     c1c3-ab:*) timeout -k 10 900 bash tools/cmp_c1.sh "$OUT/c1c3_ab" $(echo "${step#c1c3-ab:}" | tr ',' ' ') \
@@ -92,6 +95,11 @@ for step in "$@"; do
     c1-trace) timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --output-format csv -d "$OUT/c1_trace" -o run -- \
                 python3 bench.py --config c1 --steps 50 --warmup 3 --no-cpu-baseline > "$OUT/c1_trace.json" 2> "$OUT/c1_trace.err" &&
               python3 tools/c1_timeline.py "$OUT/c1_trace" > "$OUT/c1_timeline.json" ;;
+    c1-split-trace:*) k=${step#c1-split-trace:}
+      timeout -k 10 300 rocprofv3 --kernel-trace --hip-trace --output-format csv -d "$OUT/c1_split_trace_$k" -o run -- \
+        python3 bench.py --config c1 --steps 50 --warmup 3 --no-cpu-baseline --devices 1 --shards-per-device "$k" --run-split \
+        > "$OUT/c1_split_trace_$k.json" 2> "$OUT/c1_split_trace_$k.err" &&
+      python3 tools/c1_timeline.py "$OUT/c1_split_trace_$k" > "$OUT/c1_split_timeline_$k.json" ;;
     pmc) bash tools/profile_pmc.sh "$OUT/pmc" 33 > "$OUT/pmc.log" 2>&1 ;;
     pmc:*) v=${step#pmc:}; BMPOW_LIB=$v/libbmpow_hip.so bash tools/profile_pmc.sh "$OUT/pmc_$(basename "$v")" 33 \
              > "$OUT/pmc_$(basename "$v").log" 2>&1 ;;
