@@ -1226,11 +1226,18 @@ def pmc_counters():
     out = {'traffic': d.get('hbm_bytes_per_launch_upper'),
            'source': 'profiles/pmc_latest.json (bm_search_kernel, C3, 2^28-trial launches)',
            'build': full.get('build'), 'trials_per_launch': full.get('raw', {}).get('trials_per_launch')}
-    # provenance: were the counters collected on the library this run loaded?
+    # provenance: were the counters collected on the device code this run loaded?  The device code's
+    # md5 (the .hip_fatbin section, tools/lib_code_md5.py) is reproduced by a rebuild of the same
+    # sources; the whole file's md5 is not (the host code carries the build time)
     from pybitmessage_amd import _lib
-    md5 = lib_md5(_lib.lib_path())
-    out['benched_lib_md5'] = md5
-    out['stale'] = md5 is None or (full.get('build') or {}).get('lib_md5') != md5
+    from tools.lib_code_md5 import code_md5
+    build = full.get('build') or {}
+    out['benched_lib_md5'] = lib_md5(_lib.lib_path())
+    out['benched_code_md5'] = code_md5(_lib.lib_path())
+    if build.get('code_md5'):
+        out['stale'] = out['benched_code_md5'] is None or build['code_md5'] != out['benched_code_md5']
+    else:
+        out['stale'] = out['benched_lib_md5'] is None or build.get('lib_md5') != out['benched_lib_md5']
     for k in ('valu_instr_per_trial', 'valu_issue_util', 'valu_instr_per_simd_quad_cycle', 'dual_issue_share',
               'simd_busy_frac', 'wave_issue_stall_share', 'wave_wait_share', 'eff_clock_ghz'):
         if d.get(k) is not None:

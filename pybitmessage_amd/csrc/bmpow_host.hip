@@ -1750,10 +1750,15 @@ void bmpow_shutdown(void) {
 const char* bmpow_last_error(void) { return g_err.c_str(); }
 
 const char* bmpow_version(void) {
-  static char buf[128];
-  // the build time identifies the library a bench line or profile came from
-  std::snprintf(buf, sizeof buf, "bmpow %d gfx950 block=%d iters=%d built %s %s", BMPOW_ABI_VERSION, BM_BLOCK, BM_ITERS,
-                __DATE__, __TIME__);
+  static char buf[160];
+  // BM_SRC_ID (the Makefile: an md5 of every source and header the library is built from) identifies
+  // the library a bench line or profile came from; no build time, so a rebuild of the same sources in
+  // the same tree gives the same file (bench.py compares the PMC passes' library md5 with the benched one)
+#ifndef BM_SRC_ID
+#define BM_SRC_ID "unknown"
+#endif
+  std::snprintf(buf, sizeof buf, "bmpow %d gfx950 block=%d iters=%d src %s", BMPOW_ABI_VERSION, BM_BLOCK, BM_ITERS,
+                BM_SRC_ID);
   return buf;
 }
 

@@ -342,3 +342,24 @@ def test_sender_targets_match_the_reference_expressions(golden):
         t = targets.object_target(c['L'], c['ttl'], c['ntpb'], c['extra'])
         assert t == float.fromhex(c['target_float']), c
         assert int(t) == c['target']
+
+
+def test_library_identity_is_reproducible():
+    """The PMC counters' provenance (bench.py pmc_counters): the library's version names its sources
+    (BM_SRC_ID, an md5 of every source), not a build time, and the device-code md5
+    (tools/lib_code_md5.py, the .hip_fatbin section) is what `counters.stale` compares."""
+    import bench
+    from tools.lib_code_md5 import code_md5
+    path = _lib.lib_path()
+    if not os.path.exists(path):
+        pytest.skip('library not built')
+    lib = ctypes.CDLL(path)
+    lib.bmpow_version.restype = ctypes.c_char_p
+    v = lib.bmpow_version().decode()
+    assert re.search(r' src [0-9a-f]{12}', v) and 'built' not in v, v
+    md5 = code_md5(path)
+    assert md5 and re.fullmatch(r'[0-9a-f]{32}', md5) and code_md5(path) == md5
+    c = bench.pmc_counters()
+    assert c['benched_code_md5'] == md5 and isinstance(c['stale'], bool)
+    assert c['stale'] == (c['build'].get('code_md5', c['build'].get('lib_md5')) !=
+                          (md5 if c['build'].get('code_md5') else c['benched_lib_md5']))

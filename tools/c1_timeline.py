@@ -5,8 +5,8 @@
     python tools/c1_timeline.py D > timeline.json
 
 Each call of the single-object path (bmpow_host.hip search_one) launches bm_search1_kernel once per
-piece and window (one device: one launch per window; a split call: one per piece).  A launch starts a
-new call when it is issued after every search kernel launched before it has ended.  Per call:
+piece and window (one device: one launch per window; a split call: one per piece), in a burst; a launch
+more than 200 us after the previous launch call returned starts a new call.  Per call:
 
 * wall_us: first launch of the call to the first launch of the next call;
 * host_exposed_us: the part of wall_us in which none of the call's kernels ran -- the time the
@@ -25,6 +25,7 @@ import statistics
 import sys
 
 KERNEL = 'bm_search1_kernel'
+GAP_NS = 200000
 LAUNCH = ('hipLaunchKernel', 'hipExtLaunchKernel', 'hipModuleLaunchKernel')
 
 
@@ -69,14 +70,18 @@ def main():
     else:
         pairs = list(zip(launches[-len(search):], sorted(search, key=lambda k: k[0])))
     pairs.sort(key=lambda p: p[0][0])
-    # a launch issued after every earlier launch's kernel ended starts a new call
-    calls, cur, last_end = [], [], 0
+    # A call issues its launches in a burst (a window's pieces, and the window queued behind); calls
+    # are separated by at least a kernel's run.  A launch more than GAP_NS after the previous launch
+    # call returned starts a new call.  (A call whose first window ends without a hit launches its next
+    # window later and is counted as two calls: for the C1 object of the bench the answer lies in the
+    # first window.)
+    calls, cur, prev_end = [], [], None
     for a, k in pairs:
-        if cur and a[0] > last_end:
+        if cur and a[0] - prev_end > GAP_NS:
             calls.append(cur)
             cur = []
         cur.append((a, k))
-        last_end = max(last_end, k[1])
+        prev_end = a[1]
     if cur:
         calls.append(cur)
     out = []

@@ -4,7 +4,8 @@
     python tools/pmc_summary.py gpurun_out/pmc_r01 [trials_per_launch] > profiles/pmc_latest.json
 
 The summary is stamped with the build it measured ("build"): the md5 of the libbmpow_hip.so the GPU
-box ran (OUTDIR/lib.md5, written by tools/profile_pmc.sh), the library's version string from the
+box ran (OUTDIR/lib.md5, written by tools/profile_pmc.sh) and of its device code (OUTDIR/code.md5,
+tools/lib_code_md5.py: the .hip_fatbin section, reproduced by a rebuild), the library's version string from the
 bench line, and the git commit checked out here when summarising.
 
 Derived (MI355X_MICROARCH.md conventions):
@@ -94,6 +95,9 @@ def main():
     md5 = os.path.join(root, 'lib.md5')
     if os.path.exists(md5):
         build['lib_md5'] = open(md5).read().split()[0]
+    cmd5 = os.path.join(root, 'code.md5')  # the device code's md5 (tools/lib_code_md5.py): survives rebuilds
+    if os.path.exists(cmd5):
+        build['code_md5'] = open(cmd5).read().split()[0]
     for p in ['instr', 'kt']:
         bj = os.path.join(root, p + '.bench.json')
         if os.path.exists(bj):

@@ -13,6 +13,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 export BMPOW_ONE=0
 md5sum "${BMPOW_LIB:-pybitmessage_amd/lib/libbmpow_hip.so}" > "$OUT/lib.md5"
+python3 tools/lib_code_md5.py "${BMPOW_LIB:-pybitmessage_amd/lib/libbmpow_hip.so}" > "$OUT/code.md5"
 CMD=(python3 bench.py --config c3 --c3-log2 "$LOG2" --steps 1 --warmup 0 --no-cpu-baseline --step-trials 268435456)
 if [ -n "${PMC_DEFAULT_BENCH:-}" ]; then CMD=(python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline); fi
 pass() {
