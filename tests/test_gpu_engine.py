@@ -298,3 +298,48 @@ def test_long_run_leaves_the_cpu_alone(gpulib, shards):
         proofofwork.run(tg, x)  # re-checked with hashlib inside
     wall, used = time.perf_counter() - w0, cpu() - c0
     assert wall > 1.0 and used / wall < 0.1, (wall, used)
+
+
+def test_run_split_top_of_space_and_abort(gpulib, shards, run_split, coracle):
+    """Split run() (3 forced pieces) at the top of the nonce space -- windows clipped at 2^64 - 1, the
+    last nonce itself a hit, NOT_FOUND at the end -- and an abort from another thread during a long
+    split sweep: the call returns E_ABORTED within a window, and the next calls (whose launches queue
+    behind the aborted call's) are exact."""
+    import threading
+    shards([0, 0, 0])
+    run_split(True)
+    n, t = ctypes.c_uint64(), ctypes.c_uint64()
+    ih = hashlib.sha512(b'split top').digest()
+    top = U64 - 5000
+    # every nonce a hit: the first one is the answer
+    assert gpulib.bmpow_search(ih, U64, top, 1 << 20, ctypes.byref(n), ctypes.byref(t)) == _lib.FOUND
+    assert n.value == top and t.value == coracle.trial(top, ih)
+    # the first hit near the top, against the C oracle's scan of the same range
+    tg = U64 // 700
+    want = coracle.search(ih, tg, top)
+    rc = gpulib.bmpow_search(ih, tg, top, 1 << 20, ctypes.byref(n), ctypes.byref(t))
+    if want is None:
+        assert rc == _lib.NOT_FOUND
+    else:
+        assert rc == _lib.FOUND and (t.value, n.value) == tuple(want)
+    # no hit up to 2^64 - 1 (target 0): NOT_FOUND, every nonce of the clipped range hashed once
+    gpulib.bmpow_reset_stats()
+    assert gpulib.bmpow_search(ih, 0, top, 1 << 20, ctypes.byref(n), ctypes.byref(t)) == _lib.NOT_FOUND
+    st = _lib.BmpowStats()
+    gpulib.bmpow_get_stats(ctypes.byref(st))
+    assert st.trials == U64 - top + 1, st.trials
+    # abort a long split sweep from another thread
+    gpulib.bmpow_set_step_trials(1 << 26)
+    timer = threading.Timer(0.3, gpulib.bmpow_abort)
+    timer.start()
+    t0 = time.perf_counter()
+    rc = gpulib.bmpow_search(ih, 0, 1, 1 << 40, ctypes.byref(n), ctypes.byref(t))
+    took = time.perf_counter() - t0
+    timer.join()
+    gpulib.bmpow_clear_abort()
+    assert rc == _lib.E_ABORTED and took < 2.0, (rc, took)
+    rng = random.Random(3)
+    for _ in range(4):
+        x = rng.randbytes(64)
+        tg = U64 // rng.choice([5000, 300000])
+        assert proofofwork.run(tg, x) == list(coracle.search(x, tg))
