@@ -968,8 +968,8 @@ int wait_one(const Shard& sh, OnePath& op, uint64_t seq, bool spin) {
   return 0;
 }
 
-int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials, uint64_t* nonce_out,
-               uint64_t* trial_out) {
+int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials, uint64_t* nonce_out,
+                     uint64_t* trial_out) {
   const std::vector<size_t> pieces = one_pieces();
   const size_t P = pieces.size();
   for (size_t s : pieces) {
@@ -1132,6 +1132,16 @@ int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t m
     while (rc == 0 && want_next()) rc = launch();
     if (nfly == 0) return BMPOW_NOT_FOUND;
   }
+  return rc;
+}
+
+int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials, uint64_t* nonce_out,
+               uint64_t* trial_out) {
+  const int rc = search_one_calls(ih, target, start, max_trials, nonce_out, trial_out);
+  // A call that failed may have launched on only some pieces (or none): the pieces it skipped did not
+  // put the state of the call two ahead back to "no hit", which that call would then read.  Start the
+  // ring afresh (an abort comes only after every piece's first launch, so it keeps the ring).
+  if (rc < 0 && rc != BMPOW_E_ABORTED) free_one();
   return rc;
 }
 
