@@ -494,7 +494,8 @@ def one_path_desc(args, lib):
     if len(p) <= 1:
         return 'single-object (bm_search1_kernel)'
     return ('single-object split into %d pieces, one per %s (bm_search1_kernel + relay, cross-device bound)'
-            % (len(p), 'shard (forced, bmpow_set_run_split)' if args.run_split else 'device'))
+            % (len(p), 'shard (forced, bmpow_set_run_split; pieces sharing a GPU each on their own CU slice)'
+               if getattr(args, 'run_split', False) else 'device'))
 
 
 def run_c1_bench(args, dist):

@@ -82,6 +82,12 @@ OneWait g_one_wait = kOneAuto;
 // (tools/diag/one_cpu.py, profiles/r05/one_cpu.jsonl).
 int g_one_query = 8;
 bool g_one_event = true;
+// Forced pieces that share a device each run on their own slice of its CUs (a CU-masked stream, CUs
+// [j N / m, (j + 1) N / m) of the mask for piece j of m -- the mask's bits are dealt to the XCDs in turn,
+// so a slice holds N / 8m CUs of every XCD): the pieces then never compete for a SIMD, as pieces on
+// separate GPUs do not (tools/diag/cumask_probe.hip: 8 streams of 32 CUs each run side by side).
+// BMPOW_SPLIT_CUMASK=0 shares the whole device instead (A/B).
+bool g_split_cumask = true;
 bool g_one_enabled = true;
 
 // One of a shard's two engine launch buffers (the running launch and the one staged behind it).
@@ -370,6 +376,7 @@ int init_locked() {
     g_one_wait = std::strcmp(w, "spin") == 0 ? kOneSpin : std::strcmp(w, "sleep") == 0 ? kOneSleep : kOneAuto;
   if (const char* w = std::getenv("BMPOW_ONE_QUERY")) g_one_query = std::max(0, std::atoi(w));
   if (const char* w = std::getenv("BMPOW_ONE_EVENT")) g_one_event = std::atoi(w) != 0;
+  if (const char* w = std::getenv("BMPOW_SPLIT_CUMASK")) g_split_cumask = std::atoi(w) != 0;
   if (const char* w = std::getenv("BMPOW_ONE")) g_one_enabled = std::atoi(w) != 0;
   const auto vis = visible_gfx950();
   if (vis.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
@@ -859,6 +866,10 @@ struct OnePath {
   bm_one_out* h_out = nullptr;  // host-mapped ring of results
   bm_one_out* d_out = nullptr;  // the device's address of h_out
   unsigned long long* d_xone = nullptr;  // the cross-device table as this device maps it
+  hipStream_t stream = nullptr;  // the shard's stream, or (a forced piece sharing its device) its own
+  bool own_stream = false;       // a CU-masked stream of this piece's slice of the device
+  uint32_t cus = 0;              // CUs of that slice (0: the whole device)
+  uint32_t slice = 0, slices = 1;  // this piece's slice of its device, of `slices`
   hipEvent_t ev[8] = {};  // BMPOW_ONE_EVENT: recorded behind launch seq in ev[seq % 8]
   uint64_t seq = 0;
   double rate = 0;  // trials per ms, an exponential average over launches of >= 2^24 trials (0: none yet)
@@ -884,6 +895,10 @@ void free_one() {
     if (op.dev < 0) continue;
     (void)hipSetDevice(op.dev);
     if (s < g_shards.size() && g_shards[s].stream) (void)hipStreamSynchronize(g_shards[s].stream);
+    if (op.own_stream && op.stream) {
+      (void)hipStreamSynchronize(op.stream);
+      (void)hipStreamDestroy(op.stream);
+    }
     if (op.d_calls) (void)hipFree(op.d_calls);
     if (op.d_ctr) (void)hipFree(op.d_ctr);
     if (op.h_out) (void)hipHostFree(op.h_out);
@@ -895,12 +910,21 @@ void free_one() {
   g_xone = nullptr;
 }
 
-int ensure_one(size_t s) {
+int ensure_one(size_t s, uint32_t slice, uint32_t slices) {
   if (g_ones.size() != g_shards.size()) g_ones.resize(g_shards.size());
   OnePath& op = g_ones[s];
   const Shard& sh = g_shards[s];
-  if (op.dev == sh.dev && op.d_calls) return 0;
+  if (op.dev == sh.dev && op.d_calls && op.slice == slice && op.slices == slices) return 0;
   HIPTRY(hipSetDevice(sh.dev));
+  if (op.own_stream && op.stream) {  // another slice than before (the piece set changed)
+    (void)hipStreamSynchronize(op.stream);
+    (void)hipStreamDestroy(op.stream);
+  }
+  if (op.d_calls) (void)hipFree(op.d_calls);
+  if (op.d_ctr) (void)hipFree(op.d_ctr);
+  if (op.h_out) (void)hipHostFree(op.h_out);
+  for (hipEvent_t e : op.ev)
+    if (e) (void)hipEventDestroy(e);
   if (!g_xone) {
     HIPTRY(hipHostMalloc(&g_xone, sizeof(unsigned long long) * BM_MAX_SHARDS * BM_XSLOTS,
                          hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
@@ -908,6 +932,17 @@ int ensure_one(size_t s) {
   }
   op = OnePath();
   op.dev = sh.dev;
+  op.slice = slice;
+  op.slices = slices;
+  op.stream = sh.stream;
+  if (slices > 1 && g_split_cumask && sh.cus > 0) {
+    const uint32_t n = (uint32_t)sh.cus, lo = slice * n / slices, hi = (slice + 1) * n / slices;
+    std::vector<uint32_t> mask((n + 31) / 32, 0);
+    for (uint32_t cu = lo; cu < hi; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+    HIPTRY(hipExtStreamCreateWithCUMask(&op.stream, (uint32_t)mask.size(), mask.data()));
+    op.own_stream = true;
+    op.cus = hi - lo;
+  }
   bm_one_call init[BM_ONE_CALLS];
   std::memset(init, 0, sizeof init);
   for (bm_one_call& c : init) c.best = ~0ULL;
@@ -943,13 +978,13 @@ std::vector<size_t> one_pieces() {
 // thousand polls per second, each a load of host memory.  The launch's event is queried every few
 // polls, so a launch that ended without writing its result (a fault) is caught instead of waited for
 // forever.
-int wait_one(const Shard& sh, OnePath& op, uint64_t seq, bool spin) {
+int wait_one(OnePath& op, uint64_t seq, bool spin) {
   bm_one_out* o = &op.h_out[seq % BM_ONE_RING];
   const double t0 = now_ms();
   for (uint32_t k = 1;; ++k) {
     if (__atomic_load_n(&o->seq, __ATOMIC_ACQUIRE) == seq) break;
     if (spin ? k % 1024u == 0 : (g_one_query > 0 && k % (uint32_t)g_one_query == 0)) {
-      const hipError_t e = g_one_event ? hipEventQuery(op.ev[seq % 8]) : hipStreamQuery(sh.stream);
+      const hipError_t e = g_one_event ? hipEventQuery(op.ev[seq % 8]) : hipStreamQuery(op.stream);
       if (e == hipSuccess) {
         if (__atomic_load_n(&o->seq, __ATOMIC_ACQUIRE) == seq) break;
         return set_err(BMPOW_E_HIP, "single-object launch completed without its result");
@@ -972,8 +1007,14 @@ int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint
                      uint64_t* trial_out) {
   const std::vector<size_t> pieces = one_pieces();
   const size_t P = pieces.size();
-  for (size_t s : pieces) {
-    const int rc = ensure_one(s);
+  for (size_t p = 0; p < P; ++p) {
+    uint32_t slice = 0, slices = 0;  // this piece's place among the pieces on its device
+    for (size_t q = 0; q < P; ++q)
+      if (g_shards[pieces[q]].dev == g_shards[pieces[p]].dev) {
+        if (q < p) ++slice;
+        ++slices;
+      }
+    const int rc = ensure_one(pieces[p], slice, slices);
     if (rc < 0) return rc;
   }
   const uint64_t end = (max_trials - 1 > kU64Max - start) ? kU64Max : start + max_trials - 1;  // last nonce
@@ -995,14 +1036,19 @@ int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint
   bool shared = false;  // pieces share a device (bmpow_set_run_split)
   for (size_t p = 0; p < P; ++p) {
     const Shard& sh = g_shards[pieces[p]];
+    const OnePath& op = g_ones[pieces[p]];
     uint32_t same = 0;
     for (size_t q : pieces) same += g_shards[q].dev == sh.dev;
-    shared = shared || same > 1;
-    uint32_t c = sh.resident / std::min(same, hwq);
+    // a piece on its own CU slice owns that slice's resident workgroups; pieces sharing a whole device
+    // split its resident workgroups over the kernels that run at once
+    const bool sliced = op.cus > 0;
+    shared = shared || (same > 1 && !sliced);
+    const double part = sliced ? (double)op.cus / (double)std::max(1, sh.cus) : 1.0 / std::min(same, hwq);
+    uint32_t c = sliced ? (uint32_t)((uint64_t)sh.resident * op.cus / (uint32_t)std::max(1, sh.cus))
+                        : sh.resident / std::min(same, hwq);
     if (P > 1 && c > 1) --c;
     cap[p] = std::max<uint32_t>(1, std::min<uint32_t>(c, BM_ONE_MAX_WG));
-    const OnePath& op = g_ones[pieces[p]];
-    rate += (op.rate > 0 ? op.rate : kOneRateGuess) / std::min(same, hwq);
+    rate += (op.rate > 0 ? op.rate : kOneRateGuess * part);
   }
   // A window: one step per piece (a piece hashes ~1/P of it; bm_one_ctr.acc's trial field).  Pieces
   // that share a device do not all run at once (its hardware queues run 4 kernels; the rest start as
@@ -1073,8 +1119,8 @@ int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint
       a.out = op.d_out + r;
       f.seq[p] = a.seq;
       if (P > 1) HIPTRY(hipSetDevice(sh.dev));
-      HIPTRY(bm_launch_search1(sh.stream, a));
-      if (g_one_event) HIPTRY(hipEventRecord(op.ev[a.seq % 8], sh.stream));
+      HIPTRY(bm_launch_search1(op.stream, a));
+      if (g_one_event) HIPTRY(hipEventRecord(op.ev[a.seq % 8], op.stream));
     }
     ++nfly;
     if (room < step) top = true;
@@ -1090,11 +1136,10 @@ int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint
     uint64_t best = 0, best_trial = 0;
     double span = 0;
     for (size_t p = 0; p < P && rc == 0; ++p) {
-      const Shard& sh = g_shards[pieces[p]];
       OnePath& op = g_ones[pieces[p]];
       const uint64_t seq = fly[0].seq[p];
       const bool spin = g_one_wait == kOneSpin || (g_one_wait == kOneAuto && short_call);
-      rc = wait_one(sh, op, seq, spin);
+      rc = wait_one(op, seq, spin);
       if (rc < 0) break;
       const bm_one_out& o = op.h_out[seq % BM_ONE_RING];
       const double ms = (double)(o.t1 - o.t0) * 1e-5;  // s_memrealtime: 100 MHz

@@ -140,12 +140,11 @@ def test_c1_sweep_stops_within_rows_of_the_hit(gpulib, shards, golden, nshards, 
     favours older waves, so the columns drifted apart).  Shards sharing a device do not split run()
     (round 5), so 8 shards of this device behave as one.
 
-    Forced pieces on ONE device: each piece sweeps its interleaved columns of the same rows and stops at
-    the first hit of any through the cross-device bound, but the pieces' kernels share this device:
-    4 hardware queues (GPU_MAX_HW_QUEUES) run 4 pieces at once and the others start as those finish,
-    so a piece may run through its whole share of a window before the piece holding the answer starts.
-    Where pieces share a device, a window is therefore 2E (bmsched::expect_cap) rather than a step per
-    piece, and that bounds the waste.  On separate GPUs every piece runs from the start."""
+    Forced pieces on ONE device: each piece sweeps its interleaved columns of the same rows on its own
+    slice of the CUs (a CU-masked stream, as a separate smaller GPU) and stops at the first hit of any
+    through the cross-device bound.  Bound: one window's pieces run through at most their rows up to the
+    answer's, plus the pieces of the next window stopping at their first blocks (2E + rows also holds
+    with BMPOW_SPLIT_CUMASK=0, where the pieces share the whole device and a window is 2E)."""
     shards([0] * nshards)
     prev = gpulib.bmpow_set_run_split(1 if split else 0)
     k = [k for k in golden('first_nonce_kats.json')['kats'] if k['nonce'] == 10909138][0]

@@ -192,9 +192,9 @@ def run_pieces(lib):
 
 def test_run_split_over_pieces_exact(gpulib, shards, run_split, golden, coracle):
     """run() split into 2, 3 and 8 interleaved pieces (bmpow_set_run_split: one piece per shard, here
-    shards as streams of this device -- the multi-device path of round 5 rehearsed on one GPU: every
-    piece a bm_search1_kernel<true> launch with its relay, the cross-device bound in host-pinned
-    memory).  The golden C1 object (10,909,138), the test_openclpow vector (224,121,278), random
+    shards of this device, each piece on its own CU slice -- the multi-device path of round 5 rehearsed
+    on one GPU: every piece a bm_search1_kernel<true> launch with its relay, the cross-device bound in
+    host-pinned memory).  The golden C1 object (10,909,138), the test_openclpow vector (224,121,278), random
     objects against the C oracle, and bounded calls whose answer is the last nonce of the range or
     one past it."""
     kats = golden('first_nonce_kats.json')['kats']
