@@ -606,7 +606,9 @@ bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L) {
       const int x = c.xp->alloc(o, &b);
       if (x >= 0) {
         b.xs[o] = (uint8_t)(x + 1);
-        if (c.xreset) c.xreset((uint32_t)x);
+        // a fresh slot starts at the object's least hit so far, if any: pieces of a window holding it
+        // claimed after the object's previous slot went back stop at it, not at their window's end
+        if (c.xreset) c.xreset((uint32_t)x, b.hit[o] ? b.nonce[o] : kU64Max);
       }
     }
     bm_item it;
@@ -1329,8 +1331,8 @@ void Engine::stepper(size_t s) {
       std::vector<double> w;
       if (S_ > 1 && rates.weights(w)) c.weight = w[s];
       c.xp = &xp_;
-      c.xreset = [this](uint32_t x) {
-        if (ops_.xstore) ops_.xstore(x, kU64Max);
+      c.xreset = [this](uint32_t x, uint64_t v) {
+        if (ops_.xstore) ops_.xstore(x, v);
       };
       if (plan_launch(*b_, c, L)) {
         e.next ^= 1;

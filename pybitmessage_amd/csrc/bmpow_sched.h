@@ -247,7 +247,8 @@ struct PlanCtx {
   uint32_t resident = 0;     // columns a piece may get on this shard (0 = no cap)
   double weight = 1.0;       // the shard's rate over the mean (ShardRates)
   XPool* xp = nullptr;       // null: no cross-shard bound
-  std::function<void(uint32_t)> xreset;  // a slot was allocated: set it to UINT64_MAX in every row
+  // a slot was allocated: set it in every row to v (UINT64_MAX, or the object's least hit so far)
+  std::function<void(uint32_t, uint64_t)> xreset;
 };
 
 // Objects a launch may take a window or a piece from.
