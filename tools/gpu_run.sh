@@ -30,6 +30,7 @@
 #   c1-split:K       C1 with K shards on device 0, run() forced into K pieces (bmpow_set_run_split), 100 calls
 #   c3-split:K       C3 (2^34) with K forced pieces on device 0
 #   one-cpu          tools/diag/one_cpu.py: run()'s host CPU per wait configuration and per thread
+#   serial-wait:C:M  config C (c2 | c4 | c5) one run() call after another with BMPOW_WAIT1=M (auto | spin | sleep)
 #   c4-serial        8 C4 objects one after another through proofofwork.run (host CPU of a long serial call)
 #   c1c3-ab:V1,V2    tools/cmp_c1.sh over the variants (C1 40 calls + C3 2^35 each), same box
 #   c2-wait:MODE     bench-quick with BMPOW_WAIT=MODE (sleep | block | spin | poll): the steppers' CPU
@@ -66,6 +67,10 @@ for step in "$@"; do
       timeout -k 10 200 python3 bench.py --config c3 --c3-log2 34 --steps 1 --warmup 0 --no-cpu-baseline --devices 1 \
         --shards-per-device "$k" --run-split > "$OUT/c3_split_$k.json" 2> "$OUT/c3_split_$k.err" ;;
     one-cpu) timeout -k 10 300 python3 tools/diag/one_cpu.py 33 > "$OUT/one_cpu.jsonl" 2> "$OUT/one_cpu.err" ;;
+    serial-wait:*) IFS=: read -r _ cfg m <<< "$step"
+      n=0; while [ -e "$OUT/${cfg}_serial_${m}_$n.json" ]; do n=$((n + 1)); done
+      BMPOW_WAIT1=$m timeout -k 10 300 python3 bench.py --config "$cfg" --serial --steps 1 --warmup 2 --no-cpu-baseline --no-exact \
+        > "$OUT/${cfg}_serial_${m}_$n.json" 2> "$OUT/${cfg}_serial_${m}_$n.err" ;;
     c4-serial) timeout -k 10 300 python3 bench.py --config c4 --serial --objects 8 --steps 1 --warmup 1 --no-cpu-baseline \
         > "$OUT/c4_serial.json" 2> "$OUT/c4_serial.err" ;;
     c1c3-ab:*) timeout -k 10 900 bash tools/cmp_c1.sh "$OUT/c1c3_ab" $(echo "${step#c1c3-ab:}" | tr ',' ' ') \
