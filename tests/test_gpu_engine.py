@@ -225,8 +225,12 @@ def test_run_split_over_pieces_exact(gpulib, shards, run_split, golden, coracle)
         # every nonce a hit: the pieces' hit logs overflow and the trial is re-hashed on the device
         assert gpulib.bmpow_search(ih, U64, 1, 1 << 20, ctypes.byref(n), ctypes.byref(t)) == _lib.FOUND
         assert (n.value, t.value) == (1, coracle.trial(1, ih))
-        # the reference's own C export (bitmsghash.cpp:127), unchanged signature, through the pieces
+        # the reference's own C export (bitmsghash.cpp:127), unchanged signature, and the openclpow
+        # surface (do_opencl_pow, openclpow.py:77-111) through the pieces
         assert gpulib.BitmessagePOW(bytes.fromhex(c1['ih']), c1['target']) == c1['nonce']
+        from pybitmessage_amd import hippow
+        hippow.initCL()
+        assert hippow.do_opencl_pow(ocl['ih'], ocl['target']) == ocl['nonce']
 
 
 def test_run_split_small_windows_and_sweep(gpulib, shards, run_split, coracle):
