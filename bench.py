@@ -1231,12 +1231,16 @@ def pmc_counters():
     # md5 (the .hip_fatbin section, tools/lib_code_md5.py) is reproduced by a rebuild of the same
     # sources; the whole file's md5 is not (the host code carries the build time)
     from pybitmessage_amd import _lib
-    from tools.lib_code_md5 import code_md5
+    try:
+        from tools.lib_code_md5 import code_md5
+    except ImportError:  # (a tree without tools/: the whole file's md5 decides)
+        def code_md5(_path):
+            return None
     build = full.get('build') or {}
     out['benched_lib_md5'] = lib_md5(_lib.lib_path())
     out['benched_code_md5'] = code_md5(_lib.lib_path())
-    if build.get('code_md5'):
-        out['stale'] = out['benched_code_md5'] is None or build['code_md5'] != out['benched_code_md5']
+    if build.get('code_md5') and out['benched_code_md5']:
+        out['stale'] = build['code_md5'] != out['benched_code_md5']
     else:
         out['stale'] = out['benched_lib_md5'] is None or build.get('lib_md5') != out['benched_lib_md5']
     for k in ('valu_instr_per_trial', 'valu_issue_util', 'valu_instr_per_simd_quad_cycle', 'dual_issue_share',
