@@ -31,6 +31,8 @@
 #include <thread>
 #include <vector>
 
+#include <sched.h>
+
 #include "../../include/bmpow.h"
 #include "bmpow_kernels.h"
 #include "bmpow_sched.h"
@@ -82,6 +84,7 @@ OneWait g_one_wait = kOneAuto;
 // (tools/diag/one_cpu.py, profiles/r05/one_cpu.jsonl).
 int g_one_query = 8;
 bool g_one_event = true;
+bool g_spin_yield = true;  // BMPOW_SPIN_YIELD=0: a spinning wait never yields (A/B)
 // Forced pieces that share a device each run on their own slice of its CUs (a CU-masked stream, CUs
 // [j N / m, (j + 1) N / m) of the mask for piece j of m -- the mask's bits are dealt to the XCDs in turn,
 // so a slice holds N / 8m CUs of every XCD): the pieces then never compete for a SIMD, as pieces on
@@ -377,6 +380,7 @@ int init_locked() {
   if (const char* w = std::getenv("BMPOW_ONE_QUERY")) g_one_query = std::max(0, std::atoi(w));
   if (const char* w = std::getenv("BMPOW_ONE_EVENT")) g_one_event = std::atoi(w) != 0;
   if (const char* w = std::getenv("BMPOW_SPLIT_CUMASK")) g_split_cumask = std::atoi(w) != 0;
+  if (const char* w = std::getenv("BMPOW_SPIN_YIELD")) g_spin_yield = std::atoi(w) != 0;
   if (const char* w = std::getenv("BMPOW_ONE")) g_one_enabled = std::atoi(w) != 0;
   const auto vis = visible_gfx950();
   if (vis.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
@@ -992,7 +996,10 @@ int wait_one(OnePath& op, uint64_t seq, bool spin) {
       if (e != hipErrorNotReady) return set_err(BMPOW_E_HIP, std::string("single-object launch: ") + hipGetErrorString(e));
     }
     if (spin) {
-      __builtin_ia32_pause();
+      // a spinning wait still gives its CPU to any other runnable thread now and then (the reference's
+      // PoW threads run at SCHED_IDLE, bitmsghash.cpp:149: they never hold a CPU another thread wants)
+      if (g_spin_yield && (k & 63) == 0) sched_yield();
+      else __builtin_ia32_pause();
     } else {
       const double waited_us = (now_ms() - t0) * 1e3;
       std::this_thread::sleep_for(std::chrono::microseconds((int64_t)std::min(250.0, std::max(20.0, waited_us / 64))));
