@@ -349,3 +349,37 @@ def test_run_split_top_of_space_and_abort(gpulib, shards, run_split, coracle):
         x = rng.randbytes(64)
         tg = U64 // rng.choice([5000, 300000])
         assert proofofwork.run(tg, x) == list(coracle.search(x, tg))
+
+
+def test_run_split_every_first_nonce_kat_and_fuzz(gpulib, shards, run_split, golden, coracle):
+    """Every first-nonce KAT of the reference (tests/golden/first_nonce_kats.json: _doSafePoW answers,
+    the C1 object and the test_openclpow vector among them) through run() split into 5 forced pieces,
+    then a seeded fuzz of objects, targets, start nonces and call budgets over 2 to 7 pieces against the C
+    oracle's sequential search (bounded calls resumed where the previous one stopped, as _doCPoW's
+    caller would)."""
+    run_split(True)
+    shards([0] * 5)
+    for k in golden('first_nonce_kats.json')['kats']:
+        assert proofofwork.run(k['target'], bytes.fromhex(k['ih'])) == [k['trial'], k['nonce']], k['note']
+    rng = random.Random(2026)
+    n, t = ctypes.c_uint64(), ctypes.c_uint64()
+    for case in range(24):
+        shards([0] * rng.randint(2, 7))
+        ih = rng.randbytes(64)
+        e = rng.choice([2, 50, 900, 20000, 400000])
+        tg = U64 // e
+        start = rng.choice([1, 2, 1000, 1 << 32, U64 - 100000])
+        want = coracle.search(ih, tg, start)
+        # call budgets from one nonce up, at least E / 64 so a search takes at most a few hundred calls
+        budget = max(rng.choice([1, 300, 5000, 1 << 16, 1 << 22]), e // 64)
+        at, got = start, None
+        for _ in range(4096):
+            rc = gpulib.bmpow_search(ih, tg, at, budget, ctypes.byref(n), ctypes.byref(t))
+            assert rc in (_lib.FOUND, _lib.NOT_FOUND), (case, rc)
+            if rc == _lib.FOUND:
+                got = (t.value, n.value)
+                break
+            if at > U64 - budget:
+                break
+            at += budget
+        assert got == want, (case, start, budget, got, want)
