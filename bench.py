@@ -989,7 +989,7 @@ def main():
             raise SystemExit('--devices drives several GPUs from one process: run it without torch.distributed')
         os.environ['BMPOW_DEVICES'] = ','.join(str(i) for i in range(args.devices) for _ in range(args.shards_per_device))
     else:
-        os.environ['BMPOW_DEVICES'] = '0' if args.share_device else str(dist.local_rank)
+        os.environ['BMPOW_DEVICES'] = str(rank_device(dist, args.share_device))
     from pybitmessage_amd import _lib
     lib = _lib.get()
     if args.step_trials:
@@ -1054,6 +1054,23 @@ def device_pci_bus_id(lib, shard=0):
     if lib.bmpow_device_pci_bus_id(ids[shard], buf, 64) < 0:
         return None
     return buf.value.decode()
+
+
+def rank_device(dist, share=False, visible=None):
+    """The device ordinal this rank drives: its LOCAL_RANK among the visible gfx950 devices.  A launcher
+    that gives every rank one GPU of its own through HIP_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES leaves one
+    visible device per rank: then device 0 (that rank's own GPU).  --share-device: device 0 for every
+    rank (a rehearsal on one GPU)."""
+    if share:
+        return 0
+    if visible is None:
+        from pybitmessage_amd import _lib
+        visible = _lib.load().bmpow_device_count()  # counts without selecting (bmpow_init reads the choice)
+    if visible == 1 and dist.local_rank > 0:
+        return 0
+    if dist.local_rank >= max(visible, 1):
+        raise SystemExit('rank %d (local rank %d) has no GPU: %d visible' % (dist.rank, dist.local_rank, visible))
+    return dist.local_rank
 
 
 def summarize(args, dist, r, lib_version):

@@ -151,3 +151,16 @@ def test_single_rank_line_carries_the_round4_fields(monkeypatch):
     assert bench.single_object_path(types.SimpleNamespace(devices=1, shards_per_device=8))
     monkeypatch.setenv('BMPOW_ONE', '0')
     assert not bench.single_object_path(args)
+
+
+def test_rank_device_selection():
+    """Each rank drives its LOCAL_RANK's device; with one visible device per rank (a launcher that sets
+    HIP_VISIBLE_DEVICES per rank) every rank drives its own device 0; --share-device puts all on 0; a
+    rank without a GPU stops with a message."""
+    d = types.SimpleNamespace(rank=3, local_rank=3)
+    assert bench.rank_device(d, visible=8) == 3
+    assert bench.rank_device(d, visible=1) == 0
+    assert bench.rank_device(d, share=True, visible=8) == 0
+    assert bench.rank_device(types.SimpleNamespace(rank=0, local_rank=0), visible=1) == 0
+    with pytest.raises(SystemExit):
+        bench.rank_device(d, visible=2)
