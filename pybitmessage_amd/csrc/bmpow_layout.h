@@ -76,10 +76,11 @@ static_assert(sizeof(bm_item) == 48, "bm_item is 48 B");
 #define BM_XSLOTS 64
 #define BM_MAX_SHARDS 64
 
-// ---- the single-object path of run() (bmpow_search_len on one shard; bm_search1_kernel) ----
-// One launch per window of the object, the object's words in the kernel arguments, the next window
-// queued behind; the launch's last wave writes its result into host-mapped memory, so a call costs
-// one kernel launch per window and no copy, event or resolve kernel.
+// ---- the single-object path of run() (bmpow_search_len, any number of devices; bm_search1_kernel) ----
+// One launch per window of the object (per piece: one interleaved piece of each window per device), the
+// object's words in the kernel arguments, the next window queued behind; the launch's last workgroup
+// writes its result into host-mapped memory, so a call costs one kernel launch per window and piece and
+// no copy or resolve kernel.
 // Per call (a ring of BM_ONE_CALLS, slot c % BM_ONE_CALLS; every launch of call c puts slot
 // (c + 2) % BM_ONE_CALLS back to "no hit", which no launch in flight uses): the running minimum and
 // a log of the hits with their trial values (so the result needs no re-hash).
