@@ -1127,7 +1127,7 @@ def summarize(args, dist, r, lib_version):
             'avg_launch_ms': round(kernel_ms / max(launches, 1), 3), 'launches': int(launches),
             'kernel_busy_frac': round(kernel_ms * 1e-3 / r['elapsed'], 4),
         }
-        pmc = pmc_counters()
+        pmc = pmc_counters(r.get('kernel', 'bm_search_kernel'))
         if pmc:
             # PMC bytes per 2^28-trial launch, scaled to this run's launches (the traffic -- the block
             # queue's atomics and the item loads -- grows with the trials a launch hashes)
@@ -1228,21 +1228,28 @@ def lib_md5(path):
         return None
 
 
-def pmc_counters():
+def pmc_counters(kernel='bm_search_kernel'):
     """bm_search_kernel's hardware counters from the committed rocprofv3 PMC passes
     (tools/profile_pmc.sh -> tools/pmc_summary.py -> profiles/pmc_latest.json; C3 launches of 2^28
     trials, one counter group per pass): HBM bytes per launch = FETCH_SIZE doubled (gfx950
     under-count, MI355X_MICROARCH.md section HBM) + WRITE_SIZE -- the algorithmic traffic is ~0 (9
     words per workgroup) --, and the VALU issue figures (SQ_ACTIVE_INST_VALU / _VALU2 per SIMD
     quad-cycle)."""
-    path = os.path.join(ROOT, 'profiles', 'pmc_latest.json')
+    # run()'s bm_search1_kernel has its own passes (tools/profile_pmc.sh with PMC_ONE=1), when committed
+    name = 'pmc_one_latest.json' if kernel == 'bm_search1_kernel' else 'pmc_latest.json'
+    path = os.path.join(ROOT, 'profiles', name)
     if not os.path.exists(path):
-        return None
+        if name == 'pmc_latest.json':
+            return None
+        name, kernel = 'pmc_latest.json', 'bm_search_kernel'
+        path = os.path.join(ROOT, 'profiles', name)
+        if not os.path.exists(path):
+            return None
     with open(path) as f:
         full = json.load(f)
     d = full['derived']
     out = {'traffic': d.get('hbm_bytes_per_launch_upper'),
-           'source': 'profiles/pmc_latest.json (bm_search_kernel, C3, 2^28-trial launches)',
+           'source': 'profiles/%s (%s, C3, 2^28-trial launches)' % (name, kernel),
            'build': full.get('build'), 'trials_per_launch': full.get('raw', {}).get('trials_per_launch')}
     # provenance: were the counters collected on the device code this run loaded?  The device code's
     # md5 (the .hip_fatbin section, tools/lib_code_md5.py) is reproduced by a rebuild of the same

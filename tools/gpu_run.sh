@@ -16,6 +16,8 @@
 #   rocprof-bench    rocprofv3 --kernel-trace --stats over the default bench (3 steps)
 #   c1-split-trace:K the same with K forced pieces (the multi-device call's host timeline, rehearsed)
 #   pmc              tools/profile_pmc.sh OUT/pmc (C3 2^33, one counter group per pass)
+#   pmc-one          the same passes for run()'s bm_search1_kernel (OUT/pmc_one; PMC_KERNEL=bm_search1_kernel
+#                    tools/pmc_summary.py -> profiles/pmc_one_latest.json)
 #   pmc:V            the same with the variant build variants/<name> (OUT/pmc_<name>)
 #   shard-latency    tools/shard_latency.py
 #   c1-columns       tools/diag/c1_columns.py (C1 waste by column count)
@@ -108,6 +110,7 @@ for step in "$@"; do
         > "$OUT/c1_split_trace_$k.json" 2> "$OUT/c1_split_trace_$k.err" &&
       python3 tools/c1_timeline.py "$OUT/c1_split_trace_$k" > "$OUT/c1_split_timeline_$k.json" ;;
     pmc) bash tools/profile_pmc.sh "$OUT/pmc" 33 > "$OUT/pmc.log" 2>&1 ;;
+    pmc-one) PMC_ONE=1 bash tools/profile_pmc.sh "$OUT/pmc_one" 33 > "$OUT/pmc_one.log" 2>&1 ;;
     pmc:*) v=${step#pmc:}; BMPOW_LIB=$v/libbmpow_hip.so bash tools/profile_pmc.sh "$OUT/pmc_$(basename "$v")" 33 \
              > "$OUT/pmc_$(basename "$v").log" 2>&1 ;;
     shard-latency) timeout -k 10 200 python3 tools/shard_latency.py > "$OUT/shard_latency.json" 2> "$OUT/shard_latency.err" ;;

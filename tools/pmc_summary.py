@@ -27,7 +27,7 @@ import os
 import subprocess
 import sys
 
-KERNEL = 'bm_search_kernel'
+KERNEL = os.environ.get('PMC_KERNEL', 'bm_search_kernel')  # bm_search1_kernel: run()'s kernel (PMC_ONE)
 
 
 def load(path):

@@ -11,7 +11,8 @@ OUT=${1:?outdir}
 LOG2=${2:-33}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-export BMPOW_ONE=0
+# PMC_ONE=1: run()'s single-object kernel (bm_search1_kernel) on the same sweep instead
+if [ -n "${PMC_ONE:-}" ]; then export BMPOW_ONE=1; else export BMPOW_ONE=0; fi
 md5sum "${BMPOW_LIB:-pybitmessage_amd/lib/libbmpow_hip.so}" > "$OUT/lib.md5"
 python3 tools/lib_code_md5.py "${BMPOW_LIB:-pybitmessage_amd/lib/libbmpow_hip.so}" > "$OUT/code.md5"
 CMD=(python3 bench.py --config c3 --c3-log2 "$LOG2" --steps 1 --warmup 0 --no-cpu-baseline --step-trials 268435456)
