@@ -175,7 +175,8 @@ def iter_batch(objects, step_trials=0):
     and small ones packed many per launch -- without ever waiting on this interpreter's GIL.  This
     generator pops the finished objects (``bmpow_service_poll``, GIL released while it waits; the
     library re-hashes each found nonce on the host there, ``BMPOW_SERVICE_VERIFY``) and yields
-    them while the next step runs.  ``state.shutdown`` is
+    them while the next step runs.  A single object takes :func:`run`'s single-object path instead
+    (no service to set up; re-checked with hashlib as :func:`run` does).  ``state.shutdown`` is
     polled at least every 100 ms and raises :class:`PowInterrupted`; closing the generator stops
     the service after its current step."""
     import numpy as np
@@ -196,6 +197,16 @@ def iter_batch(objects, step_trials=0):
             raise ValueError('object %d has a negative target: no nonce can satisfy it' % i)
         targets[i] = t
     ihs = bytes(ihs)
+    if n == 1:
+        # One object -- the common case of a send (its ack, then its msg): run()'s single-object path
+        # (one launch per window and device, the result in host-mapped memory) rather than a service
+        # thread and a resident session set up for one object.  Same answer, same shutdown behaviour.
+        try:
+            tv, nonce = _doHIPPoW(int(targets[0]), ihs)
+        except StopIteration:
+            raise PowInterrupted()
+        yield 0, tv, nonce
+        return
     var = len(ihs) != 64 * n or any(b - a != 64 for a, b in zip(offs, offs[1:]))
     p64 = ctypes.POINTER(ctypes.c_uint64)
     s = lib.bmpow_service_create(step_trials, _lib.SERVICE_VERIFY if VERIFY else 0)

@@ -56,6 +56,7 @@ class BatchLib(object):
         self.services = []
         self.fail_step = False
         self.bad_tickets = set()
+        self.single_calls = 0
 
     def bmpow_batch_create(self, n, ihs, tg, start):
         h = self.next_handle
@@ -217,6 +218,15 @@ class BatchLib(object):
     def bmpow_last_error(self):
         return b'injected step failure' if self.fail_step else b''
 
+    def bmpow_search_len(self, ih, ih_len, target, start, max_trials, nonce_out, trial_out):
+        """run()'s bounded single-object search (the one-object batch takes it), by the C oracle."""
+        self.single_calls += 1
+        r = self.co.search(bytes(ih[:ih_len]), target, start, max_trials)
+        if r is None:
+            return _lib.NOT_FOUND
+        trial_out._obj.value, nonce_out._obj.value = r
+        return _lib.FOUND
+
 
 @pytest.fixture
 def batchlib(monkeypatch, coracle):
@@ -336,7 +346,7 @@ def test_iter_batch_stepping_thread(batchlib, coracle):
     next(gen)
     gen.close()  # the stepping thread stops and the session is destroyed
     assert not batchlib.sessions
-    hard = [(0, rng.randbytes(64))]  # never found
+    hard = [(0, rng.randbytes(64)), (0, rng.randbytes(64))]  # never found (two: the service path)
     timer = threading.Timer(0.2, lambda: setattr(state, 'shutdown', 1))
     timer.start()
     try:
@@ -350,6 +360,24 @@ def test_iter_batch_stepping_thread(batchlib, coracle):
     with pytest.raises(_lib.BmpowError, match='object 1: .*re-check'):
         proofofwork.run_batch(objs[:3])
     assert not batchlib.sessions
+
+
+def test_one_object_batch_takes_the_single_object_path(batchlib, coracle):
+    """run_batch / iter_batch / pow_objects of ONE object use run()'s bounded single-object search
+    (bmpow_search_len), not a service and a session set up for one object; the answer is the same."""
+    rng = random.Random(5)
+    t, ih = U64 // 900, rng.randbytes(64)
+    assert proofofwork.run_batch([(t, ih)]) == [list(coracle.search(ih, t))]
+    assert batchlib.single_calls == 1 and not batchlib.services and not batchlib.sessions
+    assert list(proofofwork.iter_batch([(t, ih)])) == [(0,) + tuple(coracle.search(ih, t))]
+    with pytest.raises(ValueError):
+        list(proofofwork.iter_batch([(-1, ih)]))
+    state.shutdown = 1
+    try:
+        with pytest.raises(RuntimeError):
+            proofofwork.run_batch([(t, ih)])
+    finally:
+        state.shutdown = 0
 
 
 def test_powservice_submit_many(batchlib, coracle):
