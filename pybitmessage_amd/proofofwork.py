@@ -46,6 +46,8 @@ U64_MAX = _lib.U64_MAX
 #: trials per bounded ``bmpow_search`` call from ``run``: a few steps of the scheduler
 #: (~0.1-0.3 s on one MI355X), i.e. the shutdown-poll interval of the Python loop.
 CALL_TRIALS = 1 << 30
+#: a batch of one object takes run()'s single-object path (iter_batch); False sends it to the service (A/B)
+BATCH_ONE = True
 #: re-check every returned nonce on the host, as ``_doGPUPoW`` does with hashlib (``:176-190``):
 #: hashlib here for ``run``; the library's OpenSSL SHA-512 (``BMPOW_SERVICE_VERIFY``) for batches
 VERIFY = True
@@ -197,7 +199,7 @@ def iter_batch(objects, step_trials=0):
             raise ValueError('object %d has a negative target: no nonce can satisfy it' % i)
         targets[i] = t
     ihs = bytes(ihs)
-    if n == 1:
+    if n == 1 and BATCH_ONE:
         # One object -- the common case of a send (its ack, then its msg): run()'s single-object path
         # (one launch per window and device, the result in host-mapped memory) rather than a service
         # thread and a resident session set up for one object.  Same answer, same shutdown behaviour.
