@@ -32,6 +32,7 @@
 #   c1-split:K       C1 with K shards on device 0, run() forced into K pieces (bmpow_set_run_split), 100 calls
 #   c3-split:K       C3 (2^34) with K forced pieces on device 0
 #   cpu-share        tools/diag/cpu_share.py: a spinning run() beside a CPU-bound thread on the same CPU
+#   service-overhead tools/diag/service_overhead.py: the fixed cost per batch of the library's service
 #   batch-one        tools/diag/batch_one.py: run_batch of one C1 object, single-object path vs the service
 #   one-cpu          tools/diag/one_cpu.py: run()'s host CPU per wait configuration and per thread
 #   serial-wait:C:M  config C (c2 | c4 | c5) one run() call after another with BMPOW_WAIT1=M (auto | spin | sleep)
@@ -71,6 +72,8 @@ for step in "$@"; do
       timeout -k 10 200 python3 bench.py --config c3 --c3-log2 34 --steps 1 --warmup 0 --no-cpu-baseline --devices 1 \
         --shards-per-device "$k" --run-split > "$OUT/c3_split_$k.json" 2> "$OUT/c3_split_$k.err" ;;
     cpu-share) timeout -k 10 300 python3 tools/diag/cpu_share.py 5 > "$OUT/cpu_share.json" 2> "$OUT/cpu_share.err" ;;
+    service-overhead) timeout -k 10 300 python3 tools/diag/service_overhead.py 50 2 > "$OUT/service_overhead.json" 2> "$OUT/service_overhead.err" &&
+      BMPOW_DEVICES=0,0,0,0 timeout -k 10 300 python3 tools/diag/service_overhead.py 50 2 > "$OUT/service_overhead_4shards.json" 2>> "$OUT/service_overhead.err" ;;
     batch-one) timeout -k 10 300 python3 tools/diag/batch_one.py 100 > "$OUT/batch_one.json" 2> "$OUT/batch_one.err" ;;
     one-cpu) timeout -k 10 300 python3 tools/diag/one_cpu.py 33 > "$OUT/one_cpu.jsonl" 2> "$OUT/one_cpu.err" ;;
     serial-wait:*) IFS=: read -r _ cfg m <<< "$step"
