@@ -383,3 +383,36 @@ def test_run_split_every_first_nonce_kat_and_fuzz(gpulib, shards, run_split, gol
                 break
             at += budget
         assert got == want, (case, start, budget, got, want)
+
+
+def test_serial_runs_beside_a_running_service(gpulib, shards, run_split, coracle):
+    """The worker thread's batches and the API thread's serial run() calls at once (class_singleWorker.py
+    :236, api.py:1304): a PowService solving 48 objects on the engine while two threads make run() calls
+    -- single-object launches queued on the same shard streams as the engine's, with one and with 3
+    forced pieces.  Every answer exact."""
+    import threading
+    from pybitmessage_amd import worker
+    rng = random.Random(404)
+    for layout, split in (([0, 0], False), ([0, 0, 0], True)):
+        shards(layout)
+        run_split(split)
+        batch = [(U64 // rng.choice([3000, 70000, 900000]), rng.randbytes(64)) for _ in range(48)]
+        serial = [[(U64 // rng.choice([50, 5000, 200000]), rng.randbytes(64)) for _ in range(8)] for _ in range(2)]
+        got = [None, None]
+
+        def caller(k):
+            got[k] = [proofofwork.run(t, ih) for t, ih in serial[k]]
+        svc = worker.PowService().start()
+        try:
+            futs = svc.submit_many(batch)
+            th = [threading.Thread(target=caller, args=(k,)) for k in range(2)]
+            for x in th:
+                x.start()
+            res = [f.result(timeout=120) for f in futs]
+            for x in th:
+                x.join(120)
+        finally:
+            svc.stop(30)
+        assert [list(r) for r in res] == [list(coracle.search(ih, t)) for t, ih in batch], layout
+        for k in range(2):
+            assert got[k] == [list(coracle.search(ih, t)) for t, ih in serial[k]], (layout, k)
