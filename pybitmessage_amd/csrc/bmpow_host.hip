@@ -92,6 +92,17 @@ bool g_spin_yield = true;  // BMPOW_SPIN_YIELD=0: a spinning wait never yields (
 // BMPOW_SPLIT_CUMASK=0 shares the whole device instead (A/B).
 bool g_split_cumask = true;
 bool g_one_enabled = true;
+// BMPOW_TRACE=1: the single-object path's set-up and tear-down steps on stderr, with the state of every
+// stream they wait on (a diagnostic; tools/diag/rss_layout.py).
+bool g_trace = false;
+#define BM_TRACE(...)                                                      \
+  do {                                                                     \
+    if (g_trace) {                                                         \
+      std::fprintf(stderr, "[bmpow %.3f] ", now_ms());                     \
+      std::fprintf(stderr, __VA_ARGS__);                                   \
+      std::fputc('\n', stderr);                                            \
+    }                                                                      \
+  } while (0)
 
 // One of a shard's two engine launch buffers (the running launch and the one staged behind it).
 struct LaunchBuf {
@@ -382,6 +393,7 @@ int init_locked() {
   if (const char* w = std::getenv("BMPOW_SPLIT_CUMASK")) g_split_cumask = std::atoi(w) != 0;
   if (const char* w = std::getenv("BMPOW_SPIN_YIELD")) g_spin_yield = std::atoi(w) != 0;
   if (const char* w = std::getenv("BMPOW_ONE")) g_one_enabled = std::atoi(w) != 0;
+  if (const char* w = std::getenv("BMPOW_TRACE")) g_trace = std::atoi(w) != 0;
   const auto vis = visible_gfx950();
   if (vis.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
   std::vector<int> ids = vis;
@@ -870,8 +882,8 @@ struct OnePath {
   bm_one_out* h_out = nullptr;  // host-mapped ring of results
   bm_one_out* d_out = nullptr;  // the device's address of h_out
   unsigned long long* d_xone = nullptr;  // the cross-device table as this device maps it
-  hipStream_t stream = nullptr;  // the shard's stream, or (a forced piece sharing its device) its own
-  bool own_stream = false;       // a CU-masked stream of this piece's slice of the device
+  hipStream_t stream = nullptr;  // the shard's stream, or (a forced piece sharing its device) a masked one
+  bool masked = false;           // stream is the CU-masked stream of this piece's slice (masked_stream)
   uint32_t cus = 0;              // CUs of that slice (0: the whole device)
   uint32_t slice = 0, slices = 1;  // this piece's slice of its device, of `slices`
   hipEvent_t ev[8] = {};  // BMPOW_ONE_EVENT: recorded behind launch seq in ev[seq % 8]
@@ -893,16 +905,57 @@ constexpr double kOneSpinMs = 20.0;
 // a piece's rate before it has a sample: one MI355X's bm_search1_kernel, measured
 constexpr double kOneRateGuess = 6.5e6;
 
+// CU-masked streams, one per (device, CU range), created on first use and kept for the life of the
+// process.  On this ROCm (7.2) creating a masked stream after masked streams were destroyed hangs inside
+// hipExtStreamCreateWithCUMask -- the second creation after three were destroyed, every time
+// (tools/diag/cumask_free.hip, profiles/r05/cumask_free/) -- while creating many and destroying none
+// does not.  So the library never destroys one; a forced split reuses its slices' streams, and past
+// kMaxMasked distinct ranges a piece runs on its shard's stream unmasked.  (Each holds a hardware queue
+// and ~190 MiB of host memory in the runtime: tools/diag/rss_layout.py.)
+struct MaskedStream {
+  int dev;
+  uint32_t lo, hi;
+  hipStream_t stream;
+};
+std::vector<MaskedStream> g_masked;
+constexpr size_t kMaxMasked = 24;
+
+// The stream of CUs [lo, hi) of device dev (n CUs), or null once kMaxMasked ranges exist.
+int masked_stream(int dev, uint32_t n, uint32_t lo, uint32_t hi, hipStream_t* out) {
+  *out = nullptr;
+  for (const MaskedStream& m : g_masked)
+    if (m.dev == dev && m.lo == lo && m.hi == hi) {
+      *out = m.stream;
+      return 0;
+    }
+  if (g_masked.size() >= kMaxMasked) return 0;
+  std::vector<uint32_t> mask((n + 31) / 32, 0);
+  for (uint32_t cu = lo; cu < hi; ++cu) mask[cu / 32] |= 1u << (cu % 32);
+  hipStream_t st = nullptr;
+  HIPTRY(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()));
+  g_masked.push_back({dev, lo, hi, st});
+  BM_TRACE("masked stream %zu: dev %d CUs [%u, %u) stream %p", g_masked.size() - 1, dev, lo, hi, (void*)st);
+  *out = st;
+  return 0;
+}
+
 void free_one() {
+  // every stream a piece launched on drains before any buffer is freed (hipFree waits for the device)
   for (size_t s = 0; s < g_ones.size(); ++s) {
     OnePath& op = g_ones[s];
     if (op.dev < 0) continue;
     (void)hipSetDevice(op.dev);
+    BM_TRACE("free_one: piece %zu dev %d masked %d: stream %s, shard stream %s", s, op.dev, (int)op.masked,
+             op.stream ? hipGetErrorName(hipStreamQuery(op.stream)) : "-",
+             s < g_shards.size() && g_shards[s].stream ? hipGetErrorName(hipStreamQuery(g_shards[s].stream)) : "-");
     if (s < g_shards.size() && g_shards[s].stream) (void)hipStreamSynchronize(g_shards[s].stream);
-    if (op.own_stream && op.stream) {
-      (void)hipStreamSynchronize(op.stream);
-      (void)hipStreamDestroy(op.stream);
-    }
+    if (op.masked && op.stream) (void)hipStreamSynchronize(op.stream);
+  }
+  BM_TRACE("free_one: streams drained");
+  for (size_t s = 0; s < g_ones.size(); ++s) {
+    OnePath& op = g_ones[s];
+    if (op.dev < 0) continue;
+    (void)hipSetDevice(op.dev);
     if (op.d_calls) (void)hipFree(op.d_calls);
     if (op.d_ctr) (void)hipFree(op.d_ctr);
     if (op.h_out) (void)hipHostFree(op.h_out);
@@ -912,6 +965,7 @@ void free_one() {
   g_ones.clear();
   if (g_xone) (void)hipHostFree(g_xone);
   g_xone = nullptr;
+  BM_TRACE("free_one: done");
 }
 
 int ensure_one(size_t s, uint32_t slice, uint32_t slices) {
@@ -920,10 +974,7 @@ int ensure_one(size_t s, uint32_t slice, uint32_t slices) {
   const Shard& sh = g_shards[s];
   if (op.dev == sh.dev && op.d_calls && op.slice == slice && op.slices == slices) return 0;
   HIPTRY(hipSetDevice(sh.dev));
-  if (op.own_stream && op.stream) {  // another slice than before (the piece set changed)
-    (void)hipStreamSynchronize(op.stream);
-    (void)hipStreamDestroy(op.stream);
-  }
+  if (op.masked && op.stream) (void)hipStreamSynchronize(op.stream);  // another slice than before
   if (op.d_calls) (void)hipFree(op.d_calls);
   if (op.d_ctr) (void)hipFree(op.d_ctr);
   if (op.h_out) (void)hipHostFree(op.h_out);
@@ -941,11 +992,16 @@ int ensure_one(size_t s, uint32_t slice, uint32_t slices) {
   op.stream = sh.stream;
   if (slices > 1 && g_split_cumask && sh.cus > 0) {
     const uint32_t n = (uint32_t)sh.cus, lo = slice * n / slices, hi = (slice + 1) * n / slices;
-    std::vector<uint32_t> mask((n + 31) / 32, 0);
-    for (uint32_t cu = lo; cu < hi; ++cu) mask[cu / 32] |= 1u << (cu % 32);
-    HIPTRY(hipExtStreamCreateWithCUMask(&op.stream, (uint32_t)mask.size(), mask.data()));
-    op.own_stream = true;
-    op.cus = hi - lo;
+    hipStream_t st = nullptr;
+    const int rc = masked_stream(sh.dev, n, lo, hi, &st);
+    if (rc < 0) return rc;
+    if (st) {
+      op.stream = st;
+      op.masked = true;
+      op.cus = hi - lo;
+    }
+    BM_TRACE("ensure_one: piece %zu dev %d slice %u/%u: CUs [%u, %u) stream %p", s, sh.dev, slice, slices, lo, hi,
+             (void*)op.stream);
   }
   bm_one_call init[BM_ONE_CALLS];
   std::memset(init, 0, sizeof init);

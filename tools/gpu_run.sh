@@ -35,6 +35,9 @@
 #   service-overhead tools/diag/service_overhead.py: the fixed cost per batch of the library's service
 #   batch-one        tools/diag/batch_one.py: run_batch of one C1 object, single-object path vs the service
 #   one-cpu          tools/diag/one_cpu.py: run()'s host CPU per wait configuration and per thread
+#   soak:S           tests/test_gpu_soak.py for S seconds (every entry point at once, 4 shard layouts)
+#   rss-layout       tools/diag/rss_layout.py (host RSS per shard layout / forced split)
+#   cumask-free:M    tools/diag/cumask_free mode M (re-creating CU-masked streams: drain | serial | drain-sync | drain-sleep | reuse)
 #   serial-wait:C:M  config C (c2 | c4 | c5) one run() call after another with BMPOW_WAIT1=M (auto | spin | sleep)
 #   c4-serial        8 C4 objects one after another through proofofwork.run (host CPU of a long serial call)
 #   c1c3-ab:V1,V2    tools/cmp_c1.sh over the variants (C1 40 calls + C3 2^35 each), same box
@@ -71,6 +74,11 @@ for step in "$@"; do
     c3-split:*) k=${step#c3-split:}
       timeout -k 10 200 python3 bench.py --config c3 --c3-log2 34 --steps 1 --warmup 0 --no-cpu-baseline --devices 1 \
         --shards-per-device "$k" --run-split > "$OUT/c3_split_$k.json" 2> "$OUT/c3_split_$k.err" ;;
+    soak:*) sk=${step#soak:}; BMPOW_SOAK_S=$sk timeout -k 10 $((sk * 2 + 300)) "${PYT[@]}" --timeout $((sk * 2 + 240)) -s \
+        tests/test_gpu_soak.py > "$OUT/soak_$sk.log" 2>&1 ;;
+    rss-layout) BMPOW_TRACE=1 timeout -k 10 120 python3 tools/diag/rss_layout.py > "$OUT/rss_layout.jsonl" 2> "$OUT/rss_layout.err" ;;
+    cumask-free:*) cm=${step#cumask-free:}; timeout -k 10 60 ./tools/diag/cumask_free 3 "${CF_ITERS:-20}" "$cm" >> "$OUT/cumask_free.jsonl" \
+        2> "$OUT/cumask_free_$cm.err" ;;
     cpu-share) timeout -k 10 300 python3 tools/diag/cpu_share.py 5 > "$OUT/cpu_share.json" 2> "$OUT/cpu_share.err" ;;
     service-overhead) timeout -k 10 300 python3 tools/diag/service_overhead.py 50 2 > "$OUT/service_overhead.json" 2> "$OUT/service_overhead.err" &&
       BMPOW_DEVICES=0,0,0,0 timeout -k 10 300 python3 tools/diag/service_overhead.py 50 2 > "$OUT/service_overhead_4shards.json" 2>> "$OUT/service_overhead.err" ;;
