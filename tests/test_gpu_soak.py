@@ -6,7 +6,11 @@ layout changing between phases -- the way a long-running node uses the library.
 * two threads make serial run() calls (api.py:1304,1350 and the worker's ack-then-msg,
   class_singleWorker.py:236,1276) -- run()'s single-object path, split into pieces where the phase
   forces it;
-* one thread calls run_batch on small batches (a fresh service per call beside the long-lived one).
+* one thread calls run_batch on small batches (a fresh service per call beside the long-lived one);
+* one thread verifies batches of received objects (isProofOfWorkSufficient_batch, the receive side,
+  protocol.py:258-286): objects given a valid nonce by run_batch at the network difficulty, the same
+  with one payload byte changed, and objects with random nonces, each verdict against targets.py's
+  per-object restatement.
 
 Phases, run three times over: one shard; two shards sharing the device (objects nonce-sharded between them,
 cross-shard bound slots in use); three forced run() pieces on CU slices; four shards.  Every answer is
@@ -19,6 +23,7 @@ rings and staging buffers) and the HIP runtime's high-water marks, set in the fi
 """
 import ctypes
 import gc
+import hashlib
 import os
 import queue
 import random
@@ -51,7 +56,7 @@ def _object(rng):
 
 
 def test_soak_every_entry_point_at_once(gpulib, shards, run_split, coracle):  # noqa: F811
-    from pybitmessage_amd import proofofwork, worker
+    from pybitmessage_amd import proofofwork, targets, verify, worker
     phases = PHASES * 3
     per = SOAK_S / len(phases)
     rss = []
@@ -60,7 +65,7 @@ def test_soak_every_entry_point_at_once(gpulib, shards, run_split, coracle):  # 
         run_split(split)
         stop = threading.Event()
         todo = queue.Queue()
-        counts = {'service': 0, 'serial': 0, 'batch': 0}
+        counts = {'service': 0, 'serial': 0, 'batch': 0, 'verify': 0, 'valid': 0}
         stats = {'minimal': 0, 'valid_only': 0}
         bad, crashed = [], []
         lock = threading.Lock()
@@ -99,6 +104,30 @@ def test_soak_every_entry_point_at_once(gpulib, shards, run_split, coracle):  # 
                 for (t, ih), r in zip(objs, proofofwork.run_batch(objs)):
                     put('batch', t, ih, r)
 
+        @guard
+        def verify_loop(rng):
+            while not stop.is_set():
+                now = int(time.time())
+                # a few objects given a valid nonce by run_batch (TTL 300 s, network difficulty), the
+                # same with a payload byte changed, and objects with random nonces
+                made = [(now + 300).to_bytes(8, 'big') + rng.randbytes(rng.randint(8, 200))
+                        for _ in range(rng.randint(1, 4))]
+                sol = proofofwork.run_batch([(int(targets.object_target(len(m), 300)), hashlib.sha512(m).digest())
+                                             for m in made])
+                good = [nonce.to_bytes(8, 'big') + m for (_, nonce), m in zip(sol, made)]
+                bent = [o[:-1] + bytes([o[-1] ^ 1]) for o in good]
+                junk = [rng.randbytes(8) + (now + rng.randint(-3600, 30000)).to_bytes(8, 'big')
+                        + rng.randbytes(rng.randint(6, 1000)) for _ in range(rng.randint(1, 512))]
+                objs = good + bent + junk
+                rng.shuffle(objs)
+                got = verify.isProofOfWorkSufficient_batch(objs, 0, 0, now)
+                want = [targets.isProofOfWorkSufficient(o, 0, 0, now) for o in objs]
+                if got != want or not all(targets.isProofOfWorkSufficient(o, 0, 0, now) for o in good):
+                    bad.append(('verify', [i for i, (a, b) in enumerate(zip(got, want)) if a != b][:4]))
+                with lock:
+                    counts['verify'] += len(objs)
+                    counts['valid'] += sum(got)
+
         def checker():
             while True:
                 item = todo.get()
@@ -118,11 +147,12 @@ def test_soak_every_entry_point_at_once(gpulib, shards, run_split, coracle):  # 
         for c in checkers:
             c.start()
         svc = worker.PowService().start()
-        rngs = [random.Random(9000 + 10 * p + k) for k in range(4)]
+        rngs = [random.Random(9000 + 10 * p + k) for k in range(5)]
         th = [threading.Thread(target=service_loop, args=(svc, rngs[0])),
               threading.Thread(target=serial_loop, args=(rngs[1],)),
               threading.Thread(target=serial_loop, args=(rngs[2],)),
-              threading.Thread(target=batch_loop, args=(rngs[3],))]
+              threading.Thread(target=batch_loop, args=(rngs[3],)),
+              threading.Thread(target=verify_loop, args=(rngs[4],))]
         t0 = time.time()
         for x in th:
             x.start()
@@ -142,7 +172,7 @@ def test_soak_every_entry_point_at_once(gpulib, shards, run_split, coracle):  # 
         assert not any(x.is_alive() for x in th)
         assert not bad, bad[:4]
         assert all(counts[k] > 0 for k in counts), counts
-        assert stats['minimal'] >= min(100, sum(counts.values())), stats
+        assert stats['minimal'] >= min(100, counts['service'] + counts['serial'] + counts['batch']), stats
     n = len(PHASES)
     growth = max(b - a for a, b in zip(rss[n:2 * n], rss[2 * n:]))
     assert growth < 64 * 2**20, 'resident memory grew by %.1f MiB between passes (%s MiB)' % (
