@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -47,7 +48,37 @@ constexpr uint64_t kU64Max = ~0ULL;
 constexpr uint64_t kDefaultStepTrials = 1ULL << 29;
 
 thread_local std::string g_err;
-std::mutex g_mu;  // one entry point at a time (the steppers never take it)
+// A first-come first-served mutex.  The library's entry points take it one at a time, and the batch
+// service's thread takes it for every step (up to a launch, ~80 ms) and again right after: with a plain
+// std::mutex a serial run() beside a busy service waited 0.3-36 s for it -- until the batch was nearly
+// done (tools/diag/run_beside_service.py, profiles/r05/run_beside_service/).  Tickets hand it out in
+// arrival order, and waiting() lets a service step end at its next completed launch when a caller waits.
+class FairMutex {
+ public:
+  void lock() {
+    std::unique_lock<std::mutex> lk(m_);
+    const uint64_t t = next_.fetch_add(1, std::memory_order_relaxed);
+    cv_.wait(lk, [&] { return serving_.load(std::memory_order_relaxed) == t; });
+  }
+  void unlock() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      serving_.fetch_add(1, std::memory_order_relaxed);
+    }
+    cv_.notify_all();
+  }
+  // threads waiting for the lock (while one holds it)
+  uint64_t waiting() const {
+    const uint64_t n = next_.load(std::memory_order_relaxed), s = serving_.load(std::memory_order_relaxed);
+    return n > s + 1 ? n - s - 1 : 0;
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  std::atomic<uint64_t> next_{0}, serving_{0};
+};
+FairMutex g_mu;  // one entry point at a time (the steppers never take it)
 std::atomic<int> g_abort{0};
 std::atomic<uint64_t> g_step_trials{kDefaultStepTrials};  // read without the lock (bmpow_get_step_trials)
 
@@ -95,6 +126,7 @@ bool g_one_enabled = true;
 // BMPOW_TRACE=1: the single-object path's set-up and tear-down steps on stderr, with the state of every
 // stream they wait on (a diagnostic; tools/diag/rss_layout.py).
 bool g_trace = false;
+bool g_run_stream = true;  // run() on its own stream per device (run_stream); BMPOW_RUN_STREAM=0: the shard's
 #define BM_TRACE(...)                                                      \
   do {                                                                     \
     if (g_trace) {                                                         \
@@ -394,6 +426,7 @@ int init_locked() {
   if (const char* w = std::getenv("BMPOW_SPIN_YIELD")) g_spin_yield = std::atoi(w) != 0;
   if (const char* w = std::getenv("BMPOW_ONE")) g_one_enabled = std::atoi(w) != 0;
   if (const char* w = std::getenv("BMPOW_TRACE")) g_trace = std::atoi(w) != 0;
+  if (const char* w = std::getenv("BMPOW_RUN_STREAM")) g_run_stream = std::atoi(w) != 0;
   const auto vis = visible_gfx950();
   if (vis.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
   std::vector<int> ids = vis;
@@ -882,7 +915,7 @@ struct OnePath {
   bm_one_out* h_out = nullptr;  // host-mapped ring of results
   bm_one_out* d_out = nullptr;  // the device's address of h_out
   unsigned long long* d_xone = nullptr;  // the cross-device table as this device maps it
-  hipStream_t stream = nullptr;  // the shard's stream, or (a forced piece sharing its device) a masked one
+  hipStream_t stream = nullptr;  // run_stream (or the shard's), or (a forced piece sharing its device) a masked one
   bool masked = false;           // stream is the CU-masked stream of this piece's slice (masked_stream)
   uint32_t cus = 0;              // CUs of that slice (0: the whole device)
   uint32_t slice = 0, slices = 1;  // this piece's slice of its device, of `slices`
@@ -939,6 +972,29 @@ int masked_stream(int dev, uint32_t n, uint32_t lo, uint32_t hi, hipStream_t* ou
   return 0;
 }
 
+// run()'s stream on a device: one per device, of the highest priority, kept for the process like the
+// masked streams.  On the shard's stream a run() beside a busy batch queued behind the engine's running
+// launch and its lookahead (160-240 ms, tools/diag/run_beside_service.py); on its own stream the call's
+// workgroups are dispatched as the running launch's retire.  BMPOW_RUN_STREAM=0: the shard's stream (A/B,
+// g_run_stream).
+std::vector<std::pair<int, hipStream_t>> g_run_streams;
+
+int run_stream(int dev, hipStream_t* out) {
+  for (const auto& r : g_run_streams)
+    if (r.first == dev) {
+      *out = r.second;
+      return 0;
+    }
+  int least = 0, greatest = 0;
+  HIPTRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  hipStream_t st = nullptr;
+  HIPTRY(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest));
+  g_run_streams.emplace_back(dev, st);
+  BM_TRACE("run stream: dev %d priority %d (range %d..%d) stream %p", dev, greatest, least, greatest, (void*)st);
+  *out = st;
+  return 0;
+}
+
 void free_one() {
   // every stream a piece launched on drains before any buffer is freed (hipFree waits for the device)
   for (size_t s = 0; s < g_ones.size(); ++s) {
@@ -949,7 +1005,7 @@ void free_one() {
              op.stream ? hipGetErrorName(hipStreamQuery(op.stream)) : "-",
              s < g_shards.size() && g_shards[s].stream ? hipGetErrorName(hipStreamQuery(g_shards[s].stream)) : "-");
     if (s < g_shards.size() && g_shards[s].stream) (void)hipStreamSynchronize(g_shards[s].stream);
-    if (op.masked && op.stream) (void)hipStreamSynchronize(op.stream);
+    if (op.stream && (s >= g_shards.size() || op.stream != g_shards[s].stream)) (void)hipStreamSynchronize(op.stream);
   }
   BM_TRACE("free_one: streams drained");
   for (size_t s = 0; s < g_ones.size(); ++s) {
@@ -974,7 +1030,7 @@ int ensure_one(size_t s, uint32_t slice, uint32_t slices) {
   const Shard& sh = g_shards[s];
   if (op.dev == sh.dev && op.d_calls && op.slice == slice && op.slices == slices) return 0;
   HIPTRY(hipSetDevice(sh.dev));
-  if (op.masked && op.stream) (void)hipStreamSynchronize(op.stream);  // another slice than before
+  if (op.stream && op.stream != sh.stream) (void)hipStreamSynchronize(op.stream);  // another slice than before
   if (op.d_calls) (void)hipFree(op.d_calls);
   if (op.d_ctr) (void)hipFree(op.d_ctr);
   if (op.h_out) (void)hipHostFree(op.h_out);
@@ -990,6 +1046,10 @@ int ensure_one(size_t s, uint32_t slice, uint32_t slices) {
   op.slice = slice;
   op.slices = slices;
   op.stream = sh.stream;
+  if (g_run_stream) {
+    const int rc = run_stream(sh.dev, &op.stream);
+    if (rc < 0) return rc;
+  }
   if (slices > 1 && g_split_cumask && sh.cus > 0) {
     const uint32_t n = (uint32_t)sh.cus, lo = slice * n / slices, hi = (slice + 1) * n / slices;
     hipStream_t st = nullptr;
@@ -1746,7 +1806,7 @@ bmsched::ServiceOps service_ops(bmpow_service* s) {
   bmsched::ServiceOps ops;
   ops.add = [s](size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* tg, uint32_t* slots,
                 std::string& err) {
-    std::lock_guard<std::mutex> g(g_mu);
+    std::lock_guard<FairMutex> g(g_mu);
     std::unique_lock<std::mutex> lk(g_engine->mu);
     const int rc = batch_add_locked(lk, s->b, n, ihs, tg, nullptr, slots, ih_off);
     if (rc < 0) err = g_err;
@@ -1755,21 +1815,23 @@ bmsched::ServiceOps service_ops(bmpow_service* s) {
   // let the steppers claim one round of launches (and keep one queued behind it) and return as soon
   // as an object finished, so the service hands it out while the devices go on
   ops.step = [s](std::string& err) {
-    std::lock_guard<std::mutex> g(g_mu);
+    std::lock_guard<FairMutex> g(g_mu);
     std::unique_lock<std::mutex> lk(g_engine->mu);
     g_engine->attach(lk, s->b);
     bmpow_batch* b = s->b;
     const uint64_t budget = (s->budget ? s->budget : g_step_trials.load()) * g_shards.size();
-    return g_engine->run(lk, budget, true, [b] { return b->finished_head < b->finished.size() || b->pending == 0; },
+    // ... or as soon as a launch completes while another caller waits for the library (a serial run())
+    return g_engine->run(lk, budget, true,
+                         [b] { return b->finished_head < b->finished.size() || b->pending == 0 || g_mu.waiting() > 0; },
                          err);
   };
   ops.take = [s](size_t cap, uint32_t* slot, uint64_t* nonce, uint64_t* trial, uint8_t* done) {
-    std::lock_guard<std::mutex> g(g_mu);
+    std::lock_guard<FairMutex> g(g_mu);
     std::lock_guard<std::mutex> lk(g_engine->mu);
     return bmsched::take_done(*s->b, cap, slot, nonce, trial, done);
   };
   ops.reset = [s](std::string& err) {
-    std::lock_guard<std::mutex> g(g_mu);
+    std::lock_guard<FairMutex> g(g_mu);
     std::unique_lock<std::mutex> lk(g_engine->mu);
     if (g_engine->attached() == s->b) g_engine->detach(lk);
     batch_free_dev(s->b);
@@ -1790,14 +1852,14 @@ bmsched::ServiceOps service_ops(bmpow_service* s) {
 extern "C" {
 
 int bmpow_init(void) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   return init_locked();
 }
 
 int bmpow_device_count(void) { return (int)visible_gfx950().size(); }
 
 int bmpow_set_devices(const int* ids, int n) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (n < 0) return set_err(BMPOW_E_ARG, "bad device list");
   std::vector<int> v;
   if (n == 0) {
@@ -1827,7 +1889,7 @@ int bmpow_set_device_count(int ndev) {
 }
 
 int bmpow_get_devices(int* ids, int cap) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   for (int i = 0; i < (int)g_shards.size() && i < cap; ++i) ids[i] = g_shards[i].dev;
   return (int)g_shards.size();
 }
@@ -1840,7 +1902,7 @@ int bmpow_device_pci_bus_id(int device, char* out, int len) {
 }
 
 int bmpow_get_shard_rates(double* rates, int cap) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (!rates && cap > 0) return set_err(BMPOW_E_ARG, "null pointer");
   if (!g_engine) return 0;
   std::lock_guard<std::mutex> el(g_engine->mu);
@@ -1850,7 +1912,7 @@ int bmpow_get_shard_rates(double* rates, int cap) {
 }
 
 void bmpow_shutdown(void) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (g_engine) {
     std::unique_lock<std::mutex> el(g_engine->mu);
     drop_scratch(el);
@@ -1884,7 +1946,7 @@ void bmpow_abort(void) { g_abort.store(1); }
 void bmpow_clear_abort(void) { g_abort.store(0); }
 
 int bmpow_trials_len(const uint8_t* ih, size_t ih_len, const uint64_t* nonces, size_t n, uint64_t* trials_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if ((!ih && ih_len) || (n && (!nonces || !trials_out))) return set_err(BMPOW_E_ARG, "null pointer");
@@ -1930,7 +1992,7 @@ int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t
 
 int bmpow_search_len(const uint8_t* ih, size_t ih_len, uint64_t target, uint64_t start, uint64_t max_trials,
                      uint64_t* nonce_out, uint64_t* trial_out) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if ((!ih && ih_len) || !nonce_out || !trial_out) return set_err(BMPOW_E_ARG, "null pointer");
@@ -1961,7 +2023,7 @@ int bmpow_search_len(const uint8_t* ih, size_t ih_len, uint64_t target, uint64_t
 }
 
 int bmpow_min_trial(const uint8_t ih[64], uint64_t start, uint64_t count, uint64_t* min_out, uint64_t* argmin_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if (!ih || !min_out || !argmin_out) return set_err(BMPOW_E_ARG, "null pointer");
@@ -1970,7 +2032,7 @@ int bmpow_min_trial(const uint8_t ih[64], uint64_t start, uint64_t count, uint64
 
 int bmpow_min_trial_batch(size_t n, const uint8_t* ihs, const uint64_t* start, const uint64_t* count,
                           uint64_t* min_out, uint64_t* argmin_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if (n == 0) return 0;
@@ -1991,7 +2053,7 @@ static int check_ih_offsets(size_t n, const uint8_t* ihs, const uint64_t* ih_off
 
 int bmpow_min_trial_var(size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* start,
                         const uint64_t* count, uint64_t* min_out, uint64_t* argmin_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if (n == 0) return 0;
@@ -2004,7 +2066,7 @@ int bmpow_min_trial_var(size_t n, const uint8_t* ihs, const uint64_t* ih_off, co
 
 int bmpow_search_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, uint64_t* next_start,
                        uint64_t budget, uint64_t* nonce_out, uint64_t* trial_out, uint8_t* done) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if (n == 0) return 0;
@@ -2039,7 +2101,7 @@ int bmpow_search_batch(size_t n, const uint8_t* ihs, const uint64_t* targets, ui
 }
 
 bmpow_batch* bmpow_batch_create(size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   if (init_locked() < 0) return nullptr;
   if (n && (!ihs || !targets)) {
     set_err(BMPOW_E_ARG, "null pointer");
@@ -2062,7 +2124,7 @@ bmpow_batch* bmpow_batch_create(size_t n, const uint8_t* ihs, const uint64_t* ta
 // Let the steppers claim ~budget trials of the batch (and one more launch per shard, which stays
 // queued behind the running one when this returns, so consecutive calls keep every device busy).
 int bmpow_batch_step(bmpow_batch* b, uint64_t budget) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (!g_engine) return set_err(BMPOW_E_STATE, "library not initialised");
   if (b->dev.size() != g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
@@ -2078,7 +2140,7 @@ int bmpow_batch_step(bmpow_batch* b, uint64_t budget) {
 
 int bmpow_batch_results(const bmpow_batch* b, uint64_t* nonce_out, uint64_t* trial_out, uint8_t* done,
                         uint64_t* next_start) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   std::unique_lock<std::mutex> lk;
   if (g_engine) lk = std::unique_lock<std::mutex>(g_engine->mu);
@@ -2092,7 +2154,7 @@ int bmpow_batch_results(const bmpow_batch* b, uint64_t* nonce_out, uint64_t* tri
 }
 
 int bmpow_batch_reset(bmpow_batch* b, const uint64_t* start) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (b->dev.size() != g_shards.size() || !g_engine) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
   std::unique_lock<std::mutex> lk(g_engine->mu);
@@ -2113,7 +2175,7 @@ int bmpow_batch_reset(bmpow_batch* b, const uint64_t* start) {
 }
 
 int bmpow_batch_set_pending(bmpow_batch* b, size_t first, size_t count, int pending) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (first > b->n || count > b->n - first) return set_err(BMPOW_E_ARG, "range outside the batch");
   std::unique_lock<std::mutex> lk;
@@ -2125,7 +2187,7 @@ int bmpow_batch_set_pending(bmpow_batch* b, size_t first, size_t count, int pend
 
 int bmpow_batch_add(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* targets, const uint64_t* start,
                     uint32_t* slot_out) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (n == 0) return (int)std::min<size_t>(b->pending, 0x7fffffff);
   if (!ihs || !targets) return set_err(BMPOW_E_ARG, "null pointer");
@@ -2138,7 +2200,7 @@ int bmpow_batch_add(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t
 
 int bmpow_batch_add_var(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* targets,
                         const uint64_t* start, uint32_t* slot_out) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (n == 0) return (int)std::min<size_t>(b->pending, 0x7fffffff);
   if (!targets) return set_err(BMPOW_E_ARG, "null pointer");
@@ -2154,7 +2216,7 @@ int bmpow_batch_add_var(bmpow_batch* b, size_t n, const uint8_t* ihs, const uint
 
 int bmpow_batch_take_done(bmpow_batch* b, size_t cap, uint32_t* slot_out, uint64_t* nonce_out, uint64_t* trial_out,
                           uint8_t* done_out) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   if (!b) return set_err(BMPOW_E_STATE, "null batch");
   if (cap && !slot_out) return set_err(BMPOW_E_ARG, "null pointer");
   std::unique_lock<std::mutex> lk;
@@ -2164,7 +2226,7 @@ int bmpow_batch_take_done(bmpow_batch* b, size_t cap, uint32_t* slot_out, uint64
 }
 
 void bmpow_batch_destroy(bmpow_batch* b) {
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   if (!b) return;
   if (g_engine) {
     std::unique_lock<std::mutex> lk(g_engine->mu);
@@ -2177,7 +2239,7 @@ void bmpow_batch_destroy(bmpow_batch* b) {
 bmpow_service* bmpow_service_create(uint64_t step_budget, uint32_t flags) {
   bmpow_service* s = new bmpow_service();
   {
-    std::lock_guard<std::mutex> g(g_mu);
+    std::lock_guard<FairMutex> g(g_mu);
     s->b = new bmpow_batch();
     if (init_locked() < 0) {
       delete s->b;
@@ -2245,7 +2307,7 @@ void bmpow_service_stop(bmpow_service* s) {
 void bmpow_service_destroy(bmpow_service* s) {
   if (!s) return;
   s->svc.reset();  // joins the service thread after its current op
-  std::lock_guard<std::mutex> g(g_mu);
+  std::lock_guard<FairMutex> g(g_mu);
   if (g_engine) {
     std::unique_lock<std::mutex> lk(g_engine->mu);
     if (g_engine->attached() == s->b) g_engine->detach(lk);
@@ -2256,7 +2318,7 @@ void bmpow_service_destroy(bmpow_service* s) {
 }
 
 bmpow_vbatch* bmpow_vbatch_create(size_t n, const uint8_t* objs, const uint64_t* offsets) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (init_locked() < 0) return nullptr;
   std::vector<Span> spans;
   if (spans_from(n, objs, offsets, spans) < 0) return nullptr;
@@ -2270,7 +2332,7 @@ bmpow_vbatch* bmpow_vbatch_create(size_t n, const uint8_t* objs, const uint64_t*
 }
 
 int bmpow_vbatch_run(bmpow_vbatch* vb, uint64_t* pow_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (!vb) return set_err(BMPOW_E_STATE, "null verification batch");
   for (auto& pt : vb->parts)
     if (pt.shard >= g_shards.size()) return set_err(BMPOW_E_STATE, "device set changed under a live batch");
@@ -2278,14 +2340,14 @@ int bmpow_vbatch_run(bmpow_vbatch* vb, uint64_t* pow_out) {
 }
 
 void bmpow_vbatch_destroy(bmpow_vbatch* vb) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (!vb) return;
   vbatch_free(vb);
   delete vb;
 }
 
 int bmpow_pow_values(size_t n, const uint8_t* objs, const uint64_t* offsets, uint64_t* pow_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if (n == 0) return 0;
@@ -2356,7 +2418,7 @@ static int verify_spans_locked(size_t n, const uint8_t* const* ptrs, const uint6
 
 int bmpow_verify_batch(size_t n, const uint8_t* objs, const uint64_t* offsets, const uint64_t* ntpb,
                        const uint64_t* extra, const int64_t* recv_time, uint8_t* ok_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if (n == 0) return 0;
@@ -2373,7 +2435,7 @@ int bmpow_verify_batch(size_t n, const uint8_t* objs, const uint64_t* offsets, c
 
 int bmpow_verify_batch_ptrs(size_t n, const uint8_t* const* objs, const uint64_t* lens, const uint64_t* ntpb,
                             const uint64_t* extra, const int64_t* recv_time, uint8_t* ok_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if (n == 0) return 0;
@@ -2388,7 +2450,7 @@ int bmpow_pow_sufficient(uint64_t pow, uint64_t len, uint64_t ntpb, uint64_t ext
 }
 
 int bmpow_pubkeys(size_t n, const uint8_t* privkeys, uint8_t* pubkeys_out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if (n == 0) return 0;
@@ -2429,7 +2491,7 @@ int bmpow_pubkeys(size_t n, const uint8_t* privkeys, uint8_t* pubkeys_out) {
 }
 
 int bmpow_fe_probe(int op, size_t n, const uint32_t* a, const uint32_t* b, uint32_t* out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if (n == 0) return 0;
@@ -2457,7 +2519,7 @@ int bmpow_fe_probe(int op, size_t n, const uint32_t* a, const uint32_t* b, uint3
 
 int bmpow_address_search(const uint8_t* passphrase, size_t len, uint64_t start, uint64_t max_tries, int null_bytes,
                          bmpow_address* out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   std::vector<AddrShard> as;
@@ -2468,7 +2530,7 @@ int bmpow_address_search(const uint8_t* passphrase, size_t len, uint64_t start, 
 
 int bmpow_address_search_random(const uint8_t priv_signing[32], const uint8_t* seed, size_t seed_len, uint64_t start,
                                 uint64_t max_tries, int null_bytes, bmpow_address* out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   std::vector<AddrShard> as;
@@ -2478,7 +2540,7 @@ int bmpow_address_search_random(const uint8_t priv_signing[32], const uint8_t* s
 }
 
 int bmpow_addr_set_comb(int wbits) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (wbits != 0 && wbits != ec::kCombSmall && wbits != ec::kCombLarge)
     return set_err(BMPOW_E_ARG, "comb width must be 0 (auto), 16 or 24");
   const int prev = g_addr_comb;
@@ -2487,12 +2549,12 @@ int bmpow_addr_set_comb(int wbits) {
 }
 
 int bmpow_addr_last_comb(void) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   return g_addr_last_comb;
 }
 
 int bmpow_get_stats(bmpow_stats* out) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (!out) return BMPOW_E_ARG;
   *out = g_stats;
   if (g_engine) {  // the searches: the engine's launches
@@ -2510,7 +2572,7 @@ int bmpow_get_stats(bmpow_stats* out) {
 }
 
 void bmpow_reset_stats(void) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   g_stats = bmpow_stats{};
   for (OnePath& op : g_ones) {
     op.trials = 0;
@@ -2527,7 +2589,7 @@ void bmpow_reset_stats(void) {
 }
 
 int bmpow_get_shard_stats(uint64_t* trials, double* kernel_ms, int cap) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (!g_engine) return 0;
   std::lock_guard<std::mutex> el(g_engine->mu);
   const bmsched::EngineStats& es = g_engine->stats;
@@ -2541,7 +2603,7 @@ int bmpow_get_shard_stats(uint64_t* trials, double* kernel_ms, int cap) {
 }
 
 int bmpow_set_run_split(int per_shard) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   const int prev = g_run_split ? 1 : 0;
   if (per_shard < 0) return prev;
   if ((per_shard != 0) != g_run_split) {
@@ -2553,7 +2615,7 @@ int bmpow_set_run_split(int per_shard) {
 }
 
 int bmpow_get_run_pieces(int* shards, int cap) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   const int rc = init_locked();
   if (rc < 0) return rc;
   const std::vector<size_t> p = one_pieces();
@@ -2563,7 +2625,7 @@ int bmpow_get_run_pieces(int* shards, int cap) {
 }
 
 int bmpow_get_thread_info(double* cpu_s, int* policy, int cap) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (!g_engine) return 0;
   std::vector<double> c;
   std::vector<int> p;
@@ -2579,7 +2641,7 @@ int bmpow_get_thread_info(double* cpu_s, int* policy, int cap) {
 }
 
 int bmpow_set_shard_throttle(int shard, double ms) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   if (!g_engine) return set_err(BMPOW_E_STATE, "library not initialised");
   if (shard < 0 || shard >= (int)g_shards.size() || !(ms >= 0)) return set_err(BMPOW_E_ARG, "bad shard or delay");
   g_engine->set_throttle((size_t)shard, ms);
@@ -2589,7 +2651,7 @@ int bmpow_set_shard_throttle(int shard, double ms) {
 uint64_t bmpow_get_step_trials(void) { return g_step_trials.load(); }
 
 void bmpow_set_step_trials(uint64_t t) {
-  std::lock_guard<std::mutex> lk(g_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
   g_step_trials.store(t ? std::max<uint64_t>(t, BM_CHUNK) : kDefaultStepTrials);
   if (g_engine) {
     std::lock_guard<std::mutex> el(g_engine->mu);

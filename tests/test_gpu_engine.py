@@ -416,3 +416,29 @@ def test_serial_runs_beside_a_running_service(gpulib, shards, run_split, coracle
         assert [list(r) for r in res] == [list(coracle.search(ih, t)) for t, ih in batch], layout
         for k in range(2):
             assert got[k] == [list(coracle.search(ih, t)) for t, ih in serial[k]], (layout, k)
+
+
+def test_run_is_not_starved_by_a_busy_service(gpulib, shards, coracle):
+    """A serial run() while a PowService works through a batch of hard objects (PyBitmessage's API
+    thread, api.py:1304, beside its worker's batches): the library's lock is handed out first come first
+    served and a service step ends at its next completed launch when a caller waits, and run() has its
+    own stream of the highest priority -- so a call waits about one engine launch (~80 ms), not for the
+    batch (up to 36 s with a plain mutex: tools/diag/run_beside_service.py).  Answers exact."""
+    from pybitmessage_amd import worker
+    shards([0])
+    rng = random.Random(505)
+    batch = [(U64 // 2_000_000_000, rng.randbytes(64)) for _ in range(64)]  # ~0.3 s each: ~20 s of work
+    calls = [(U64 // 300_000, rng.randbytes(64)) for _ in range(6)]
+    svc = worker.PowService().start()
+    try:
+        svc.submit_many(batch)
+        time.sleep(0.5)
+        took, got = [], []
+        for t, ih in calls:
+            t0 = time.perf_counter()
+            got.append(proofofwork.run(t, ih))
+            took.append(time.perf_counter() - t0)
+    finally:
+        svc.stop(60)
+    assert got == [list(coracle.search(ih, t)) for t, ih in calls]
+    assert max(took) < 1.0, took

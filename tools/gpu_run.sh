@@ -38,6 +38,7 @@
 #   soak:S           tests/test_gpu_soak.py for S seconds (every entry point at once, 4 shard layouts)
 #   rss-layout       tools/diag/rss_layout.py (host RSS per shard layout / forced split)
 #   cumask-free:M    tools/diag/cumask_free mode M (re-creating CU-masked streams: drain | serial | drain-sync | drain-sleep | reuse)
+#   run-beside-service  tools/diag/run_beside_service.py (run() latency while the batch service is busy)
 #   serial-wait:C:M  config C (c2 | c4 | c5) one run() call after another with BMPOW_WAIT1=M (auto | spin | sleep)
 #   c4-serial        8 C4 objects one after another through proofofwork.run (host CPU of a long serial call)
 #   c1c3-ab:V1,V2    tools/cmp_c1.sh over the variants (C1 40 calls + C3 2^35 each), same box
@@ -79,6 +80,8 @@ for step in "$@"; do
     rss-layout) BMPOW_TRACE=1 timeout -k 10 120 python3 tools/diag/rss_layout.py > "$OUT/rss_layout.jsonl" 2> "$OUT/rss_layout.err" ;;
     cumask-free:*) cm=${step#cumask-free:}; timeout -k 10 60 ./tools/diag/cumask_free 3 "${CF_ITERS:-20}" "$cm" >> "$OUT/cumask_free.jsonl" \
         2> "$OUT/cumask_free_$cm.err" ;;
+    run-beside-service) timeout -k 10 300 python3 tools/diag/run_beside_service.py 20 256 > "$OUT/run_beside_service.json" \
+        2> "$OUT/run_beside_service.err" ;;
     cpu-share) timeout -k 10 300 python3 tools/diag/cpu_share.py 5 > "$OUT/cpu_share.json" 2> "$OUT/cpu_share.err" ;;
     service-overhead) timeout -k 10 300 python3 tools/diag/service_overhead.py 50 2 > "$OUT/service_overhead.json" 2> "$OUT/service_overhead.err" &&
       BMPOW_DEVICES=0,0,0,0 timeout -k 10 300 python3 tools/diag/service_overhead.py 50 2 > "$OUT/service_overhead_4shards.json" 2>> "$OUT/service_overhead.err" ;;
