@@ -975,7 +975,9 @@ int masked_stream(int dev, uint32_t n, uint32_t lo, uint32_t hi, hipStream_t* ou
 // run()'s stream on a device: one per device, of the highest priority, kept for the process like the
 // masked streams.  On the shard's stream a run() beside a busy batch queued behind the engine's running
 // launch and its lookahead (160-240 ms, tools/diag/run_beside_service.py); on its own stream the call's
-// workgroups are dispatched as the running launch's retire.  BMPOW_RUN_STREAM=0: the shard's stream (A/B,
+// workgroups are dispatched as the running launch's retire.  Used only by calls made while the engine
+// has work, and created at the first such call: a stream costs the runtime a hardware queue and ~190 MiB
+// of host memory (tools/diag/rss_layout.py).  BMPOW_RUN_STREAM=0: always the shard's stream (A/B,
 // g_run_stream).
 std::vector<std::pair<int, hipStream_t>> g_run_streams;
 
@@ -1045,11 +1047,7 @@ int ensure_one(size_t s, uint32_t slice, uint32_t slices) {
   op.dev = sh.dev;
   op.slice = slice;
   op.slices = slices;
-  op.stream = sh.stream;
-  if (g_run_stream) {
-    const int rc = run_stream(sh.dev, &op.stream);
-    if (rc < 0) return rc;
-  }
+  op.stream = sh.stream;  // search_one_calls moves it to run_stream while a batch is running
   if (slices > 1 && g_split_cumask && sh.cus > 0) {
     const uint32_t n = (uint32_t)sh.cus, lo = slice * n / slices, hi = (slice + 1) * n / slices;
     hipStream_t st = nullptr;
@@ -1139,6 +1137,29 @@ int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint
       }
     const int rc = ensure_one(pieces[p], slice, slices);
     if (rc < 0) return rc;
+  }
+  // beside a batch with work (the engine's launches on the shard streams): run()'s own stream; else the
+  // shard's.  A piece changing streams first lets the old one drain (a queued window of the previous
+  // call stops at its first block), so its launches stay in call order.
+  bool busy = false;
+  if (g_run_stream && g_engine) {
+    std::lock_guard<std::mutex> el(g_engine->mu);
+    const bmsched::BatchState* b = g_engine->attached();
+    busy = g_engine->in_flight() > 0 || (b && b->pending > 0);
+  }
+  for (size_t p = 0; p < P; ++p) {
+    OnePath& op = g_ones[pieces[p]];
+    if (op.masked) continue;
+    hipStream_t want = g_shards[pieces[p]].stream;
+    if (busy) {
+      HIPTRY(hipSetDevice(op.dev));
+      const int rc = run_stream(op.dev, &want);
+      if (rc < 0) return rc;
+    }
+    if (op.stream != want) {
+      HIPTRY(hipStreamSynchronize(op.stream));
+      op.stream = want;
+    }
   }
   const uint64_t end = (max_trials - 1 > kU64Max - start) ? kU64Max : start + max_trials - 1;  // last nonce
   const uint64_t call = ++g_one_call;  // every call launches on every piece (it resets call + 2's state)
