@@ -38,6 +38,9 @@ pytestmark = pytest.mark.gpu
 U64 = (1 << 64) - 1
 SOAK_S = float(os.environ.get('BMPOW_SOAK_S', '30'))
 PHASES = (([0], False), ([0, 0], False), ([0, 0, 0], True), ([0, 0, 0, 0], False))
+# BMPOW_SOAK_LAYOUTS=wide: eight shards, with and without forced pieces, and two forced pieces
+if os.environ.get('BMPOW_SOAK_LAYOUTS') == 'wide':
+    PHASES = (([0] * 8, False), ([0] * 8, True), ([0, 0], True), ([0], False))
 EXPECT = (20, 200, 2000, 20000, 200000)      # expected trials per object (target = 2^64 / E)
 WEIGHT = (2, 3, 3, 2, 1)
 BACKLOG = 400                                  # past this many unchecked answers: validity only
