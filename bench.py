@@ -216,6 +216,20 @@ def one_wait(st, elapsed):
             'spin_share': round(spin / (spin + sleep), 5)}
 
 
+def past_answers(st):
+    """Where the engine hashed past the objects' answers (bmpow_stats.past_*, round 6): the window
+    holding an answer (blocks above it), windows above it (the lookahead), and pieces of windows split
+    over device groups -- estimates from each item's block queue (include/bmpow.h), with the estimated
+    hashed total beside the device's count.  None when no batch ran."""
+    est = int(getattr(st, 'engine_hashed_est', 0) or 0)
+    if not est:
+        return None
+    return {'window': int(st.past_window), 'later': int(st.past_later), 'split': int(st.past_split),
+            'hashed_est': est, 'trials': int(st.trials),
+            'what': 'nonces hashed above the objects\' answers by where: the window holding the answer, '
+                    'unsplit windows above it, split pieces (block-queue estimates, bmsched::WasteStats)'}
+
+
 def prove_sample(lib, objs, nonce, idx, k, seed):
     """Exactness of k answers (a seeded sample of idx) at any size: each nonce n is the _doSafePoW
     answer (src/proofofwork.py:100-111) iff trial(n) <= target (re-checked with hashlib by the
@@ -970,6 +984,11 @@ def main():
     ap.add_argument('--run-split', action='store_true',
                     help='run() legs (c1, c3, --serial): one piece per shard even where shards share a device '
                          '(bmpow_set_run_split; the multi-device path rehearsed on one GPU)')
+    ap.add_argument('--engine-split', action='store_true',
+                    help='--devices: every shard its own device group (bmpow_set_engine_split), so windows split '
+                         'over shards that share a GPU -- the multi-device split rehearsed on one GPU')
+    ap.add_argument('--no-nonce-sharded', action='store_true',
+                    help='N > 1: skip the in-process nonce-sharded C3/C4 leg after the timed region')
     ap.add_argument('--serial', action='store_true',
                     help='c2/c4/c5: the objects one after another through proofofwork.run (the reference\'s '
                          'serial call sites), not as one batch')
@@ -996,6 +1015,8 @@ def main():
         lib.bmpow_set_step_trials(args.step_trials)
     if args.run_split:
         lib.bmpow_set_run_split(1)
+    if args.engine_split:
+        lib.bmpow_set_engine_split(1)
     if args.throttle:
         shard, ms = args.throttle.split(':')
         _lib.check(lib, lib.bmpow_set_shard_throttle(int(shard), float(ms)), 'bmpow_set_shard_throttle')
@@ -1038,9 +1059,105 @@ def main():
     line = summarize(args, dist, r, lib.bmpow_version().decode())
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_threads or None)
+    if dist.world > 1 and not args.devices and not args.no_nonce_sharded and args.config in ('c2', 'c4', 'c5'):
+        # the nonce split over the node's GPUs (C3, C4), outside the timed region: rank 0 alone
+        dist.barrier()
+        if dist.rank == 0:
+            try:
+                line['nonce_sharded'] = nonce_sharded(lib, dist.world, args.share_device)
+            except Exception as e:  # reported in the line; the scaling value above stands
+                line['nonce_sharded'] = {'error': repr(e)}
+        dist.barrier()
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
     dist.close()
+
+
+def per_device(lib, ids):
+    """Work per physical device of the shard set `ids` since bmpow_reset_stats: PCI bus id, trials and
+    summed kernel time of its shards (bmpow_get_shard_stats: the engine's launches and run()'s pieces)."""
+    tr, ms = (ctypes.c_uint64 * 64)(), (ctypes.c_double * 64)()
+    n = lib.bmpow_get_shard_stats(tr, ms, 64)
+    out = []
+    for dev in sorted(set(ids)):
+        shards = [i for i, d in enumerate(ids) if d == dev and i < n]
+        buf = ctypes.create_string_buffer(64)
+        bus = buf.value.decode() if lib.bmpow_device_pci_bus_id(dev, buf, 64) >= 0 else None
+        out.append({'device': dev, 'pci_bus_id': bus, 'shards': len(shards),
+                    'trials': int(sum(tr[i] for i in shards)), 'kernel_ms': round(sum(ms[i] for i in shards), 2)})
+    return out
+
+
+def nonce_sharded(lib, n, share=False, c3_log2=36, c4_objs=None):
+    """The north star's nonce split on a multi-GPU node (BASELINE.json C3 and C4 over 1/2/4/8 GPUs),
+    measured in ONE process over n devices -- the SCALE run's ranks each drive one GPU with object
+    sharding, which never splits an object.  Run by rank 0 after the timed region while the other ranks
+    wait at a barrier (their GPUs idle):
+      * C3: a run() sweep of 2^c3_log2 nonces with no hit (target 0), one interleaved piece per device
+        sharing the cross-device bound: every nonce hashed exactly once;
+      * C4: the 64 objects of 20x difficulty as one batch on the engine, one stepper per device (object
+        mode, then windows split over the devices at the tail), answers re-hashed with hashlib.
+    Falls back to n shards of device 0 when fewer than n devices are visible (then a rehearsal: the
+    per_device list shows one bus id).  The rank's own device selection is restored after."""
+    from pybitmessage_amd import _lib, proofofwork
+    import numpy as np
+    visible = lib.bmpow_device_count()
+    ids = [0] * n if share or visible < n else list(range(n))
+    own = (ctypes.c_int * 64)()
+    k = lib.bmpow_get_devices(own, 64)
+    own_ids = list(own[:k])
+    _lib.check(lib, lib.bmpow_set_devices((ctypes.c_int * n)(*ids), n), 'bmpow_set_devices')
+    out = {'devices': ids, 'device_groups': len(set(ids)),
+           'what': 'rank 0 alone after the timed region, one process over %d device(s) (bmpow_set_devices); the '
+                   'other ranks at a barrier%s' % (len(set(ids)), '' if len(set(ids)) == n else
+                                                   ' -- fewer devices visible than ranks: a rehearsal, not scaling')}
+    try:
+        # C3: no hit anywhere in [1, 2^k]: exactly 2^k trials over the pieces
+        ih = hashlib.sha512(b'bmpow-sweep').digest()
+        nn, tt = ctypes.c_uint64(), ctypes.c_uint64()
+        lib.bmpow_reset_stats()
+        t0 = time.perf_counter()
+        rc = _lib.check(lib, lib.bmpow_search(ih, 0, 1, 1 << c3_log2, ctypes.byref(nn), ctypes.byref(tt)), 'search')
+        el = time.perf_counter() - t0
+        st = _lib.BmpowStats()
+        lib.bmpow_get_stats(ctypes.byref(st))
+        out['c3'] = {'nonces': 1 << c3_log2, 'seconds': round(el, 3), 'ghs': round((1 << c3_log2) / el / 1e9, 4),
+                     'not_found': rc == _lib.NOT_FOUND, 'trials_exact': int(st.trials) == 1 << c3_log2,
+                     'per_device': per_device(lib, ids)}
+        # C4: the batch, exact answers
+        objs = c4_objs if c4_objs is not None else make_objects('c4', 0)[0]
+        m = len(objs)
+        tg = np.array([t for t, _ in objs], dtype=np.uint64)
+        p64 = ctypes.POINTER(ctypes.c_uint64)
+        h = lib.bmpow_batch_create(m, b''.join(ih for _, ih in objs), tg.ctypes.data_as(p64), None)
+        if not h:
+            raise RuntimeError('bmpow_batch_create: %s' % lib.bmpow_last_error().decode())
+        try:
+            lib.bmpow_reset_stats()
+            t0 = time.perf_counter()
+            solve_batch(lib, h)
+            el = time.perf_counter() - t0
+            st = _lib.BmpowStats()
+            lib.bmpow_get_stats(ctypes.byref(st))
+            nonce, trial = np.zeros(m, dtype=np.uint64), np.zeros(m, dtype=np.uint64)
+            done = np.zeros(m, dtype=np.uint8)
+            lib.bmpow_batch_results(h, nonce.ctypes.data_as(p64), trial.ctypes.data_as(p64),
+                                    done.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)), None)
+        finally:
+            lib.bmpow_batch_destroy(h)
+        for i in range(m):
+            assert done[i] == _lib.DONE_FOUND
+            proofofwork._verify(int(tg[i]), objs[i][1], int(trial[i]), int(nonce[i]))
+        useful = float(sum(int(x) for x in nonce))
+        out['c4'] = {'objects': m, 'seconds': round(el, 3), 'ghs': round(useful / el / 1e9, 4),
+                     'performed_ghs': round(int(st.trials) / el / 1e9, 4),
+                     'wasted_frac': round(1.0 - useful / int(st.trials), 5) if st.trials else None,
+                     'past_answers': past_answers(st), 'per_device': per_device(lib, ids)}
+    finally:
+        lib.bmpow_set_devices((ctypes.c_int * len(own_ids))(*own_ids), len(own_ids))
+    out['c3_ghs'], out['c4_ghs'] = out['c3']['ghs'], out['c4']['ghs']
+    out['c4_wasted_frac'] = out['c4']['wasted_frac']
+    return out
 
 
 def device_pci_bus_id(lib, shard=0):
@@ -1170,6 +1287,9 @@ def summarize(args, dist, r, lib_version):
             line['host_cpu']['wait']['run_calls'] = w1
     if r.get('exact_sample'):
         line['exact_sample'] = r['exact_sample']
+    pa = past_answers(st)
+    if pa:
+        line['past_answers'] = pa
     if dist.world > 1:
         # which physical GPU each rank drove, and its work: a reader can see that N distinct devices
         # (PCI bus ids) did the job -- the one-GPU rehearsals (--share-device) show one id

@@ -89,6 +89,14 @@ BMPOW_API int bmpow_get_shard_rates(double *rates, int cap);
 /* Release all device memory and streams (bmpow_init may be called again). */
 BMPOW_API void bmpow_shutdown(void);
 
+/* Process exit: stop every live service's thread, then release everything bmpow_shutdown does plus the
+ * streams the library keeps for the life of the process (run()'s and the rehearsal's CU-masked ones),
+ * before the HIP runtime's own exit handlers run.  The library registers it with atexit() at its first
+ * initialisation (after the runtime's handlers, so it runs before them); pybitmessage_amd._lib also runs it
+ * from Python's atexit.  Idempotent; afterwards every initialising call fails with BMPOW_E_STATE.  A call
+ * still running in another thread for 5 s leaves the library as it is. */
+BMPOW_API void bmpow_atexit(void);
+
 BMPOW_API const char *bmpow_last_error(void);
 BMPOW_API const char *bmpow_version(void);
 
@@ -363,6 +371,14 @@ typedef struct bmpow_stats {
        spinning on the result word (a short call's last window) and sleeping between polls */
     double one_wait_spin_ms;
     double one_wait_sleep_ms;
+    /* the engine's (batch) trials hashed past the objects' answers, by where, priced once an object's
+       answer is final.  Estimates from each item's block queue: every workgroup ends on one unit it
+       takes and does not hash, so of the units handed out the first (taken - workgroups) count as
+       hashed (within one block per workgroup of the device's count) */
+    uint64_t past_window;     /* unsplit windows holding the answer: nonces above it */
+    uint64_t past_later;      /* unsplit windows starting above the answer (the lookahead queued behind) */
+    uint64_t past_split;      /* pieces of windows split over device groups: nonces above the answer */
+    uint64_t engine_hashed_est; /* every priced item's estimated hashed nonces (compare with trials) */
 } bmpow_stats;
 
 BMPOW_API int bmpow_get_stats(bmpow_stats *out);
@@ -388,6 +404,12 @@ BMPOW_API int bmpow_set_shard_throttle(int shard, double ms);
  * rehearsal knob (pieces on one device compete for its SIMDs).  < 0 only queries.  Returns the
  * previous setting. */
 BMPOW_API int bmpow_set_run_split(int per_shard);
+/* The batch engine's device groups: 0 (default) = the shards of one physical device form one group,
+ * which never holds an object on two of its shards at once and never splits a window among them (a
+ * split window has one piece per device); 1 = every shard its own group, as if each were a separate
+ * GPU -- the test and rehearsal knob for the multi-device split on one GPU (its pieces then compete for
+ * the device's SIMDs).  Drains the engine.  < 0 only queries.  Returns the previous setting. */
+BMPOW_API int bmpow_set_engine_split(int per_shard);
 /* The shards carrying run()'s pieces into shards[0..cap) (may be NULL); returns their count or < 0. */
 BMPOW_API int bmpow_get_run_pieces(int *shards, int cap);
 

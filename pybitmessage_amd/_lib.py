@@ -5,6 +5,7 @@ Loaded the way the reference loads its native PoW library
 ``argtypes``/``restype`` set for every entry point.  There is no CPU fallback: if the library
 or a gfx950 device is missing, :func:`get` raises :class:`BmpowUnavailable`.
 """
+import atexit
 import ctypes
 import os
 import threading
@@ -55,7 +56,9 @@ class BmpowStats(ctypes.Structure):
                 ('verify_host_build_ms', ctypes.c_double), ('verify_host_run_ms', ctypes.c_double),
                 ('verify_host_verdict_ms', ctypes.c_double),
                 ('cut_trials', ctypes.c_uint64),
-                ('one_wait_spin_ms', ctypes.c_double), ('one_wait_sleep_ms', ctypes.c_double)]
+                ('one_wait_spin_ms', ctypes.c_double), ('one_wait_sleep_ms', ctypes.c_double),
+                ('past_window', ctypes.c_uint64), ('past_later', ctypes.c_uint64),
+                ('past_split', ctypes.c_uint64), ('engine_hashed_est', ctypes.c_uint64)]
 
 
 class BmpowAddress(ctypes.Structure):
@@ -78,6 +81,7 @@ SIGNATURES = [
     ('bmpow_device_pci_bus_id', ctypes.c_int, [ctypes.c_int, ctypes.c_char_p, ctypes.c_int]),
     ('bmpow_get_shard_rates', ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.c_int]),
     ('bmpow_shutdown', None, []),
+    ('bmpow_atexit', None, []),
     ('bmpow_last_error', ctypes.c_char_p, []),
     ('bmpow_version', ctypes.c_char_p, []),
     ('bmpow_abort', None, []),
@@ -114,6 +118,7 @@ SIGNATURES = [
     ('bmpow_get_thread_info', ctypes.c_int, [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ('bmpow_set_shard_throttle', ctypes.c_int, [ctypes.c_int, ctypes.c_double]),
     ('bmpow_set_run_split', ctypes.c_int, [ctypes.c_int]),
+    ('bmpow_set_engine_split', ctypes.c_int, [ctypes.c_int]),
     ('bmpow_get_run_pieces', ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ('bmpow_get_step_trials', _u64, []),
     ('bmpow_set_step_trials', None, [_u64]),
@@ -139,6 +144,7 @@ SIGNATURES = [
 
 _lock = threading.Lock()
 _lib = None
+_exit_hooked = False
 
 
 def lib_path():
@@ -166,7 +172,7 @@ def load(path=None):
 
 def get():
     """The initialised library (devices selected).  Raises BmpowUnavailable."""
-    global _lib
+    global _lib, _exit_hooked
     with _lock:
         if _lib is None:
             lib = load()
@@ -174,7 +180,20 @@ def get():
             if rc <= 0:
                 raise BmpowUnavailable(rc, 'bmpow_init failed: %s' % lib.bmpow_last_error().decode())
             _lib = lib
+            if not _exit_hooked:
+                # release the devices (service threads, stepper threads, the streams kept for the
+                # process) while the interpreter is still whole; the library's own C atexit hook then
+                # finds nothing left to do
+                atexit.register(_at_exit, lib)
+                _exit_hooked = True
         return _lib
+
+
+def _at_exit(lib):
+    """Python's exit: ``bmpow_atexit`` (include/bmpow.h) before the HIP runtime's exit handlers."""
+    fn = getattr(lib, 'bmpow_atexit', None)
+    if fn is not None:
+        fn()
 
 
 def reset():

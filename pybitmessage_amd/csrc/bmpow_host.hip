@@ -67,6 +67,17 @@ class FairMutex {
     }
     cv_.notify_all();
   }
+  // take the lock only if it comes free (no holder, no one queued) within d; false otherwise (the
+  // process's exit hook: a call still running in another thread is left alone)
+  bool try_lock_for(std::chrono::milliseconds d) {
+    std::unique_lock<std::mutex> lk(m_);
+    if (!cv_.wait_for(lk, d, [&] {
+          return serving_.load(std::memory_order_relaxed) == next_.load(std::memory_order_relaxed);
+        }))
+      return false;
+    next_.fetch_add(1, std::memory_order_relaxed);  // our ticket is the one being served
+    return true;
+  }
   // threads waiting for the lock (while one holds it)
   uint64_t waiting() const {
     const uint64_t n = next_.load(std::memory_order_relaxed), s = serving_.load(std::memory_order_relaxed);
@@ -79,6 +90,11 @@ class FairMutex {
   std::atomic<uint64_t> next_{0}, serving_{0};
 };
 FairMutex g_mu;  // one entry point at a time (the steppers never take it)
+// run()'s single-object state (g_ones, g_xone, the call ring, the streams run() launches on): held by a
+// 64-byte run() for its whole call -- which releases g_mu while it waits for its windows, so the batch
+// service steps between them -- and by every entry point that frees or re-plans that state (device
+// selection, shutdown, the split knob).  Lock order: g_one_mu, then g_mu.
+std::timed_mutex g_one_mu;
 std::atomic<int> g_abort{0};
 std::atomic<uint64_t> g_step_trials{kDefaultStepTrials};  // read without the lock (bmpow_get_step_trials)
 
@@ -205,9 +221,14 @@ std::vector<Shard> g_shards;
 // The cross-shard bound (bmpow_layout.h): BM_MAX_SHARDS rows of BM_XSLOTS words, host-pinned, coherent
 // and mapped into every device; allocated with the shard set.
 unsigned long long* g_xb = nullptr;
-// Columns a work item may get per shard: the device's resident workgroups over the shards sharing
-// it, so every shard's sweep is on the chip at once.
-uint32_t g_resident = 0;
+// Columns a work item may get per shard.  Shards of one device form one device group of the engine
+// (bmsched::PlanCtx::group): they never hold one object at once and never split a window among
+// themselves, so an item may have all of its device's resident workgroups (g_dev_resident).  Under the
+// rehearsal knob (bmpow_set_engine_split: every shard its own group, as separate GPUs) the pieces of a
+// split window share a device, and each gets the device's resident workgroups over the shards sharing
+// it (g_resident), so every piece's sweep is on the chip at once.
+uint32_t g_resident = 0, g_dev_resident = 0;
+bool g_engine_split = false;
 // The per-device steppers over the shard set (created with it; bmsched::Engine).
 std::unique_ptr<bmsched::Engine> g_engine;
 bool g_inited = false;
@@ -367,6 +388,25 @@ void make_engine() {
   }
 }
 
+// Hand the engine its device groups (one per physical device, or every shard its own under
+// bmpow_set_engine_split) and the matching column cap; drains what is in flight.
+void apply_engine_groups() {
+  if (!g_engine) return;
+  std::vector<uint16_t> group;
+  uint32_t resident = g_resident;
+  if (!g_engine_split) {
+    std::vector<int> devs;
+    for (const Shard& sh : g_shards) {
+      size_t g = (size_t)(std::find(devs.begin(), devs.end(), sh.dev) - devs.begin());
+      if (g == devs.size()) devs.push_back(sh.dev);
+      group.push_back((uint16_t)g);
+    }
+    resident = g_dev_resident;
+  }
+  std::unique_lock<std::mutex> lk(g_engine->mu);
+  g_engine->set_groups(lk, group, resident);
+}
+
 void free_one();
 
 int select_devices(const std::vector<int>& ids) {
@@ -391,6 +431,7 @@ int select_devices(const std::vector<int>& ids) {
     for (size_t i = 0; i < (size_t)BM_MAX_SHARDS * BM_XSLOTS; ++i) g_xb[i] = ~0ULL;
   }
   g_resident = ~0u;
+  g_dev_resident = ~0u;
   for (auto& sh : g_shards) {
     HIPTRY(hipSetDevice(sh.dev));
     void* dp = nullptr;
@@ -406,12 +447,17 @@ int select_devices(const std::vector<int>& ids) {
     if (const char* e = std::getenv("GPU_MAX_HW_QUEUES"))
       if (std::atoi(e) > 0) hwq = (uint32_t)std::atoi(e);
     g_resident = std::min<uint32_t>(g_resident, std::max<uint32_t>(1, sh.resident / std::min(same, hwq)));
+    g_dev_resident = std::min<uint32_t>(g_dev_resident, std::max<uint32_t>(1, sh.resident));
   }
   make_engine();
+  apply_engine_groups();
   return (int)g_shards.size();
 }
 
+bool g_exited = false;  // bmpow_atexit ran: no stream may be created again (see g_masked)
+
 int init_locked() {
+  if (g_exited) return set_err(BMPOW_E_STATE, "the process is exiting (bmpow_atexit ran)");
   if (g_inited) return (int)g_shards.size();
   if (const char* w = std::getenv("BMPOW_WAIT"))
     g_wait = std::strcmp(w, "spin") == 0    ? kWaitSpin
@@ -428,6 +474,16 @@ int init_locked() {
   if (const char* w = std::getenv("BMPOW_TRACE")) g_trace = std::atoi(w) != 0;
   if (const char* w = std::getenv("BMPOW_RUN_STREAM")) g_run_stream = std::atoi(w) != 0;
   const auto vis = visible_gfx950();
+  // Release everything at exit, before the HIP runtime's own exit handlers: they were registered when
+  // the runtime initialised (by the call above), and atexit runs handlers last-registered first.  Without
+  // it the stepper threads were joined by g_engine's static destructor, and the streams kept for the
+  // process destroyed by the runtime, after its teardown (a traced process with CU-masked streams alive
+  // ended in a segfault inside the runtime's exit handlers, round 5).
+  static bool hooked = false;
+  if (!hooked) {
+    hooked = true;
+    std::atexit(bmpow_atexit);
+  }
   if (vis.empty()) return set_err(BMPOW_E_NODEV, "no gfx950 (MI355X) device visible to the HIP runtime");
   std::vector<int> ids = vis;
   if (const char* e = std::getenv("BMPOW_BLOCKS_PER_WORKER"))  // A/B knob
@@ -935,6 +991,9 @@ bool g_run_split = false;  // bmpow_set_run_split: one piece per shard even wher
 // caller's own thread here, so it keeps its priority and instead leaves the CPU alone while the GPU
 // works, except for the last few ms of a short call.
 constexpr double kOneSpinMs = 20.0;
+// A run() beside a busy batch expected to take longer than this (one engine launch is ~80 ms) shares the
+// device with the batch instead of going first (search_one_calls)
+constexpr double kOneShareMs = 100.0;
 // a piece's rate before it has a sample: one MI355X's bm_search1_kernel, measured
 constexpr double kOneRateGuess = 6.5e6;
 
@@ -1096,7 +1155,7 @@ std::vector<size_t> one_pieces() {
 // thousand polls per second, each a load of host memory.  The launch's event is queried every few
 // polls, so a launch that ended without writing its result (a fault) is caught instead of waited for
 // forever.
-int wait_one(OnePath& op, uint64_t seq, bool spin) {
+int wait_one(OnePath& op, uint64_t seq, bool spin, double& spin_ms, double& sleep_ms) {
   bm_one_out* o = &op.h_out[seq % BM_ONE_RING];
   const double t0 = now_ms();
   for (uint32_t k = 1;; ++k) {
@@ -1120,12 +1179,15 @@ int wait_one(OnePath& op, uint64_t seq, bool spin) {
     }
   }
   const double ms = now_ms() - t0;
-  (spin ? g_stats.one_wait_spin_ms : g_stats.one_wait_sleep_ms) += ms;
+  (spin ? spin_ms : sleep_ms) += ms;
   return 0;
 }
 
+// g: the library's lock (g_mu), held by the caller, who also holds g_one_mu for the whole call.  It is
+// released while the call waits for a window's pieces, so the batch service's steps go on between
+// run()'s windows (round 6: before, a long run() held it to the end and the batch stalled behind it).
 int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials, uint64_t* nonce_out,
-                     uint64_t* trial_out) {
+                     uint64_t* trial_out, std::unique_lock<FairMutex>& g) {
   const std::vector<size_t> pieces = one_pieces();
   const size_t P = pieces.size();
   for (size_t p = 0; p < P; ++p) {
@@ -1137,29 +1199,6 @@ int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint
       }
     const int rc = ensure_one(pieces[p], slice, slices);
     if (rc < 0) return rc;
-  }
-  // beside a batch with work (the engine's launches on the shard streams): run()'s own stream; else the
-  // shard's.  A piece changing streams first lets the old one drain (a queued window of the previous
-  // call stops at its first block), so its launches stay in call order.
-  bool busy = false;
-  if (g_run_stream && g_engine) {
-    std::lock_guard<std::mutex> el(g_engine->mu);
-    const bmsched::BatchState* b = g_engine->attached();
-    busy = g_engine->in_flight() > 0 || (b && b->pending > 0);
-  }
-  for (size_t p = 0; p < P; ++p) {
-    OnePath& op = g_ones[pieces[p]];
-    if (op.masked) continue;
-    hipStream_t want = g_shards[pieces[p]].stream;
-    if (busy) {
-      HIPTRY(hipSetDevice(op.dev));
-      const int rc = run_stream(op.dev, &want);
-      if (rc < 0) return rc;
-    }
-    if (op.stream != want) {
-      HIPTRY(hipStreamSynchronize(op.stream));
-      op.stream = want;
-    }
   }
   const uint64_t end = (max_trials - 1 > kU64Max - start) ? kU64Max : start + max_trials - 1;  // last nonce
   const uint64_t call = ++g_one_call;  // every call launches on every piece (it resets call + 2's state)
@@ -1193,6 +1232,35 @@ int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint
     if (P > 1 && c > 1) --c;
     cap[p] = std::max<uint32_t>(1, std::min<uint32_t>(c, BM_ONE_MAX_WG));
     rate += (op.rate > 0 ? op.rate : kOneRateGuess * part);
+  }
+  // Beside a batch with work (the engine's launches on the shard streams): a call expected to end within
+  // kOneShareMs (E, or its budget, over the pieces' rate) takes run()'s own stream of the highest priority
+  // -- its windows are dispatched first, and the batch waits at most that long --, a longer one the shard's
+  // stream, where its windows and the engine's launches queue in turn and share the device launch by
+  // launch (with g_mu released between its windows the service keeps the engine fed).  Round 5 gave every
+  // call the priority stream and held g_mu throughout: a C4-difficulty run() stalled the batch for its
+  // whole call.  Else the shard's stream.  A piece changing streams first lets the old one drain (a queued
+  // window of the previous call stops at its first block), so its launches stay in call order.
+  const double expect_ms = std::min(18446744073709551616.0 / ((double)target + 1.0), (double)max_trials) / rate;
+  bool busy = false;
+  if (g_run_stream && g_engine && expect_ms <= kOneShareMs) {
+    std::lock_guard<std::mutex> el(g_engine->mu);
+    const bmsched::BatchState* b = g_engine->attached();
+    busy = g_engine->in_flight() > 0 || (b && b->pending > 0);
+  }
+  for (size_t p = 0; p < P; ++p) {
+    OnePath& op = g_ones[pieces[p]];
+    if (op.masked) continue;
+    hipStream_t want = g_shards[pieces[p]].stream;
+    if (busy) {
+      HIPTRY(hipSetDevice(op.dev));
+      const int rc = run_stream(op.dev, &want);
+      if (rc < 0) return rc;
+    }
+    if (op.stream != want) {
+      HIPTRY(hipStreamSynchronize(op.stream));
+      op.stream = want;
+    }
   }
   // A window: one step per piece (a piece hashes ~1/P of it; bm_one_ctr.acc's trial field).  Pieces
   // that share a device do not all run at once (its hardware queues run 4 kernels; the rest start as
@@ -1275,16 +1343,20 @@ int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint
   int rc = launch();
   while (rc == 0 && want_next()) rc = launch();  // the next window, queued behind
   while (rc == 0) {
-    // the oldest window: every piece's launch
+    // the oldest window: every piece's launch, waited for without the library's lock (only this
+    // call's pieces are read meanwhile: g_one_mu keeps every other user of them out)
     bool found = false;
     uint64_t best = 0, best_trial = 0;
-    double span = 0;
+    double span = 0, spin_ms = 0, sleep_ms = 0;
+    const bool spin = g_one_wait == kOneSpin || (g_one_wait == kOneAuto && short_call);
+    g.unlock();
+    for (size_t p = 0; p < P && rc == 0; ++p) rc = wait_one(g_ones[pieces[p]], fly[0].seq[p], spin, spin_ms, sleep_ms);
+    g.lock();
+    g_stats.one_wait_spin_ms += spin_ms;
+    g_stats.one_wait_sleep_ms += sleep_ms;
     for (size_t p = 0; p < P && rc == 0; ++p) {
       OnePath& op = g_ones[pieces[p]];
       const uint64_t seq = fly[0].seq[p];
-      const bool spin = g_one_wait == kOneSpin || (g_one_wait == kOneAuto && short_call);
-      rc = wait_one(op, seq, spin);
-      if (rc < 0) break;
       const bm_one_out& o = op.h_out[seq % BM_ONE_RING];
       const double ms = (double)(o.t1 - o.t0) * 1e-5;  // s_memrealtime: 100 MHz
       g_stats.launches++;
@@ -1325,8 +1397,8 @@ int search_one_calls(const uint8_t ih[64], uint64_t target, uint64_t start, uint
 }
 
 int search_one(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t max_trials, uint64_t* nonce_out,
-               uint64_t* trial_out) {
-  const int rc = search_one_calls(ih, target, start, max_trials, nonce_out, trial_out);
+               uint64_t* trial_out, std::unique_lock<FairMutex>& g) {
+  const int rc = search_one_calls(ih, target, start, max_trials, nonce_out, trial_out, g);
   // A call that failed may have launched on only some pieces (or none): the pieces it skipped did not
   // put the state of the call two ahead back to "no hit", which that call would then read.  Start the
   // ring afresh (an abort comes only after every piece's first launch, so it keeps the ring).
@@ -1823,11 +1895,23 @@ struct bmpow_service {
 
 namespace {
 
+// Services not yet destroyed: bmpow_atexit stops their threads before it releases the devices.
+std::mutex g_svc_mu;
+std::vector<bmpow_service*> g_live_services;
+
+// A service op finds the library shut down (bmpow_shutdown / resetPoW under a live service): an error
+// the service reports through its poll, never a step on released devices.
+int engine_gone(std::string& err) {
+  err = "the library was shut down under this service";
+  return BMPOW_E_STATE;
+}
+
 bmsched::ServiceOps service_ops(bmpow_service* s) {
   bmsched::ServiceOps ops;
   ops.add = [s](size_t n, const uint8_t* ihs, const uint64_t* ih_off, const uint64_t* tg, uint32_t* slots,
                 std::string& err) {
     std::lock_guard<FairMutex> g(g_mu);
+    if (!g_engine || s->b->dev.size() != g_shards.size()) return engine_gone(err);
     std::unique_lock<std::mutex> lk(g_engine->mu);
     const int rc = batch_add_locked(lk, s->b, n, ihs, tg, nullptr, slots, ih_off);
     if (rc < 0) err = g_err;
@@ -1837,6 +1921,7 @@ bmsched::ServiceOps service_ops(bmpow_service* s) {
   // as an object finished, so the service hands it out while the devices go on
   ops.step = [s](std::string& err) {
     std::lock_guard<FairMutex> g(g_mu);
+    if (!g_engine || s->b->dev.size() != g_shards.size()) return engine_gone(err);
     std::unique_lock<std::mutex> lk(g_engine->mu);
     g_engine->attach(lk, s->b);
     bmpow_batch* b = s->b;
@@ -1846,13 +1931,15 @@ bmsched::ServiceOps service_ops(bmpow_service* s) {
                          [b] { return b->finished_head < b->finished.size() || b->pending == 0 || g_mu.waiting() > 0; },
                          err);
   };
-  ops.take = [s](size_t cap, uint32_t* slot, uint64_t* nonce, uint64_t* trial, uint8_t* done) {
+  ops.take = [s](size_t cap, uint32_t* slot, uint64_t* nonce, uint64_t* trial, uint8_t* done) -> size_t {
     std::lock_guard<FairMutex> g(g_mu);
+    if (!g_engine) return 0;
     std::lock_guard<std::mutex> lk(g_engine->mu);
     return bmsched::take_done(*s->b, cap, slot, nonce, trial, done);
   };
   ops.reset = [s](std::string& err) {
     std::lock_guard<FairMutex> g(g_mu);
+    if (!g_engine) return engine_gone(err);
     std::unique_lock<std::mutex> lk(g_engine->mu);
     if (g_engine->attached() == s->b) g_engine->detach(lk);
     batch_free_dev(s->b);
@@ -1880,6 +1967,7 @@ int bmpow_init(void) {
 int bmpow_device_count(void) { return (int)visible_gfx950().size(); }
 
 int bmpow_set_devices(const int* ids, int n) {
+  std::lock_guard<std::timed_mutex> one(g_one_mu);
   std::lock_guard<FairMutex> lk(g_mu);
   if (n < 0) return set_err(BMPOW_E_ARG, "bad device list");
   std::vector<int> v;
@@ -1932,8 +2020,7 @@ int bmpow_get_shard_rates(double* rates, int cap) {
   return (int)g_shards.size();
 }
 
-void bmpow_shutdown(void) {
-  std::lock_guard<FairMutex> lk(g_mu);
+static void shutdown_locked() {
   if (g_engine) {
     std::unique_lock<std::mutex> el(g_engine->mu);
     drop_scratch(el);
@@ -1946,6 +2033,43 @@ void bmpow_shutdown(void) {
   if (g_xb) (void)hipHostFree(g_xb);
   g_xb = nullptr;
   g_inited = false;
+}
+
+void bmpow_shutdown(void) {
+  std::lock_guard<std::timed_mutex> one(g_one_mu);
+  std::lock_guard<FairMutex> lk(g_mu);
+  shutdown_locked();
+}
+
+void bmpow_atexit(void) {
+  // the services' threads step the engine: stopped (joined after their current op) first
+  std::vector<bmpow_service*> live;
+  {
+    std::lock_guard<std::mutex> g(g_svc_mu);
+    live = g_live_services;
+  }
+  for (bmpow_service* s : live) s->svc->stop();
+  // a call still running in another thread (a daemon thread at interpreter exit) keeps the library
+  std::unique_lock<std::timed_mutex> one(g_one_mu, std::chrono::milliseconds(5000));
+  if (!one.owns_lock() || !g_mu.try_lock_for(std::chrono::milliseconds(5000))) return;
+  if (!g_exited) {
+    g_exited = true;
+    shutdown_locked();
+    // the streams kept for the life of the process (no stream is created after this: init refuses)
+    for (const MaskedStream& m : g_masked) {
+      (void)hipSetDevice(m.dev);
+      (void)hipStreamSynchronize(m.stream);
+      (void)hipStreamDestroy(m.stream);
+    }
+    g_masked.clear();
+    for (const auto& r : g_run_streams) {
+      (void)hipSetDevice(r.first);
+      (void)hipStreamSynchronize(r.second);
+      (void)hipStreamDestroy(r.second);
+    }
+    g_run_streams.clear();
+  }
+  g_mu.unlock();
 }
 
 const char* bmpow_last_error(void) { return g_err.c_str(); }
@@ -2013,7 +2137,8 @@ int bmpow_search(const uint8_t ih[64], uint64_t target, uint64_t start, uint64_t
 
 int bmpow_search_len(const uint8_t* ih, size_t ih_len, uint64_t target, uint64_t start, uint64_t max_trials,
                      uint64_t* nonce_out, uint64_t* trial_out) {
-  std::lock_guard<FairMutex> g(g_mu);
+  std::lock_guard<std::timed_mutex> one(g_one_mu);
+  std::unique_lock<FairMutex> g(g_mu);
   int rc = init_locked();
   if (rc < 0) return rc;
   if ((!ih && ih_len) || !nonce_out || !trial_out) return set_err(BMPOW_E_ARG, "null pointer");
@@ -2022,7 +2147,7 @@ int bmpow_search_len(const uint8_t* ih, size_t ih_len, uint64_t target, uint64_t
   if (g_abort.load()) return set_err(BMPOW_E_ABORTED, "aborted");
   // every 64-byte object takes the single-object path, on any number of devices (round 5; before, only
   // one shard did and several took the engine's split windows)
-  if (ih_len == 64 && g_one_enabled) return search_one(ih, target, start, max_trials, nonce_out, trial_out);
+  if (ih_len == 64 && g_one_enabled) return search_one(ih, target, start, max_trials, nonce_out, trial_out, g);
   const uint8_t zero = 0;
   const uint64_t off[2] = {0, ih_len};
   std::unique_lock<std::mutex> lk(g_engine->mu);
@@ -2277,6 +2402,8 @@ bmpow_service* bmpow_service_create(uint64_t step_budget, uint32_t flags) {
     s->budget = step_budget;
   }
   s->svc.reset(new bmsched::Service(service_ops(s), (flags & BMPOW_SERVICE_VERIFY) != 0));
+  std::lock_guard<std::mutex> g(g_svc_mu);
+  g_live_services.push_back(s);
   return s;
 }
 
@@ -2327,6 +2454,10 @@ void bmpow_service_stop(bmpow_service* s) {
 
 void bmpow_service_destroy(bmpow_service* s) {
   if (!s) return;
+  {
+    std::lock_guard<std::mutex> g(g_svc_mu);
+    g_live_services.erase(std::remove(g_live_services.begin(), g_live_services.end(), s), g_live_services.end());
+  }
   s->svc.reset();  // joins the service thread after its current op
   std::lock_guard<FairMutex> g(g_mu);
   if (g_engine) {
@@ -2588,6 +2719,10 @@ int bmpow_get_stats(bmpow_stats* out) {
     double mx = 0;
     for (double ms : es.shard_ms) mx = std::max(mx, ms);
     out->max_shard_kernel_ms += mx;
+    out->past_window += es.waste.window;
+    out->past_later += es.waste.later;
+    out->past_split += es.waste.split;
+    out->engine_hashed_est += es.waste.hashed;
   }
   return 0;
 }
@@ -2624,6 +2759,7 @@ int bmpow_get_shard_stats(uint64_t* trials, double* kernel_ms, int cap) {
 }
 
 int bmpow_set_run_split(int per_shard) {
+  std::lock_guard<std::timed_mutex> one(g_one_mu);
   std::lock_guard<FairMutex> lk(g_mu);
   const int prev = g_run_split ? 1 : 0;
   if (per_shard < 0) return prev;
@@ -2631,6 +2767,17 @@ int bmpow_set_run_split(int per_shard) {
     // a shard that carries no piece misses the ring resets of the calls it sits out: start afresh
     free_one();
     g_run_split = per_shard != 0;
+  }
+  return prev;
+}
+
+int bmpow_set_engine_split(int per_shard) {
+  std::lock_guard<FairMutex> lk(g_mu);
+  const int prev = g_engine_split ? 1 : 0;
+  if (per_shard < 0) return prev;
+  if ((per_shard != 0) != g_engine_split) {
+    g_engine_split = per_shard != 0;
+    apply_engine_groups();
   }
   return prev;
 }

@@ -132,9 +132,11 @@ void restart_slot(BatchState& b, size_t k, uint64_t st) {
   b.top[k] = 0;
   b.holder[k] = kNoHolder;
   b.nfly[k] = 0;
+  b.fly1[k] = b.fly2[k] = 0;
   b.xs[k] = 0;
   b.open[k].clear();
   b.wseq[k] = 0;
+  b.wrec[k].clear();
 }
 
 void grow_slots(BatchState& b, size_t n) {
@@ -149,9 +151,12 @@ void grow_slots(BatchState& b, size_t n) {
   b.top.resize(n, 0);
   b.holder.resize(n, kNoHolder);
   b.nfly.resize(n, 0);
+  b.fly1.resize(n, 0);
+  b.fly2.resize(n, 0);
   b.xs.resize(n, 0);
   b.open.resize(n);
   b.wseq.resize(n, 0);
+  b.wrec.resize(n);
 }
 
 }  // namespace
@@ -502,17 +507,33 @@ uint64_t resume_point(const BatchState& b, size_t o) {
   return b.next[o];
 }
 
+namespace {
+inline uint64_t sbit(size_t s) { return 1ULL << (s & 63); }
+}  // namespace
+
 bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L) {
   while (b.first_pending < b.n && b.done[b.first_pending] != BMPOW_PENDING) ++b.first_pending;
   if (b.pending == 0 || b.broken) return false;
+  const size_t S = std::max<size_t>(c.S, 1);
+  const bool grouped = c.group && c.group->size() >= S;
+  const size_t D = grouped ? std::max<size_t>(c.D, 1) : S;
+  // the other shards on this shard's device: they never hold one of its objects at the same time
+  uint64_t mates = 0;
+  if (grouped)
+    for (size_t t = 0; t < S; ++t)
+      if (t != c.s && (*c.group)[t] == (*c.group)[c.s]) mates |= sbit(t);
   thread_local std::vector<uint32_t> cand, take;
   cand.clear();
   take.clear();
-  for (size_t i = b.first_pending; i < b.n; ++i)
-    if (claimable(b, i)) cand.push_back((uint32_t)i);
+  size_t C = 0;  // claimable objects (by any shard)
+  for (size_t i = b.first_pending; i < b.n; ++i) {
+    if (!claimable(b, i)) continue;
+    ++C;
+    if (b.fly1[i] & mates) continue;  // another shard of this device has the object in flight
+    cand.push_back((uint32_t)i);
+  }
   if (cand.empty()) return false;
-  const size_t S = std::max<size_t>(c.S, 1), C = cand.size();
-  const bool split = S > 1 && C < S;
+  const bool split = D > 1 && C < D;
   if (split || S == 1) {
     take = cand;
   } else {
@@ -568,11 +589,11 @@ bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L) {
       cl.piece = w.claimed++;
     } else {
       const uint64_t st = b.next[o], lim = b.lim[o];
-      const uint16_t P = split ? (uint16_t)S : 1;
+      const uint16_t P = split ? (uint16_t)D : 1;
       uint64_t want = (k + (nth++ < spare ? 1 : 0)) * chunk;
       if (split) {
-        const uint64_t cap = expect_cap(b.objs[o].target, S, chunk);
-        want = std::min<uint64_t>(cap, (k * chunk > kU64Max / S) ? kU64Max : k * chunk * S);
+        const uint64_t cap = expect_cap(b.objs[o].target, P, chunk);
+        want = std::min<uint64_t>(cap, (k * chunk > kU64Max / P) ? kU64Max : k * chunk * P);
       }
       const uint64_t room = lim - st;  // nonces after st up to lim
       if (want - 1 >= room) {
@@ -602,6 +623,8 @@ bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L) {
     if (b.nfly[o] == 0) b.holder[o] = (int16_t)c.s;
     else if (b.holder[o] != (int16_t)c.s) b.holder[o] = kShared;
     b.nfly[o]++;
+    if (b.fly1[o] & sbit(c.s)) b.fly2[o] |= sbit(c.s);
+    else b.fly1[o] |= sbit(c.s);
     if (c.xp && !b.xs[o] && (cl.P > 1 || b.holder[o] == kShared)) {
       const int x = c.xp->alloc(o, &b);
       if (x >= 0) {
@@ -677,12 +700,58 @@ const Claim* unfly(BatchState& b, const Launch& L, const bm_item& it) {
   if (o >= b.n || b.gen[o] != cl.gen) return nullptr;  // stale: the slot restarted since the plan
   if (b.nfly[o]) b.nfly[o]--;
   if (b.nfly[o] == 0) b.holder[o] = kNoHolder;
+  const uint64_t bit = sbit(L.shard);
+  if (b.fly2[o] & bit) b.fly2[o] &= ~bit;
+  else b.fly1[o] &= ~bit;
   return &cl;
+}
+
+// Price the object's applied items against its answer once that is final (WasteStats).  With no hit
+// and nothing in flight, every applied item lies below any hit to come (later windows start at the
+// frontier): none of them hashed past an answer.
+void price_waste(BatchState& b, uint32_t o, WasteStats& w) {
+  std::vector<WasteRec>& rs = b.wrec[o];
+  if (rs.empty()) return;
+  uint64_t h;
+  if (b.done[o] == BMPOW_DONE_FOUND) h = b.nonce[o];
+  else if (b.done[o] == BMPOW_DONE_EXHAUSTED || (!b.hit[o] && b.nfly[o] == 0)) h = kU64Max;
+  else return;  // a hit that is not final yet, or items in flight that may hold one below these
+  for (const WasteRec& r : rs) {
+    uint64_t above = 0, hashed = 0;
+    waste_of(r, h, above, hashed);
+    w.hashed += hashed;
+    if (r.P > 1) w.split += above;
+    else if (r.start > h) w.later += above;
+    else w.window += above;
+  }
+  rs.clear();
 }
 
 }  // namespace
 
-size_t apply_launch(BatchState& b, const Launch& L, XPool* xp, const std::function<void(uint32_t, uint64_t)>& publish) {
+void waste_of(const WasteRec& r, uint64_t h, uint64_t& above, uint64_t& hashed) {
+  const uint64_t nblk = r.count / BM_BLOCK + (r.count % BM_BLOCK ? 1 : 0);
+  const uint64_t gn = std::max<uint32_t>(r.gn, 1), nwg = std::max<uint32_t>(r.nwg, 1);
+  // units of the item's queue whose block is at or below block x (bm_block_of: row k / nwg, column
+  // g0 + k % nwg): the rows below x's, then the item's columns of x's row up to x
+  auto upto = [&](uint64_t x) -> uint64_t {
+    const uint64_t row = x / gn, rem = x - row * gn;
+    return row * nwg + (rem + 1 > r.g0 ? std::min<uint64_t>(nwg, rem + 1 - r.g0) : 0);
+  };
+  const uint64_t units = nblk ? upto(nblk - 1) : 0;
+  const uint64_t got = r.taken > nwg ? std::min<uint64_t>(r.taken - nwg, units) : 0;
+  hashed = got * BM_BLOCK;
+  if (h < r.start) {
+    above = hashed;
+    return;
+  }
+  const uint64_t hb = (h - r.start) / BM_BLOCK;
+  const uint64_t below = hb >= nblk ? units : upto(hb);
+  above = got > below ? (got - below) * BM_BLOCK : 0;
+}
+
+size_t apply_launch(BatchState& b, const Launch& L, XPool* xp, const std::function<void(uint32_t, uint64_t)>& publish,
+                    WasteStats* waste) {
   const std::vector<bm_item>& items = L.plan.items[0];
   thread_local std::vector<uint32_t> touched;
   touched.clear();
@@ -701,10 +770,14 @@ size_t apply_launch(BatchState& b, const Launch& L, XPool* xp, const std::functi
       b.trial[o] = r.trial;
       if (b.xs[o] && publish) publish(b.xs[o] - 1u, r.nonce);
     }
+    if (waste)
+      b.wrec[o].push_back(WasteRec{cl->start, cl->count, items[k].g0, items[k].gn, items[k].nwg, r.pad, cl->P});
     touched.push_back(o);
   }
   size_t fin = 0;
   for (uint32_t o : touched) fin += settle(b, o) ? 1 : 0;
+  if (waste)
+    for (uint32_t o : touched) price_waste(b, o, *waste);
   release_xslots(b, L, xp);
   for (uint32_t o : touched) free_idle_xslot(b, o, xp);
   return fin;
@@ -1260,7 +1333,7 @@ void Service::loop() {
 // Engine: one stepper thread per shard
 // ---------------------------------------------------------------------------------------
 Engine::Engine(EngineOps ops, size_t S, uint32_t resident, uint64_t step_trials)
-    : ops_(std::move(ops)), S_(S), resident_(resident), step_(step_trials), sh_(S) {
+    : ops_(std::move(ops)), S_(S), resident_(resident), D_(S), step_(step_trials), sh_(S) {
   rates.reset(S);
   stats.shard_ms.assign(S, 0.0);
   stats.shard_trials.assign(S, 0);
@@ -1285,6 +1358,22 @@ Engine::~Engine() {
 void Engine::set_throttle(size_t s, double ms) {
   std::lock_guard<std::mutex> lk(mu);
   if (s < S_) sh_[s].throttle_ms = ms;
+}
+
+void Engine::set_groups(std::unique_lock<std::mutex>& lk, const std::vector<uint16_t>& group, uint32_t resident) {
+  // the per-object holdings (fly1/fly2, a window's smask) are read against the groups: nothing in flight
+  drain(lk);
+  if (group.size() == S_) {
+    group_ = group;
+    std::vector<uint16_t> ids(group);
+    std::sort(ids.begin(), ids.end());
+    D_ = (size_t)(std::unique(ids.begin(), ids.end()) - ids.begin());
+  } else {
+    group_.clear();
+    D_ = S_;
+  }
+  resident_ = resident;
+  cv_.notify_all();
 }
 
 bool Engine::can_plan() const {
@@ -1326,6 +1415,10 @@ void Engine::stepper(size_t s) {
       PlanCtx c;
       c.s = s;
       c.S = S_;
+      if (!group_.empty()) {
+        c.group = &group_;
+        c.D = D_;
+      }
       c.budget = std::min<uint64_t>(step_, limit_ - claimed_);
       c.resident = resident_;
       std::vector<double> w;
@@ -1390,9 +1483,12 @@ void Engine::stepper(size_t s) {
         stats.shard_ms[s] += L.ms;
         stats.shard_trials[s] += L.trials;
         rates.sample(s, L.trials, L.ms);
-        apply_launch(*L.batch, L, &xp_, [this](uint32_t x, uint64_t v) {
-          if (ops_.xstore) ops_.xstore(x, v);
-        });
+        apply_launch(
+            *L.batch, L, &xp_,
+            [this](uint32_t x, uint64_t v) {
+              if (ops_.xstore) ops_.xstore(x, v);
+            },
+            &stats.waste);
       }
       cv_.notify_all();
       continue;

@@ -62,6 +62,25 @@ struct OpenWin {
   uint16_t seq;               // the object's window number (BatchState::wseq; claimable's cap)
 };
 
+// One applied item whose share of the trials past the object's answer is not known yet (the answer
+// was not final when it was applied): kept per object until it settles (BatchState::wrec).
+struct WasteRec {
+  uint64_t start, count;  // the window
+  uint32_t g0, gn, nwg;   // the item's columns (bmpow_layout.h)
+  uint32_t taken;         // units its block queue handed out (bm_result.pad, from the resolve kernel)
+  uint16_t P;
+};
+
+// Trials hashed past the objects' answers, by where they were hashed (EngineStats; estimates from the
+// block queues: every workgroup ends on one unit it takes and does not hash, so of the `taken` units
+// handed out the first taken - nwg are counted as hashed).
+struct WasteStats {
+  uint64_t window = 0;  // unsplit windows holding the answer: blocks above it
+  uint64_t later = 0;   // unsplit windows starting above the answer (the lookahead queued behind)
+  uint64_t split = 0;   // pieces of split windows: blocks above the answer
+  uint64_t hashed = 0;  // every item's estimated hashed nonces (checks the estimate against trials)
+};
+
 // Holder of an object's in-flight windows (BatchState::holder): none, one shard (its index), or
 // several shards at once.
 constexpr int16_t kNoHolder = -1, kShared = -2;
@@ -98,8 +117,12 @@ struct BatchState {
   std::vector<int16_t> holder;   // shard holding the object's in-flight items, kNoHolder or kShared
   std::vector<uint32_t> nfly;    // the object's items in flight
   std::vector<uint8_t> xs;       // cross-shard bound slot + 1 while the object is shared, 0 none
+  // shards with items of the object in flight (a shard has at most two: its running and staged
+  // launch): bit s of fly1 = at least one, of fly2 = two
+  std::vector<uint64_t> fly1, fly2;
   std::vector<std::vector<OpenWin>> open;  // windows not yet fully applied, ascending start
   std::vector<uint16_t> wseq;    // the number the object's next window gets (wraps; only differences count)
+  std::vector<std::vector<WasteRec>> wrec;  // applied items not yet priced against the final answer
   bool broken = false;           // a launch was lost to a device error: only reset() continues it
 };
 
@@ -181,7 +204,7 @@ struct ShardRates {
   bool weights(std::vector<double>& w) const;
 };
 
-// A window split over the shards (P = S pieces) covers kExpectWindows x E nonces (E = 2^64 /
+// A window split over the device groups (P = D pieces) covers kExpectWindows x E nonces (E = 2^64 /
 // (target + 1), the expected trials to a hit; at least one chunk per piece): a split object then
 // takes about one round of pieces, and with the cross-shard bound the pieces above a hit stop within
 // a block row of it.  An object owned by one shard is not capped: its own early exit stops at its hit.
@@ -243,6 +266,13 @@ struct XPool {
 // What plan_launch needs to know about the shard it plans for.
 struct PlanCtx {
   size_t s = 0, S = 1;
+  // Device groups: group[s] = the physical device of shard s (ids 0 .. D-1), null = every shard its own.
+  // Shards of one group share a device's SIMDs, where the kernel launched first holds the older waves:
+  // two of them on one object would race each other's columns, so they never hold one object at once
+  // and a split window has one piece per group (round 6; run()'s pieces follow the same rule).  A group
+  // of one shard is the round-5 engine exactly.
+  const std::vector<uint16_t>* group = nullptr;
+  size_t D = 0;              // groups (0: S)
   uint64_t budget = 0;       // nonces this launch may claim (at least one chunk is claimed)
   uint32_t resident = 0;     // columns a piece may get on this shard (0 = no cap)
   double weight = 1.0;       // the shard's rate over the mean (ShardRates)
@@ -258,21 +288,28 @@ constexpr uint16_t kMaxOpen = 2;
 bool claimable(const BatchState& b, size_t o);
 
 // Plan the next launch of shard c.s from the claimable objects (slot order):
-//   * object mode (at least S claimable objects, or S == 1): the shard takes its fair share q =
+//   * object mode (at least D claimable objects, or one group): the shard takes its fair share q =
 //     ceil(C x weight / S) of them -- those it already holds first, then ones no shard holds, then
 //     (only if it found none) ones other shards hold -- each a window of budget / taken nonces;
-//   * split mode (fewer claimable objects than shards): every object, one piece each of windows of
-//     P = S pieces, expect_cap nonces per window;
-//   * an object whose latest window still has pieces to hand out gets the next piece first.
+//   * split mode (fewer claimable objects than groups): every object, one piece each of windows of
+//     P = D pieces, expect_cap nonces per window;
+//   * an object whose latest window still has pieces to hand out gets the next piece first;
+//   * never an object another shard of the shard's group has in flight (with one group: no split, and
+//     each object on one shard at a time, its windows in order on that shard's stream).
 // Objects with items on several shards get a cross-shard bound slot (c.xp).  Returns false (L
 // untouched) when nothing is claimable.
 bool plan_launch(BatchState& b, const PlanCtx& c, Launch& L);
 
 // Fold a completed launch into the state (results L.res[k] for L.plan.items[0][k]); an object that
 // becomes final is queued for take_done.  publish(xslot, nonce): a new least hit of a shared object,
-// for the other shards' relays.  Returns the objects finished by it.
+// for the other shards' relays.  waste (may be null): trials past the answers, priced once an object's
+// answer is final (L.res[k].pad = the units item k's block queue handed out).  Returns the objects
+// finished by it.
 size_t apply_launch(BatchState& b, const Launch& L, XPool* xp,
-                    const std::function<void(uint32_t, uint64_t)>& publish);
+                    const std::function<void(uint32_t, uint64_t)>& publish, WasteStats* waste = nullptr);
+// Nonces of an item hashed above nonce h (all of them when h lies below its window), and the nonces it
+// hashed in all: the first taken - nwg units its queue handed out, clipped to its blocks (WasteStats).
+void waste_of(const WasteRec& r, uint64_t h, uint64_t& above, uint64_t& hashed);
 // A launch that was never enqueued (an error before its kernels): its items are no longer in flight,
 // and its windows never complete (the batch is broken).
 void drop_launch(BatchState& b, const Launch& L, XPool* xp);
@@ -293,6 +330,7 @@ struct EngineStats {
   double kernel_ms = 0;
   std::vector<double> shard_ms;      // per shard: summed kernel time
   std::vector<uint64_t> shard_trials;
+  WasteStats waste;                  // trials past the answers, by phase (apply_launch)
 };
 
 class Engine {
@@ -318,6 +356,10 @@ class Engine {
   void notify() { cv_.notify_all(); }  // after changing the attached batch's state (add, set_pending)
   void set_step_trials(uint64_t t) { step_ = t; }
   void set_throttle(size_t s, double ms);  // A/B knob: a shard sleeps this long before each launch
+  // Device groups (PlanCtx::group; empty = every shard its own) and the columns an item may get, after
+  // draining what is in flight.  lk holds mu.
+  void set_groups(std::unique_lock<std::mutex>& lk, const std::vector<uint16_t>& group, uint32_t resident);
+  size_t groups() const { return D_; }
   size_t shards() const { return S_; }
   size_t in_flight() const { return inflight_; }
   // Cross-shard bound slots with an owner (under mu); gc: first give back those no object needs.  After
@@ -346,7 +388,9 @@ class Engine {
   bool can_plan() const;
   EngineOps ops_;
   const size_t S_;
-  const uint32_t resident_;
+  uint32_t resident_;
+  std::vector<uint16_t> group_;  // empty: every shard its own group
+  size_t D_;
   uint64_t step_;
   std::vector<EShard> sh_;
   BatchState* b_ = nullptr;

@@ -36,7 +36,9 @@ __device__ uint64_t trial_obj(const bm_obj* o, uint64_t nonce, const uint64_t* v
 
 // For each launched item whose object has a hit, recompute the trial value at the winning
 // nonce (one thread per item).  res[k] = {nonce, trial, found = 1} or {UINT64_MAX, 0, found = 0}:
-// the found flag, not the nonce, says whether there is a hit (2^64-1 is a legal answer).
+// the found flag, not the nonce, says whether there is a hit (2^64-1 is a legal answer).  res[k].pad =
+// the units item k's block queue handed out (trials[2 + k], clipped to 32 bits): the host's estimate of
+// the trials hashed past the answers (bmsched::WasteStats).
 __global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item* __restrict__ items,
                                   uint32_t nitems, unsigned long long* __restrict__ best,
                                   uint32_t* __restrict__ found, bm_result* __restrict__ res,
@@ -57,7 +59,8 @@ __global__ void bm_resolve_kernel(const bm_obj* __restrict__ objs, const bm_item
   r.nonce = best[obj];
   r.trial = 0;
   r.found = found[obj];
-  r.pad = 0;
+  const unsigned long long taken = trials[2 + k];
+  r.pad = taken > 0xffffffffULL ? 0xffffffffu : (uint32_t)taken;
   if (r.found) r.trial = trial_obj(objs + obj, r.nonce, vpool);
   res[k] = r;
   // best[] / found[] are left as they are: a launch queued behind this one on the stream (the

@@ -55,6 +55,15 @@ def shards(gpulib):
     gpulib.bmpow_set_step_trials(0)  # the library's default
 
 
+@pytest.fixture
+def engine_split(gpulib):
+    """bmpow_set_engine_split for the test body (every shard its own device group: the multi-device
+    split rehearsed on one GPU), restored after."""
+    prev = gpulib.bmpow_set_engine_split(-1)
+    yield lambda on: gpulib.bmpow_set_engine_split(1 if on else 0)
+    gpulib.bmpow_set_engine_split(prev)
+
+
 @pytest.fixture(autouse=True)
 def _reenable_backend():
     """A test that feeds a wrong GPU answer disables the backend process-wide (proofofwork.gpu_failed,

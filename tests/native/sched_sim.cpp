@@ -26,6 +26,7 @@
 #include <memory>
 #include <mutex>
 #include <random>
+#include <set>
 #include <thread>
 #include <vector>
 
@@ -290,7 +291,8 @@ class SimLib {
     uint64_t& best = d.best[it.obj];
     uint32_t& found = d.found[it.obj];
     const uint64_t nblk = (it.count + BM_BLOCK - 1) / BM_BLOCK;
-    for (uint64_t k = 0;; ++k) {
+    uint64_t k = 0;
+    for (;; ++k) {
       const uint64_t blk = block_of(it, k);
       if (blk >= nblk) break;
       if (it.xslot != BM_NO_XSLOT) {  // the relay folds the other shards' hits in
@@ -301,6 +303,10 @@ class SimLib {
       if (best < first) break;  // early exit above the running minimum
       const uint64_t cnt = std::min<uint64_t>(BM_BLOCK, it.count - blk * BM_BLOCK);
       trials += cnt;
+      if (log_blocks_) {
+        std::lock_guard<std::mutex> lk(logmu_);
+        blocks_.push_back({it.obj, first, cnt});
+      }
       for (uint64_t j = 0; j < cnt; ++j) {
         if (sim_trial(o, d.vpool, first + j) <= o.target) {
           const uint64_t n = first + j;
@@ -317,8 +323,25 @@ class SimLib {
     r.nonce = best;
     r.found = found;
     r.trial = found ? sim_trial(o, d.vpool, best) : 0;
+    // the units the item's queue handed out: the k hashed, plus one per workgroup that it took and did
+    // not hash (bm_resolve_kernel's pad; the one sweep stands for the item's nwg workgroups)
+    r.pad = (uint32_t)(k + it.nwg);
+    items_.fetch_add(1);
     return r;
   }
+
+ public:
+  // Hashed blocks (object, first nonce, nonces), logged while log_blocks_ (the waste scenario)
+  struct Blk {
+    uint32_t obj;
+    uint64_t first, cnt;
+  };
+  std::atomic<bool> log_blocks_{false};
+  std::mutex logmu_;
+  std::vector<Blk> blocks_;
+  std::atomic<uint64_t> items_{0};  // items run
+
+ private:
   const size_t S_;
   std::vector<SimDev> dev_;
   std::vector<std::deque<SimCmd>> q_;
@@ -643,6 +666,140 @@ static void scenario_split() {
     }
   }
   fprintf(stderr, "split: interleaved pieces over 8 shards, exact over 2/3/8 shards\n");
+}
+
+// ---- scenario 3b: device groups -- shards sharing a device never hold one object at once ----
+// Round 6: 8 shards on ONE device split tail objects into 8 pieces whose kernels raced
+// each other on the same SIMDs; now the shards of a device form a group (PlanCtx::group): no split
+// within a group, no object on two of its shards at once, and a split window has one piece per group.
+static void scenario_groups() {
+  std::mt19937_64 rng(23);
+  // planning, one group of 8 shards, 3 hard objects: each of the first three shards takes one object
+  // whole (P = 1), the others find nothing; the holders' staged plans take their own objects' next windows
+  {
+    std::vector<Obj> objs = random_objs(rng, 3, 1);
+    for (Obj& o : objs) o.target = kU64Max / 50000000;
+    std::vector<uint8_t> ihs;
+    std::vector<uint64_t> tg, st;
+    pack_list(objs, ihs, tg, st);
+    BatchState b;
+    init(b, 3, ihs.data(), tg.data(), st.data());
+    const std::vector<uint16_t> one(8, 0);
+    XPool xp;
+    std::vector<uint32_t> got(8, ~0u);
+    for (size_t s = 0; s < 8; ++s) {
+      Launch L;
+      L.shard = s;
+      PlanCtx c;
+      c.s = s;
+      c.S = 8;
+      c.group = &one;
+      c.D = 1;
+      c.budget = 1 << 20;
+      c.resident = 1024;
+      c.xp = &xp;
+      const bool ok = plan_launch(b, c, L);
+      if (s < 3) {
+        CHECK(ok && L.claims.size() == 1 && L.claims[0].P == 1, "one group: shard %zu took %zu claims", s,
+              ok ? L.claims.size() : 0);
+        if (ok) got[s] = L.claims[0].obj;
+        CHECK(ok && L.plan.items[0][0].xslot == BM_NO_XSLOT, "one group: an object of one shard needs no bound");
+      } else {
+        CHECK(!ok, "one group: shard %zu found work although every object is held by another shard", s);
+      }
+    }
+    CHECK(got[0] != got[1] && got[1] != got[2] && got[0] != got[2], "one group: an object on two shards");
+    Launch L2;
+    L2.shard = 1;
+    PlanCtx c;
+    c.s = 1;
+    c.S = 8;
+    c.group = &one;
+    c.D = 1;
+    c.budget = 1 << 20;
+    c.resident = 1024;
+    c.xp = &xp;
+    CHECK(plan_launch(b, c, L2) && L2.claims.size() == 1 && L2.claims[0].obj == got[1] &&
+              L2.claims[0].start > b.open[got[1]][0].start,
+          "one group: the holder's staged launch takes its object's next window");
+  }
+  // planning, two groups of three shards, one object: a window of P = 2 pieces, one per group
+  {
+    std::vector<Obj> objs = random_objs(rng, 1, 1);
+    objs[0].target = kU64Max / 12700000;
+    BatchState b;
+    init(b, 1, objs[0].ih, &objs[0].target, &objs[0].start);
+    const std::vector<uint16_t> two = {0, 0, 0, 1, 1, 1};
+    XPool xp;
+    auto plan = [&](size_t s, Launch& L) {
+      L.shard = s;
+      PlanCtx c;
+      c.s = s;
+      c.S = 6;
+      c.group = &two;
+      c.D = 2;
+      c.budget = 1 << 28;
+      c.resident = 1025;
+      c.xp = &xp;
+      return plan_launch(b, c, L);
+    };
+    Launch a, m, x;
+    CHECK(plan(0, a) && a.claims[0].P == 2 && a.claims[0].piece == 0, "two groups: the first piece of two");
+    CHECK(a.plan.items[0][0].count == expect_cap(objs[0].target, 2, a.plan.chunk), "two groups: a 2E window");
+    CHECK(!plan(1, m), "two groups: a shard of the same device took a piece beside its mate");
+    CHECK(plan(4, x) && x.claims[0].piece == 1 && x.claims[0].start == a.claims[0].start, "two groups: the other "
+          "device takes the second piece");
+    CHECK(x.plan.items[0][0].xslot != BM_NO_XSLOT, "two groups: a split window without its cross-shard bound");
+  }
+  // exact answers and the waste accounting: one group of 8 (no split: nothing past the answers but the
+  // rows in flight, here none -- the stand-in's sweep stops at the next block), 2 x 3 and 3 x 2 shards
+  struct Case { std::vector<uint16_t> group; size_t n; uint64_t div; };
+  const Case cases[] = {{std::vector<uint16_t>(8, 0), 24, 60000},
+                        {{0, 0, 0, 1, 1, 1}, 3, 150000},
+                        {{0, 0, 1, 1, 2, 2}, 20, 50000},
+                        {std::vector<uint16_t>(4, 0), 3, 500000}};
+  for (const Case& cs : cases) {
+    const size_t S = cs.group.size();
+    std::vector<Obj> objs = random_objs(rng, cs.n, 1);
+    for (Obj& o : objs) o.target = kU64Max / (cs.div / 2 + rng() % cs.div);
+    std::vector<uint8_t> ihs;
+    std::vector<uint64_t> tg, st;
+    pack_list(objs, ihs, tg, st);
+    std::vector<double> slow(S, 1.0);
+    slow[S - 1] = 2.0;
+    SimLib lib(S, 64, 1 << 16, slow);
+    lib.log_blocks_ = true;
+    {
+      std::unique_lock<std::mutex> lk(lib.eng().mu);
+      lib.eng().set_groups(lk, cs.group, 64);
+    }
+    BatchState b;
+    init(b, cs.n, ihs.data(), tg.data(), st.data());
+    lib.upload(b);
+    solve(lib, b, (uint64_t)S << 16);
+    for (size_t i = 0; i < cs.n; ++i) expect_exact(objs[i], b.done[i], b.nonce[i], b.trial[i], "groups", i);
+    std::unique_lock<std::mutex> lk(lib.eng().mu);
+    lib.eng().detach(lk);
+    const WasteStats& w = lib.eng().stats.waste;
+    // the truth from the stand-in's log: nonces of blocks hashed that start above the object's answer
+    uint64_t past = 0;
+    {
+      std::lock_guard<std::mutex> g(lib.logmu_);
+      for (const auto& x : lib.blocks_)
+        if (x.first > b.nonce[x.obj]) past += x.cnt;
+    }
+    const uint64_t est = w.window + w.later + w.split, trials = lib.eng().stats.trials, items = lib.items_.load();
+    CHECK(lib.eng().groups() == std::set<uint16_t>(cs.group.begin(), cs.group.end()).size(), "groups counted");
+    // the estimate counts whole blocks: within one block per item of the truth
+    CHECK(est >= past && est - past <= (uint64_t)BM_BLOCK * items, "groups: waste estimate %llu, truth %llu",
+          (unsigned long long)est, (unsigned long long)past);
+    CHECK(w.hashed >= trials && w.hashed - trials <= (uint64_t)BM_BLOCK * items,
+          "groups: hashed estimate %llu against %llu trials", (unsigned long long)w.hashed, (unsigned long long)trials);
+    if (lib.eng().groups() == 1) CHECK(w.split == 0, "one group: split pieces");
+    fprintf(stderr, "groups: S=%zu D=%zu n=%zu exact; past the answers %llu (window %llu, later %llu, split %llu) of "
+            "%llu trials\n", S, lib.eng().groups(), cs.n, (unsigned long long)past, (unsigned long long)w.window,
+            (unsigned long long)w.later, (unsigned long long)w.split, (unsigned long long)trials);
+  }
 }
 
 // ---- scenario 4: shards of unequal speed (one 3x slower): exact, and the others not gated ----
@@ -1368,6 +1525,7 @@ int main(int argc, char** argv) {
   timed("batches", scenario_batches);
   timed("var", scenario_var);
   timed("split", scenario_split);
+  timed("groups", scenario_groups);
   timed("unequal", scenario_unequal);
   timed("top_of_space", scenario_top_of_space);
   timed("bounded", scenario_bounded);

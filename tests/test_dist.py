@@ -108,6 +108,114 @@ def test_two_rank_aggregation(tmp_path):
     assert r0['first_ih'] != r1['first_ih']
 
 
+class _FakeLib(object):
+    """A CPU stand-in for libbmpow_hip.so's calls made by bench.nonce_sharded: two devices, a no-hit sweep
+    counted exactly, batches solved by the oracle's _doSafePoW restatement, per-shard stats."""
+
+    def __init__(self, visible=2):
+        import ctypes
+        self.ctypes = ctypes
+        self.visible, self.ids, self.trials, self.batch = visible, [0], 0, None
+
+    def bmpow_device_count(self):
+        return self.visible
+
+    def bmpow_get_devices(self, arr, cap):
+        for i, d in enumerate(self.ids[:cap]):
+            arr[i] = d
+        return len(self.ids)
+
+    def bmpow_set_devices(self, arr, n):
+        self.ids = [arr[i] for i in range(n)]
+        return n
+
+    def bmpow_reset_stats(self):
+        self.trials = 0
+
+    def bmpow_search(self, ih, target, start, count, pn, pt):
+        self.trials = count  # target 0: no hit, every nonce once
+        return 0
+
+    def bmpow_get_stats(self, ref):
+        ref._obj.trials = self.trials
+
+    def bmpow_get_shard_stats(self, tr, ms, cap):
+        for i in range(len(self.ids)):
+            tr[i], ms[i] = self.trials // len(self.ids), 1.5
+        return len(self.ids)
+
+    def bmpow_device_pci_bus_id(self, dev, buf, n):
+        buf.value = b'0000:%02x:00.0' % (0x10 * (dev + 1))
+        return 0
+
+    def bmpow_batch_create(self, m, ihs, tg, start):
+        self.batch = [(int(tg[i]), ihs[64 * i:64 * i + 64]) for i in range(m)]
+        return 1
+
+    def bmpow_batch_reset(self, h, start):
+        return len(self.batch)
+
+    def bmpow_batch_step(self, h, budget):
+        from oracle import oracle
+        self.res = [oracle.safe_pow(t, ih) for t, ih in self.batch]
+        self.trials += sum(n + 256 for _, n in self.res)
+        return 0
+
+    def bmpow_batch_results(self, h, nonce, trial, done, nxt):
+        for i, (tv, n) in enumerate(self.res):
+            nonce[i], trial[i], done[i] = n, tv, 1
+        return 0
+
+    def bmpow_batch_destroy(self, h):
+        self.batch = None
+
+    def bmpow_last_error(self):
+        return b''
+
+
+def _ns_worker(rank, world, port, outdir):
+    os.environ.update({'RANK': str(rank), 'LOCAL_RANK': str(rank), 'WORLD_SIZE': str(world),
+                       'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
+    import hashlib
+    d = bench.Dist()
+    lib = _FakeLib()
+    objs = [((1 << 64) // 40, hashlib.sha512(b'ns %d' % i).digest()) for i in range(6)]
+    line = {}
+    # main()'s pattern: a barrier, rank 0 alone runs the leg, a barrier
+    d.barrier()
+    if d.rank == 0:
+        line['nonce_sharded'] = bench.nonce_sharded(lib, d.world, c3_log2=20, c4_objs=objs)
+        line['restored'] = lib.ids
+    d.barrier()
+    with open(os.path.join(outdir, 'ns%d.json' % rank), 'w') as f:
+        json.dump(line, f)
+    d.close()
+
+
+def test_nonce_sharded_field(tmp_path):
+    """SCALE runs (N > 1) carry `nonce_sharded`: rank 0, after the timed region and while the other
+    ranks wait at a barrier, runs C3 and C4 nonce-sharded over N devices in one process (the north
+    star's split, which object-sharded ranks never exercise).  gloo world_size 2 with a CPU stand-in for
+    the library: the field's shape, one entry per device with its PCI bus id, the rank's own device
+    selection restored; rank 1 carries no field."""
+    port = _free_port()
+    mp.spawn(_ns_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True)
+    r0 = json.load(open(tmp_path / 'ns0.json'))
+    assert json.load(open(tmp_path / 'ns1.json')) == {}
+    ns = r0['nonce_sharded']
+    assert r0['restored'] == [0]
+    assert ns['devices'] == [0, 1] and ns['device_groups'] == 2
+    assert set(ns) >= {'c3_ghs', 'c4_ghs', 'c4_wasted_frac', 'c3', 'c4', 'what'}
+    assert ns['c3']['trials_exact'] and ns['c3']['not_found'] and ns['c3']['nonces'] == 1 << 20
+    assert [p['pci_bus_id'] for p in ns['c4']['per_device']] == ['0000:10:00.0', '0000:20:00.0']
+    assert ns['c4']['objects'] == 6 and 0 < ns['c4']['wasted_frac'] < 1
+    # one visible device: the leg says it is a rehearsal, one bus id
+    lib = _FakeLib(visible=1)
+    one = bench.nonce_sharded(lib, 2, c3_log2=16, c4_objs=[((1 << 64) // 10, b'\x01' * 64)])
+    assert one['devices'] == [0, 0] and one['device_groups'] == 1 and 'rehearsal' in one['what']
+    assert len(one['c3']['per_device']) == 1
+
+
 def test_c2_workload_is_deterministic():
     a, da = bench.make_objects('c2', 0, 16)
     b, _ = bench.make_objects('c2', 0, 16)

@@ -44,9 +44,52 @@ def test_header_declares_the_boundary():
               'bmpow_service_stop', 'bmpow_service_destroy', 'bmpow_set_device_count', 'bmpow_trials_len',
               'bmpow_search_len', 'bmpow_min_trial_var', 'bmpow_batch_add_var', 'bmpow_service_submit_var',
               'bmpow_get_shard_rates', 'bmpow_get_shard_stats', 'bmpow_get_thread_info', 'bmpow_set_shard_throttle',
-              'bmpow_set_run_split', 'bmpow_get_run_pieces', 'bmpow_device_pci_bus_id']:
+              'bmpow_set_run_split', 'bmpow_get_run_pieces', 'bmpow_device_pci_bus_id', 'bmpow_set_engine_split',
+              'bmpow_atexit']:
         assert s in syms
-    assert len(syms) == 60
+    assert len(syms) == 62
+
+
+def test_exit_hook_registered_and_final(monkeypatch, tmp_path):
+    """The library is released at process exit before the HIP runtime's own exit handlers (round 5's
+    traced runs with CU-masked streams alive segfaulted in them): _lib.get() registers bmpow_atexit with
+    Python's atexit once, and bmpow_atexit is final -- a fresh copy of the library refuses to initialise
+    after it (E_STATE), so no stream can be created after the teardown.  No GPU needed."""
+    import atexit
+    import shutil
+    calls = []
+
+    class Fake(object):
+        def bmpow_init(self):
+            return 1
+
+        def bmpow_atexit(self):
+            calls.append('atexit')
+    fake = Fake()
+    registered = []
+    monkeypatch.setattr(_lib, 'load', lambda path=None: fake)
+    monkeypatch.setattr(_lib, '_lib', None)
+    monkeypatch.setattr(_lib, '_exit_hooked', False)
+    monkeypatch.setattr(atexit, 'register', lambda fn, *a: registered.append((fn, a)))
+    assert _lib.get() is fake
+    assert registered == [(_lib._at_exit, (fake,))]
+    monkeypatch.setattr(_lib, '_lib', None)
+    _lib.get()
+    assert len(registered) == 1  # once per process
+    _lib._at_exit(fake)
+    assert calls == ['atexit']
+    # the real export: final, and safe with nothing initialised
+    path = _lib.lib_path()
+    if not os.path.exists(path):
+        pytest.skip('library not built')
+    copy = tmp_path / 'libbmpow_copy.so'
+    shutil.copy(path, copy)
+    lib = ctypes.CDLL(str(copy))
+    lib.bmpow_atexit()
+    lib.bmpow_atexit()  # idempotent
+    assert lib.bmpow_init() == _lib.E_STATE
+    lib.bmpow_last_error.restype = ctypes.c_char_p
+    assert b'exiting' in lib.bmpow_last_error()
 
 
 def test_library_exports_every_declared_symbol(rawlib):
