@@ -16,8 +16,10 @@
  * Return codes: >= 0 success (meaning per function), < 0 error (BMPOW_E_*);
  * bmpow_last_error() describes the last error of the calling thread.
  *
- * Thread safety: all entry points may be called from any thread; searches are serialised
- * by an internal mutex (one search in flight per process), the GIL is not needed.
+ * Thread safety: all entry points may be called from any thread; they are serialised by an
+ * internal first-come first-served mutex, the GIL is not needed.  A 64-byte bmpow_search holds a
+ * second mutex of its own for its whole call (one such search at a time) and gives the first up while
+ * it waits for its windows, so a batch session or service steps between them.
  */
 #ifndef BMPOW_H
 #define BMPOW_H
@@ -379,6 +381,10 @@ typedef struct bmpow_stats {
     uint64_t past_later;      /* unsplit windows starting above the answer (the lookahead queued behind) */
     uint64_t past_split;      /* pieces of windows split over device groups: nonces above the answer */
     uint64_t engine_hashed_est; /* every priced item's estimated hashed nonces (compare with trials) */
+    /* streams the library keeps for the life of the process (current counts, not reset): CU-masked
+       streams of the forced-split rehearsal (bmpow_set_run_split) and run()'s priority streams */
+    uint64_t masked_streams;
+    uint64_t run_streams;
 } bmpow_stats;
 
 BMPOW_API int bmpow_get_stats(bmpow_stats *out);

@@ -58,7 +58,8 @@ class BmpowStats(ctypes.Structure):
                 ('cut_trials', ctypes.c_uint64),
                 ('one_wait_spin_ms', ctypes.c_double), ('one_wait_sleep_ms', ctypes.c_double),
                 ('past_window', ctypes.c_uint64), ('past_later', ctypes.c_uint64),
-                ('past_split', ctypes.c_uint64), ('engine_hashed_est', ctypes.c_uint64)]
+                ('past_split', ctypes.c_uint64), ('engine_hashed_est', ctypes.c_uint64),
+                ('masked_streams', ctypes.c_uint64), ('run_streams', ctypes.c_uint64)]
 
 
 class BmpowAddress(ctypes.Structure):

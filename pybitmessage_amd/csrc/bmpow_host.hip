@@ -193,6 +193,9 @@ struct Shard {
   size_t parts_cap = 0;
   // the engine's launches (searches)
   LaunchBuf lb[2];
+  // launch buffers outgrown while the stepper held the engine's mutex: freed by the same stepper after
+  // its next wait, without the mutex (hipFree / hipHostFree wait for the device)
+  std::vector<void*> retired_dev, retired_host;
   std::vector<UpBuf> up;
   double t_prev_done = 0;  // steady-clock ms when the stepper last saw a launch complete
   // address search: the fixed-base comb tables (v * 2^(W i) * G) for W = 16 ([0]) and 24 ([1]),
@@ -263,15 +266,18 @@ int ensure_items(Shard& s, size_t n) {
   return 0;
 }
 
-// Grow an engine launch buffer to n items (only ever called for a buffer not in flight).
+// Grow an engine launch buffer to n items (only ever called for a buffer not in flight).  Called from
+// engine_launch, under the engine's mutex: the old buffers are not freed here -- hipFree and hipHostFree
+// wait for the whole device, every shard's launches in flight included -- but retired,
+// and free_retired releases them from the stepper's wait, outside the mutex.
 int ensure_launch_buf(Shard& s, LaunchBuf& lb, size_t n) {
   if (n <= lb.cap) return 0;
   const size_t cap = std::max<size_t>({n, 2 * lb.cap, 1024});
   HIPTRY(hipSetDevice(s.dev));
-  if (lb.h_items) HIPTRY(hipHostFree(lb.h_items));
-  if (lb.d_items) HIPTRY(hipFree(lb.d_items));
-  if (lb.h_res) HIPTRY(hipHostFree(lb.h_res));
-  if (lb.d_res) HIPTRY(hipFree(lb.d_res));
+  if (lb.h_items) s.retired_host.push_back(lb.h_items);
+  if (lb.d_items) s.retired_dev.push_back(lb.d_items);
+  if (lb.h_res) s.retired_host.push_back(lb.h_res);
+  if (lb.d_res) s.retired_dev.push_back(lb.d_res);
   lb.h_items = nullptr;
   lb.d_items = nullptr;
   lb.h_res = nullptr;
@@ -285,10 +291,19 @@ int ensure_launch_buf(Shard& s, LaunchBuf& lb, size_t n) {
   return 0;
 }
 
+// Free the launch buffers the shard's stepper outgrew (ensure_launch_buf); none is in flight.
+void free_retired(Shard& s) {
+  for (void* p : s.retired_dev) (void)hipFree(p);
+  for (void* p : s.retired_host) (void)hipHostFree(p);
+  s.retired_dev.clear();
+  s.retired_host.clear();
+}
+
 void free_shard(Shard& s) {
   if (s.dev < 0) return;
   (void)hipSetDevice(s.dev);
   if (s.stream) (void)hipStreamSynchronize(s.stream);
+  free_retired(s);
   if (s.d_items) (void)hipFree(s.d_items);
   if (s.d_res) (void)hipFree(s.d_res);
   if (s.h_items) (void)hipHostFree(s.h_items);
@@ -795,6 +810,7 @@ int engine_wait(bmsched::Launch& L, std::string& err) {
   sh.t_prev_done = now_ms();
   const size_t n = L.plan.items[0].size();
   L.res.assign(lb.h_res, lb.h_res + n);
+  if (!sh.retired_dev.empty() || !sh.retired_host.empty()) free_retired(sh);
   L.trials = lb.h_res[n].nonce;  // the trials counter rides home after the results
   L.ms = ms;
   return 0;
@@ -2709,6 +2725,8 @@ int bmpow_get_stats(bmpow_stats* out) {
   std::lock_guard<FairMutex> lk(g_mu);
   if (!out) return BMPOW_E_ARG;
   *out = g_stats;
+  out->masked_streams = g_masked.size();
+  out->run_streams = g_run_streams.size();
   if (g_engine) {  // the searches: the engine's launches
     std::lock_guard<std::mutex> el(g_engine->mu);
     const bmsched::EngineStats& es = g_engine->stats;
