@@ -995,9 +995,15 @@ def main():
     ap.add_argument('--throttle', default=None,
                     help='--devices A/B: "shard:ms" -- that shard\'s stepper sleeps ms before each launch')
     ap.add_argument('--cpu-baseline-worker', action='store_true', help=argparse.SUPPRESS)
+    ap.add_argument('--nonce-sharded-child', type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.cpu_baseline_worker:
         cpu_baseline_worker(args.cpu_seconds, args.cpu_threads, args.cpu_mode)
+        return
+    if args.nonce_sharded_child:
+        os.environ['BMPOW_DEVICES'] = '0'
+        from pybitmessage_amd import _lib
+        print(json.dumps(nonce_sharded(_lib.get(), args.nonce_sharded_child, args.share_device)), flush=True)
         return
 
     dist = Dist()
@@ -1060,13 +1066,11 @@ def main():
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu_baseline:
         line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_threads or None)
     if dist.world > 1 and not args.devices and not args.no_nonce_sharded and args.config in ('c2', 'c4', 'c5'):
-        # the nonce split over the node's GPUs (C3, C4), outside the timed region: rank 0 alone
+        # the nonce split over the node's GPUs (C3, C4), outside the timed region: rank 0 alone, in a
+        # child process under a time limit, so a failure there costs this line nothing but the field
         dist.barrier()
         if dist.rank == 0:
-            try:
-                line['nonce_sharded'] = nonce_sharded(lib, dist.world, args.share_device)
-            except Exception as e:  # reported in the line; the scaling value above stands
-                line['nonce_sharded'] = {'error': repr(e)}
+            line['nonce_sharded'] = run_nonce_sharded_child(dist.world, args.share_device)
         dist.barrier()
     if dist.rank == 0:
         print(json.dumps(line), flush=True)
@@ -1158,6 +1162,24 @@ def nonce_sharded(lib, n, share=False, c3_log2=36, c4_objs=None):
     out['c3_ghs'], out['c4_ghs'] = out['c3']['ghs'], out['c4']['ghs']
     out['c4_wasted_frac'] = out['c4']['wasted_frac']
     return out
+
+
+def run_nonce_sharded_child(n, share=False, timeout=600, argv=None):
+    """nonce_sharded over n devices in a child process (`bench.py --nonce-sharded-child N`), bounded by
+    `timeout` seconds: its JSON, or {'error': ...} when it fails, times out or prints none."""
+    argv = argv or ([sys.executable, os.path.abspath(__file__), '--nonce-sharded-child', str(n)] +
+                    (['--share-device'] if share else []))
+    env = dict(os.environ)
+    for k in ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)  # the child is a single process
+    try:
+        r = subprocess.run(argv, capture_output=True, text=True, timeout=timeout, env=env)
+    except subprocess.TimeoutExpired:
+        return {'error': 'timed out after %d s' % timeout}
+    lines = [x for x in r.stdout.splitlines() if x.startswith('{')]
+    if r.returncode != 0 or not lines:
+        return {'error': 'exit status %d' % r.returncode, 'stderr': r.stderr[-800:]}
+    return json.loads(lines[-1])
 
 
 def device_pci_bus_id(lib, shard=0):

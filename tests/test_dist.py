@@ -272,3 +272,15 @@ def test_rank_device_selection():
     assert bench.rank_device(types.SimpleNamespace(rank=0, local_rank=0), visible=1) == 0
     with pytest.raises(SystemExit):
         bench.rank_device(d, visible=2)
+
+
+def test_nonce_sharded_child_wrapper():
+    """rank 0 runs the nonce-sharded leg in a child process under a time limit: its JSON comes back; a
+    child that fails, prints nothing or overruns is an `error` entry, never a lost scaling line."""
+    import sys
+    ok = bench.run_nonce_sharded_child(2, argv=[sys.executable, '-c', 'print("noise"); print(\'{"c3_ghs": 1.5}\')'])
+    assert ok == {'c3_ghs': 1.5}
+    bad = bench.run_nonce_sharded_child(2, argv=[sys.executable, '-c', 'import sys; sys.exit(3)'])
+    assert bad['error'] == 'exit status 3'
+    slow = bench.run_nonce_sharded_child(2, timeout=1, argv=[sys.executable, '-c', 'import time; time.sleep(5)'])
+    assert 'timed out' in slow['error']
