@@ -1092,13 +1092,14 @@ def per_device(lib, ids):
     return out
 
 
-def nonce_sharded(lib, n, share=False, c3_log2=36, c4_objs=None):
+def nonce_sharded(lib, n, share=False, c3_log2=38, c4_objs=None):
     """The north star's nonce split on a multi-GPU node (BASELINE.json C3 and C4 over 1/2/4/8 GPUs),
     measured in ONE process over n devices -- the SCALE run's ranks each drive one GPU with object
     sharding, which never splits an object.  Run by rank 0 after the timed region while the other ranks
     wait at a barrier (their GPUs idle):
       * C3: a run() sweep of 2^c3_log2 nonces with no hit (target 0), one interleaved piece per device
-        sharing the cross-device bound: every nonce hashed exactly once;
+        sharing the cross-device bound: every nonce hashed exactly once (2^38: BASELINE.json's C3 size,
+        ~5 s over 8 GPUs, ~41 s when a one-GPU rehearsal puts every piece on one device);
       * C4: the 64 objects of 20x difficulty as one batch on the engine, one stepper per device (object
         mode, then windows split over the devices at the tail), answers re-hashed with hashlib.
     Falls back to n shards of device 0 when fewer than n devices are visible (then a rehearsal: the
