@@ -110,6 +110,19 @@ class COracle(object):
             return t.value, n.value
         return None
 
+    def search_many(self, jobs, threads=None):
+        """``search`` of every (target, ih) in jobs, in order: the same sequential search, the objects
+        spread over a pool of threads (ctypes releases the GIL for each call).  Threads default to the
+        CPUs this process may use, at most 16 (the GPU box's quota)."""
+        from concurrent.futures import ThreadPoolExecutor
+        jobs = list(jobs)
+        if threads is None:
+            threads = max(1, min(16, len(os.sched_getaffinity(0))))
+        if threads <= 1 or len(jobs) <= 1:
+            return [self.search(ih, t) for t, ih in jobs]
+        with ThreadPoolExecutor(threads) as ex:
+            return list(ex.map(lambda j: self.search(j[1], j[0]), jobs))
+
     def min_trial(self, ih, start, count):
         """(min trial over [start, start+count), first nonce reaching it); (U64_MAX, start)
         for an empty range."""

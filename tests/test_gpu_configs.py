@@ -135,7 +135,7 @@ def test_c5_default_difficulty_slice(gpulib, shards, coracle):
     bench.make_objects('c5', 0) with steps of 2^26 trials, so a step's 8,192 chunks are fewer than
     the pending objects -- the 100k flood's regime, where each object spans thousands of chunks
     over many steps (round 1's lost-work-item bug lived there).  Every answer proven minimal by the
-    min-trial probe; 20 of them (seeded draw) also solved by the C oracle."""
+    min-trial probe; 8 of them (seeded draw) also solved by the C oracle."""
     shards([0])
     gpulib.bmpow_set_step_trials(1 << 26)
     objs, _ = bench.make_objects('c5', 0)
@@ -147,7 +147,7 @@ def test_c5_default_difficulty_slice(gpulib, shards, coracle):
     hashed = assert_exact_first_nonces(gpulib, objs, res)
     assert hashed > 1e11
     rng = random.Random(55)
-    oracle_sample(coracle, objs, res, rng.sample(range(len(objs)), 20))
+    oracle_sample(coracle, objs, res, rng.sample(range(len(objs)), 8))
 
 
 @pytest.mark.parametrize('nshards,split', [(1, False), (8, False), (4, True), (8, True)])

@@ -438,9 +438,9 @@ def test_serial_runs_beside_a_running_service(gpulib, shards, run_split, coracle
                 x.join(120)
         finally:
             svc.stop(30)
-        assert [list(r) for r in res] == [list(coracle.search(ih, t)) for t, ih in batch], layout
+        assert [list(r) for r in res] == [list(r) for r in coracle.search_many(batch)], layout
         for k in range(2):
-            assert got[k] == [list(coracle.search(ih, t)) for t, ih in serial[k]], (layout, k)
+            assert got[k] == [list(r) for r in coracle.search_many(serial[k])], (layout, k)
 
 
 def test_run_is_not_starved_by_a_busy_service(gpulib, shards, coracle):

@@ -78,7 +78,7 @@ def test_random_batch_vs_c_oracle(gpulib, coracle):
     for _ in range(300):
         ih = rng.randbytes(64)
         objs.append((U64 // rng.choice([1, 2, 7, 100, 1000, 30000, 200000]), ih))
-    want = [list(coracle.search(ih, t)) for t, ih in objs]
+    want = [list(r) for r in coracle.search_many(objs)]
     assert proofofwork.run_batch(objs) == want
 
 
@@ -92,7 +92,7 @@ def test_shard_layouts_and_step_sizes(gpulib, shards, coracle, golden, layout, s
     gpulib.bmpow_set_step_trials(step)
     rng = random.Random(len(layout) * 7 + step)
     objs = [(U64 // rng.choice([3, 900, 40000]), rng.randbytes(64)) for _ in range(40)]
-    want = [list(coracle.search(ih, t)) for t, ih in objs]
+    want = [list(r) for r in coracle.search_many(objs)]
     assert proofofwork.run_batch(objs) == want
     for k in golden('first_nonce_kats.json')['kats'][:10]:
         assert gpu_search(gpulib, bytes.fromhex(k['ih']), k['target']) == (k['trial'], k['nonce'])
@@ -106,7 +106,7 @@ def test_many_objects_per_step(gpulib, shards, coracle, layout, step):
     gpulib.bmpow_set_step_trials(step)
     rng = random.Random(4242 + len(layout))
     objs = [(U64 // rng.choice([2, 40, 300, 9000]), rng.randbytes(64)) for _ in range(6000)]
-    want = [list(coracle.search(ih, t)) for t, ih in objs]
+    want = [list(r) for r in coracle.search_many(objs)]
     assert proofofwork.run_batch(objs) == want
 
 
@@ -323,7 +323,7 @@ def test_concurrent_callers_are_serialised_and_exact(gpulib, coracle):
     with ThreadPoolExecutor(6) as ex:
         got = list(ex.map(lambda j: proofofwork.run(*j), jobs))
         batches = list(ex.map(proofofwork.run_batch, [jobs[i::3] for i in range(3)]))
-    assert got == [list(coracle.search(ih, t)) for t, ih in jobs]
+    assert got == [list(r) for r in coracle.search_many(jobs)]
     for i in range(3):
         assert batches[i] == got[i::3]
 
@@ -408,8 +408,8 @@ def test_session_add_and_take_done(gpulib, coracle):
         gpulib.bmpow_batch_destroy(h)
         gpulib.bmpow_set_step_trials(0)  # the library's default
     assert len(got) == serial
-    for (t, ih), res in got.values():
-        assert res == coracle.search(ih, t)
+    objs = [o for o, _ in got.values()]
+    assert [res for _, res in got.values()] == coracle.search_many(objs)
 
 
 def test_native_service_producers_cancel_abort(gpulib, coracle):
@@ -465,8 +465,9 @@ def test_native_service_producers_cancel_abort(gpulib, coracle):
         for t in ths:
             t.join()
         assert len(got) == len(jobs) and gpulib.bmpow_service_outstanding(s) == 0
-        for t, (target, ih) in jobs.items():
-            assert got[t] == coracle.search(ih, target)
+        want = coracle.search_many(list(jobs.values()))
+        for t, w in zip(jobs, want):
+            assert got[t] == w
         # cancel drops in-flight work (a target-0 object never finishes) and the service goes on
         submit([(0, bytes(64))] * 3)
         time.sleep(0.2)

@@ -70,6 +70,15 @@ def test_first_nonce_kats_c_oracle(golden, coracle):
         assert coracle.search(ih, k['target']) == (k['trial'], k['nonce']), k['note']
 
 
+def test_search_many_is_search_in_order(golden, coracle):
+    """search_many (the GPU tests' checker for many objects) = search per object, in input order."""
+    kats = [k for k in golden('first_nonce_kats.json')['kats'] if k['nonce'] <= 200_000]
+    jobs = [(k['target'], bytes.fromhex(k['ih'])) for k in kats]
+    assert len(jobs) >= 8
+    assert coracle.search_many(jobs, threads=4) == [(k['trial'], k['nonce']) for k in kats]
+    assert coracle.search_many(jobs[:3], threads=1) == [coracle.search(ih, t) for t, ih in jobs[:3]]
+
+
 def test_first_nonce_slow_kats_mt(golden, coracle):
     for k in golden('first_nonce_kats.json')['kats']:
         if k['nonce'] <= 2_000_000 or k['nonce'] > 50_000_000:
