@@ -82,6 +82,43 @@ def test_random_batch_vs_c_oracle(gpulib, coracle):
     assert proofofwork.run_batch(objs) == want
 
 
+@pytest.mark.parametrize('layout,split', [([0], False), ([0, 0, 0], False), ([0, 0, 0], True)])
+def test_duplicate_objects_and_one_hash_many_targets(gpulib, shards, engine_split, coracle, layout, split):
+    """A batch may hold the same object more than once (the same payload queued twice) and one
+    initialHash under several targets (a payload re-sent at another difficulty): each entry is solved on
+    its own to the same `_doSafePoW` answer (src/proofofwork.py:100-111), whatever the slots, shards and
+    cross-shard bound slots the engine gives them.  Layouts: one shard; three shards of this device (one
+    device group: no object on two shards); three shards as separate device groups (every tail window
+    split into pieces sharing the cross-shard bound, the multi-device path rehearsed)."""
+    shards(layout)
+    engine_split(split)
+    gpulib.bmpow_set_step_trials(1 << 22)
+    rng = random.Random(31 + len(layout) + split)
+    ih = rng.randbytes(64)
+    dup = (U64 // 60000, rng.randbytes(64))
+    objs = [dup] * 6 + [(U64 // d, ih) for d in (1, 2, 50, 3000, 70000, 3000, 1)] + [dup]
+    objs += [(U64 // rng.choice([20, 4000, 90000]), rng.randbytes(64)) for _ in range(10)] + [dup] * 3
+    rng.shuffle(objs)
+    want = [list(r) for r in coracle.search_many(objs)]
+    assert proofofwork.run_batch(objs) == want
+    # the same entries through the library's service, submitted by two producers at once
+    from pybitmessage_amd import worker
+    svc = worker.PowService().start()
+    try:
+        half = len(objs) // 2
+        futs = []
+        th = [threading.Thread(target=lambda part: futs.extend(svc.submit_many(part)), args=(p,))
+              for p in (objs[:half], objs[half:])]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(60)
+        got = sorted([list(f.result(timeout=120)) for f in futs])
+    finally:
+        svc.stop(30)
+    assert got == sorted(want)
+
+
 @pytest.mark.parametrize('layout,step', [([0], 1 << 28), ([0], 8192 * 3), ([0, 0], 1 << 20),
                                          ([0, 0, 0], 8192 * 5), ([0, 0], 3001), ([0], (1 << 26) + 777)])
 def test_shard_layouts_and_step_sizes(gpulib, shards, coracle, golden, layout, step):
